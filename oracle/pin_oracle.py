@@ -1,0 +1,530 @@
+"""CPU oracle: a numpy restatement of PIN-SLAM's neural-point query hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in ``pin_slam_amd`` may import this module;
+only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg use it, and only as the checker / the timed CPU baseline.
+
+Pinned against the reference: ``tests/test_oracle_golden.py`` checks every
+function here against ``tests/golden/*.npz``, which ``tests/golden/gen_golden.py``
+produced by running the reference code itself (torch CPU) in the build container.
+
+Semantics follow the reference file:line cited on each function.  Arithmetic is
+float32 where the reference's discrete decisions depend on it (voxel floor, the
+squared distance that gates validity and the k-NN order, ReLU masks) and the
+same op order as the reference where practical; reductions may differ in the
+last bits (the tests state their tolerances).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+
+PRIMES = np.array([73856093, 19349669, 83492791], dtype=np.int64)  # model/neural_points.py:69
+IDW_EPS = 1e-15                                                    # model/neural_points.py:618
+INVALID_DIST2 = 9e3                                                # model/neural_points.py:561
+
+
+# ---------------------------------------------------------------- neighbourhood / hash
+def neighbor_offsets(num_nei_cells: int, search_alpha: float) -> np.ndarray:
+    """model/neural_points.py:430-453: integer offsets inside the (c+alpha) sphere, meshgrid 'ij' order."""
+    d = np.arange(-num_nei_cells, num_nei_cells + 1, dtype=np.int64)
+    gx, gy, gz = np.meshgrid(d, d, d, indexing="ij")
+    dx = np.stack([gx, gy, gz], -1).reshape(-1, 3)
+    dx2 = (dx ** 2).sum(-1)
+    return dx[dx2 < (num_nei_cells + search_alpha) ** 2]
+
+
+def max_valid_dist2(num_nei_cells: int, resolution: float) -> float:
+    """model/neural_points.py:457."""
+    return 3 * ((num_nei_cells + 1) * resolution) ** 2
+
+
+def voxel_coords(points: np.ndarray, resolution: float) -> np.ndarray:
+    """model/neural_points.py:465 / :214: f32 true division, floor, to int64."""
+    res = np.float32(resolution)
+    return np.floor(points.astype(np.float32) / res).astype(np.int64)
+
+
+def hash_slots(cells: np.ndarray, buffer_size: int) -> np.ndarray:
+    """model/neural_points.py:472 + the index wrap of :476: fmod keeps the dividend's
+    sign; a negative remainder r indexes slot B + r (Python negative indexing)."""
+    h = np.fmod((cells * PRIMES).sum(-1), np.int64(buffer_size))
+    return np.where(h < 0, h + buffer_size, h)
+
+
+# ---------------------------------------------------------------- map state
+@dataclasses.dataclass
+class MapState:
+    """Plain-array snapshot of the NeuralPoints tensors the query path reads
+    (model/neural_points.py:73-95, :293-311)."""
+    resolution: float
+    buffer_size: int
+    table: np.ndarray                 # [B] int64, -1 = empty
+    points: np.ndarray                # [M,3] f32
+    orientations: np.ndarray          # [M,4] f32 (w,x,y,z)
+    geo_features: np.ndarray          # [M+1,F] f32 (last row = padding)
+    ts_create: np.ndarray             # [M] int64
+    ts_update: np.ndarray             # [M] int64
+    certainties: np.ndarray           # [M] f32
+    travel_dist: np.ndarray           # [T] f32
+    cur_ts: int
+    diff_travel_dist_local: float
+    local_mask: np.ndarray            # [M+1] bool
+    global2local: np.ndarray          # [M+1] int64
+    local_points: np.ndarray
+    local_orientations: np.ndarray
+    local_features: np.ndarray        # [L+1,F]
+    local_certainties: np.ndarray
+    local_ts_update: np.ndarray
+    after_pgo: bool = False
+
+    def copy(self) -> "MapState":
+        return dataclasses.replace(self, **{f.name: (getattr(self, f.name).copy()
+                                                      if isinstance(getattr(self, f.name), np.ndarray)
+                                                      else getattr(self, f.name))
+                                             for f in dataclasses.fields(self)})
+
+
+def table_from_slots(buffer_size: int, slots: np.ndarray, vals: np.ndarray) -> np.ndarray:
+    t = np.full(int(buffer_size), -1, dtype=np.int64)
+    t[slots] = vals
+    return t
+
+
+def build_table(points: np.ndarray, resolution: float, buffer_size: int) -> np.ndarray:
+    """Hash every point into a fresh table, last writer wins (neural_points.py:420-422)."""
+    t = np.full(int(buffer_size), -1, dtype=np.int64)
+    slots = hash_slots(voxel_coords(points, resolution), buffer_size)
+    t[slots] = np.arange(points.shape[0], dtype=np.int64)
+    return t
+
+
+def reset_local_map(st: MapState, sensor_position: np.ndarray, cur_ts: int, local_map_radius: float,
+                    use_mid_ts: bool = False) -> None:
+    """model/neural_points.py:272-311 (travel-distance form)."""
+    st.cur_ts = int(cur_ts)
+    d2 = ((st.points - sensor_position.astype(np.float32)) ** 2).sum(-1)
+    ts_used = (st.ts_create + st.ts_update) // 2 if use_mid_ts else st.ts_create
+    dtd = np.abs(st.travel_dist[cur_ts] - st.travel_dist[ts_used])
+    mask = (d2 < local_map_radius ** 2) & (dtd < st.diff_travel_dist_local)
+    st.local_points = st.points[mask]
+    st.local_orientations = st.orientations[mask]
+    st.local_certainties = st.certainties[mask]
+    st.local_ts_update = st.ts_update[mask]
+    mask = np.concatenate([mask, [True]])
+    st.local_mask = mask
+    # reference quirk (neural_points.py:301): non-local points map to local index 1
+    g2l = np.full(mask.shape[0], 1, dtype=np.int64)
+    li = np.nonzero(mask)[0]
+    g2l[li] = np.arange(li.shape[0])
+    g2l[-1] = -1
+    st.global2local = g2l
+    st.local_features = st.geo_features[mask].copy()
+
+
+def assign_local_to_global(st: MapState) -> None:
+    """model/neural_points.py:315-324."""
+    m = st.local_mask
+    st.points[m[:-1]] = st.local_points
+    st.orientations[m[:-1]] = st.local_orientations
+    st.geo_features[m] = st.local_features
+    st.certainties[m[:-1]] = st.local_certainties
+    st.ts_update[m[:-1]] = st.local_ts_update
+
+
+# ---------------------------------------------------------------- search
+def radius_neighborhood_search(st: MapState, q: np.ndarray, neighbor_dx: np.ndarray, maxd2: float,
+                               time_filtering: bool = False):
+    """model/neural_points.py:459-509 -> (dist2 [N,Kc] f32, idx [N,Kc] int64 global)."""
+    q = q.astype(np.float32)
+    g = voxel_coords(q, st.resolution)
+    cells = g[:, None, :] + neighbor_dx[None]
+    idx = st.table[hash_slots(cells, st.buffer_size)].copy()
+    if time_filtering:
+        dtd = np.abs(st.travel_dist[st.cur_ts] - st.travel_dist[st.ts_create[idx]])
+        idx[~(dtd < st.diff_travel_dist_local)] = -1
+    diff = st.points[idx] - q[:, None, :]
+    dist2 = (diff * diff).sum(-1, dtype=np.float32)
+    dist2[idx == -1] = np.float32(maxd2)
+    idx[dist2 > np.float32(maxd2)] = -1
+    return dist2, idx
+
+
+def quat_rotate_passive(quat: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """utils/tools.py:316-323: p' = q* p q (rotation by the conjugate)."""
+    w = quat[..., :1]
+    u = -quat[..., 1:]
+    t = 2.0 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)
+
+
+def quat_to_rotmat(quat: np.ndarray) -> np.ndarray:
+    """Active rotation matrix R(q); the passive form above is R(q)^T v."""
+    w, x, y, z = [quat[..., i].astype(np.float64) for i in range(4)]
+    R = np.stack([
+        1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], -1)
+    return R.reshape(quat.shape[:-1] + (3, 3))
+
+
+@dataclasses.dataclass
+class Query:
+    feat: np.ndarray          # [N,F+3] (weighted_first) or [N,k,F+3]
+    weights: np.ndarray       # [N,k] f32
+    nn_counts: np.ndarray     # [N] int64
+    certainty: np.ndarray     # [N] f32
+    idx: np.ndarray           # [N,k] int64 (local or global index, -1 invalid)
+    dist2: np.ndarray         # [N,k] f32
+    vec: np.ndarray           # [N,k,3] f32 (after optional rotation, zero for invalid)
+    nbr_points: np.ndarray    # [N,k,3] f32 neighbour positions read through the (local) index
+    nbr_gpoints: np.ndarray   # [N,k,3] f32 positions of the GLOBAL candidate the distance came from
+    nbr_quat: np.ndarray      # [N,k,4]
+    nbr_feat: np.ndarray      # [N,k,F]
+
+
+def query_feature(st: MapState, q: np.ndarray, nn_k: int, neighbor_dx: np.ndarray, maxd2: float,
+                  weighted_first: bool = True, training_mode: bool = False, query_locally: bool = True,
+                  query_ts: Optional[np.ndarray] = None, time_filtering: bool = True) -> Query:
+    """model/neural_points.py:528-674.  Training-mode side effects update ``st`` in place."""
+    q = q.astype(np.float32)
+    N = q.shape[0]
+    d2, idx = radius_neighborhood_search(st, q, neighbor_dx, maxd2, time_filtering and query_locally)
+    gidx = idx
+    if query_locally:
+        # NB neural_points.py:301 builds global2local with full_like(<bool mask>, -1).long(),
+        # i.e. every non-local point maps to local index 1 (not -1).  The fixture arrays carry
+        # that exact table; distances (and their gradient) still come from the global point.
+        idx = st.global2local[idx]
+    nn_counts = (idx >= 0).sum(-1).astype(np.int64)
+    d2 = d2.copy()
+    d2[idx == -1] = np.float32(INVALID_DIST2)
+    order = np.argsort(d2, axis=1, kind="stable")
+    d2 = np.take_along_axis(d2, order, 1)[:, :nn_k]
+    idx = np.take_along_axis(idx, order, 1)[:, :nn_k]
+    gidx = np.take_along_axis(gidx, order, 1)[:, :nn_k]
+    nbr_gpts = st.points[gidx]
+    valid = idx >= 0
+    if query_locally:
+        feats_src, pts_src, quat_src, cert_src = (st.local_features, st.local_points,
+                                                  st.local_orientations, st.local_certainties)
+    else:
+        feats_src, pts_src, quat_src, cert_src = (st.geo_features, st.points, st.orientations, st.certainties)
+    F = feats_src.shape[1]
+    nbr_feat = np.zeros((N, nn_k, F), np.float32)
+    nbr_feat[valid] = feats_src[idx[valid]]
+    nbr_pts = pts_src[idx]
+    nbr_quat = quat_src[idx]
+    certainty = cert_src[idx].copy()
+    vec = (q[:, None, :] - nbr_pts).astype(np.float32)
+    if st.after_pgo:
+        vec = quat_rotate_passive(nbr_quat, vec).astype(np.float32)
+    vec[~valid] = 0.0
+    fv = np.concatenate([nbr_feat, vec], -1)
+    w = (np.float32(1.0) / (d2 + np.float32(IDW_EPS))).astype(np.float32)
+    w[~valid] = 0.0
+    w[nn_counts == 0] = np.float32(IDW_EPS)
+    w = (w / w.sum(1, keepdims=True, dtype=np.float32)).astype(np.float32)
+    w[~valid] = 0.0
+    if training_mode:
+        sidx = idx.copy()
+        sidx[~valid] = 0
+        if query_locally:
+            np.add.at(st.local_certainties, sidx.ravel(), w.ravel())
+            if query_ts is not None:
+                tsr = np.repeat(np.asarray(query_ts, np.int64)[:, None], nn_k, 1)
+                tsr[~valid] = 0
+                np.maximum.at(st.local_ts_update, sidx.ravel(), tsr.ravel())
+        else:
+            np.add.at(st.certainties, sidx.ravel(), w.ravel())
+    certainty[~valid] = 0.0
+    qc = (certainty * w).sum(1, dtype=np.float32)
+    if weighted_first:
+        fv = (fv * w[..., None]).sum(1, dtype=np.float32)
+    return Query(fv, w, nn_counts, qc, idx, d2, vec, nbr_pts, nbr_gpts, nbr_quat, nbr_feat)
+
+
+# ---------------------------------------------------------------- decoder + gradient
+@dataclasses.dataclass
+class MLP:
+    """model/decoder.py:16-57 with hidden_level=1: Linear(F+3,H)+ReLU, Linear(H,1), * sdf_scale."""
+    W1: np.ndarray  # [H, D]
+    b1: np.ndarray  # [H]
+    W2: np.ndarray  # [1, H]
+    b2: np.ndarray  # [1]
+    sdf_scale: float
+
+    def forward(self, x: np.ndarray):
+        """model/decoder.py:66-88. Returns (sdf [...], pre-activation [..., H])."""
+        pre = (x.astype(np.float32) @ self.W1.T.astype(np.float32) + self.b1).astype(np.float32)
+        h = np.maximum(pre, 0)
+        out = (h @ self.W2.T + self.b2)[..., 0].astype(np.float32)
+        return (out * np.float32(self.sdf_scale)).astype(np.float32), pre
+
+    def grad_x(self, pre: np.ndarray) -> np.ndarray:
+        """d sdf / d x for each row: s * W1^T (w2 * 1[pre > 0]) (ReLU'(0) = 0)."""
+        gh = (pre > 0) * self.W2[0].astype(np.float64)
+        return (gh @ self.W1.astype(np.float64)) * float(self.sdf_scale)
+
+
+def _weight_grads(qry: Query, q: np.ndarray):
+    """du_k/dq = -2 u_k^2 (q - p_k) for valid k; returns (u, S, du) in float64."""
+    valid = qry.idx >= 0
+    d = qry.dist2.astype(np.float64)
+    u = np.where(valid, 1.0 / (d + IDW_EPS), 0.0)
+    S = u.sum(1)
+    diff = q.astype(np.float64)[:, None, :] - qry.nbr_gpoints.astype(np.float64)
+    du = (-2.0 * u * u)[..., None] * diff
+    du[~valid] = 0.0
+    return u, S, du
+
+
+def _vec_jacobian_t(qry: Query, st_after_pgo: bool, gv: np.ndarray) -> np.ndarray:
+    """(d vec_k / d q)^T gv : identity, or R(q_k) gv after pgo (vec = R^T (q - p))."""
+    if not st_after_pgo:
+        return gv
+    R = quat_to_rotmat(qry.nbr_quat)
+    return np.einsum("...ij,...j->...i", R, gv)
+
+
+def sdf_and_grad(st: MapState, mlp: MLP, q: np.ndarray, nn_k: int, neighbor_dx: np.ndarray, maxd2: float,
+                 weighted_first: bool = True, query_locally: bool = True, zero_empty: bool = False):
+    """SDF, analytic dSDF/dq (what utils/tools.py:174 get_gradient returns through autograd at
+    utils/tracker.py:252), per-neighbour weighted std (utils/tracker.py:245-249) and the
+    query outputs.  ``zero_empty`` gives rows with nn_count == 0 sdf 0 (mesher, utils/mesher.py:96-103)."""
+    qry = query_feature(st, q, nn_k, neighbor_dx, maxd2, weighted_first, False, query_locally)
+    valid = qry.idx >= 0
+    u, S, du = _weight_grads(qry, q)
+    Ssafe = np.where(S > 0, S, 1.0)
+    w64 = qry.weights.astype(np.float64)
+    F = qry.nbr_feat.shape[-1]
+    if weighted_first:
+        sdf, pre = mlp.forward(qry.feat)
+        gx = mlp.grad_x(pre)                                               # [N, F+3]
+        fv = np.concatenate([qry.nbr_feat, qry.vec], -1).astype(np.float64)  # [N,k,F+3]
+        a = (fv * gx[:, None, :]).sum(-1)                                  # [N,k]
+        abar = (a * w64).sum(1)
+        g1 = (((a - abar[:, None]) * valid)[..., None] * du).sum(1) / Ssafe[:, None]
+        gv = np.broadcast_to(gx[:, None, F:], qry.vec.shape)
+        g2 = (w64[..., None] * _vec_jacobian_t(qry, st.after_pgo, gv)).sum(1)
+        grad = g1 + g2
+        std = np.zeros(q.shape[0], np.float32)
+    else:
+        sdf_k, pre = mlp.forward(qry.feat)                                 # [N,k]
+        mean = (sdf_k * qry.weights).sum(1, dtype=np.float32)
+        var = (qry.weights * (sdf_k - mean[:, None]) ** 2).sum(1, dtype=np.float32)
+        std = np.sqrt(var).astype(np.float32)
+        gx = mlp.grad_x(pre)                                               # [N,k,F+3]
+        s64 = sdf_k.astype(np.float64)
+        sbar = (s64 * w64).sum(1)
+        g1 = (((s64 - sbar[:, None]) * valid)[..., None] * du).sum(1) / Ssafe[:, None]
+        g2 = (w64[..., None] * _vec_jacobian_t(qry, st.after_pgo, gx[..., F:])).sum(1)
+        grad = g1 + g2
+        sdf = mean
+    empty = qry.nn_counts == 0
+    grad[empty] = 0.0
+    if zero_empty:
+        sdf = np.where(empty, np.float32(0), sdf)
+    return sdf.astype(np.float32), grad.astype(np.float32), std, qry
+
+
+# ---------------------------------------------------------------- mapper (utils/mapper.py:425-593)
+def bce_with_logits_grad(pred: np.ndarray, label: np.ndarray, sigma: float):
+    """utils/loss.py:40-47 (unweighted, mean): loss and dL/dpred."""
+    p = pred.astype(np.float64) / sigma
+    y = 1.0 / (1.0 + np.exp(-label.astype(np.float64) / sigma))
+    loss = np.mean(np.maximum(p, 0) - p * y + np.log1p(np.exp(-np.abs(p))))
+    dp = (1.0 / (1.0 + np.exp(-p)) - y) / (pred.shape[0] * sigma)
+    return loss, dp
+
+
+def numerical_grad_points(x: np.ndarray, eps: float) -> np.ndarray:
+    """utils/mapper.py:683-711: two-sided stencil, blocks ordered x+,x-,y+,y-,z+,z-."""
+    out = []
+    for a in range(3):
+        e = np.zeros(3, np.float32)
+        e[a] = np.float32(eps)
+        out.append(x + e)
+        out.append(x - e)
+    return np.concatenate(out, 0).astype(np.float32)
+
+
+def _mlp_backward(mlp: MLP, x: np.ndarray, pre: np.ndarray, dsdf: np.ndarray):
+    """Accumulate MLP parameter grads and return dL/dx for rows x with upstream dsdf."""
+    s = float(mlp.sdf_scale)
+    d_out = dsdf.astype(np.float64) * s                                   # dL/d(lout output)
+    h = np.maximum(pre.astype(np.float64), 0)
+    dh = d_out[:, None] * mlp.W2[0].astype(np.float64)[None] * (pre > 0)
+    gW2 = (d_out[:, None] * h).sum(0)[None]
+    gb2 = np.array([d_out.sum()])
+    gW1 = dh.T @ x.astype(np.float64)
+    gb1 = dh.sum(0)
+    dx = dh @ mlp.W1.astype(np.float64)
+    return dx, dict(W1=gW1, b1=gb1, W2=gW2, b2=gb2)
+
+
+def mapper_forward_backward(st: MapState, mlp: MLP, coord: np.ndarray, label: np.ndarray, ts: np.ndarray,
+                            nn_k: int, neighbor_dx: np.ndarray, maxd2: float, weighted_first: bool,
+                            sigma: float, weight_e: float, decimation: int, eps: float):
+    """One mapping iteration up to the backward pass (utils/mapper.py:448-572): training-mode
+    queries (main batch with ts, then the numerical-gradient stencil without ts), BCE +
+    weight_e * eikonal, gradients w.r.t. local features [L+1,F] and MLP params."""
+    N = coord.shape[0]
+    Lp1, F = st.local_features.shape
+    qm = query_feature(st, coord, nn_k, neighbor_dx, maxd2, weighted_first, True, True, ts)
+    xd = coord[::decimation]
+    Nd = xd.shape[0]
+    qs_pts = numerical_grad_points(xd, eps)
+    qn = query_feature(st, qs_pts, nn_k, neighbor_dx, maxd2, weighted_first, True, True, None)
+
+    def predict(qry):
+        if weighted_first:
+            sdf, pre = mlp.forward(qry.feat)
+            return sdf, pre
+        sdf_k, pre = mlp.forward(qry.feat)
+        return (sdf_k * qry.weights).sum(1, dtype=np.float32), pre
+
+    sdf_m, pre_m = predict(qm)
+    sdf_n, pre_n = predict(qn)
+    sp = sdf_n.astype(np.float64).reshape(6, Nd)
+    g = np.stack([(sp[0] - sp[1]), (sp[2] - sp[3]), (sp[4] - sp[5])], 1) / (2 * eps)
+    gn = np.linalg.norm(g, axis=1)
+    loss_bce, d_m = bce_with_logits_grad(sdf_m, label, sigma)
+    loss = loss_bce + weight_e * np.mean((gn - 1.0) ** 2)
+    dg = weight_e * 2.0 * (gn - 1.0)[:, None] * g / np.where(gn > 0, gn, 1.0)[:, None] / Nd
+    d_n = np.zeros((6, Nd))
+    for a in range(3):
+        d_n[2 * a] = dg[:, a] / (2 * eps)
+        d_n[2 * a + 1] = -dg[:, a] / (2 * eps)
+    d_n = d_n.reshape(-1)
+    feat_grad = np.zeros((Lp1, F))
+    grads = dict(W1=0.0, b1=0.0, W2=0.0, b2=0.0)
+    for qry, pre, dsdf in ((qm, pre_m, d_m), (qn, pre_n, d_n)):
+        valid = qry.idx >= 0
+        if weighted_first:
+            dx, gp = _mlp_backward(mlp, qry.feat, pre, dsdf)
+            contrib = qry.weights.astype(np.float64)[..., None] * dx[:, None, :F]   # [n,k,F]
+        else:
+            n, k = qry.weights.shape
+            drow = (dsdf[:, None] * qry.weights.astype(np.float64)).reshape(-1)
+            dx, gp = _mlp_backward(mlp, qry.feat.reshape(n * k, -1), pre.reshape(n * k, -1), drow)
+            contrib = dx.reshape(n, k, -1)[..., :F]
+        np.add.at(feat_grad, qry.idx[valid], contrib[valid])
+        for key in grads:
+            grads[key] = grads[key] + gp[key]
+    return dict(loss=loss, sdf=sdf_m, numgrad=g.astype(np.float32), feat_grad=feat_grad.astype(np.float32),
+                mlp_grads={k: v.astype(np.float32) for k, v in grads.items()})
+
+
+def adam_step(param: np.ndarray, grad: np.ndarray, m: np.ndarray, v: np.ndarray, step: int,
+              lr: float, beta1: float = 0.9, beta2: float = 0.99, eps: float = 1e-15) -> None:
+    """torch.optim.Adam single-tensor update as configured by utils/tools.py:111-112
+    (betas (0.9, 0.99), eps 1e-15, no weight decay), float32 in place."""
+    f = np.float32
+    grad = grad.astype(np.float32)
+    m += f(1 - beta1) * (grad - m)                      # exp_avg.lerp_(grad, 1-beta1)
+    v *= f(beta2)
+    v += f(1 - beta2) * grad * grad                     # addcmul_(grad, grad, 1-beta2)
+    bc1 = 1 - beta1 ** step
+    bc2s = (1 - beta2 ** step) ** 0.5
+    denom = np.sqrt(v) / f(bc2s) + f(eps)
+    param += f(-lr / bc1) * m / denom
+
+
+# ---------------------------------------------------------------- tracker (utils/tracker.py)
+def expmap(axis_angle: np.ndarray) -> np.ndarray:
+    """utils/tracker.py:580-589 (Rodrigues)."""
+    angle = np.linalg.norm(axis_angle)
+    axis = axis_angle / angle
+    S = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    return np.eye(3) + S * np.sin(angle) + (S @ S) * (1.0 - np.cos(angle))
+
+
+def implicit_reg(points, sdf_grad, sdf_residual, weight, lm_lambda=0.0):
+    """utils/tracker.py:468-496: J = [p x g, g], N = J^T W J (+ lambda diag), t = N^-1 (-(JW)^T r)."""
+    p = points.astype(np.float64)
+    g = sdf_grad.astype(np.float64)
+    J = np.concatenate([np.cross(p, g), g], 1)
+    w = weight.astype(np.float64).reshape(-1, 1)
+    Nm = J.T @ (w * J)
+    Nm = Nm + lm_lambda * np.diag(np.diag(Nm))
+    gv = -(J * w).T @ sdf_residual.astype(np.float64)
+    t = np.linalg.inv(Nm) @ gv
+    T = np.eye(4)
+    T[:3, :3] = expmap(t[:3])
+    T[:3, 3] = t[3:]
+    return T, Nm, gv
+
+
+def registration_step(st: MapState, mlp: MLP, points: np.ndarray, sdf_labels: np.ndarray, nn_k: int,
+                      neighbor_dx: np.ndarray, maxd2: float, weighted_first: bool, min_grad_norm: float,
+                      max_grad_norm: float, GM_dist: float, GM_grad: float, lm_lambda: float,
+                      max_sdf_std: float):
+    """utils/tracker.py:277-452 without colours/normals: query, validity mask, Geman-McClure
+    weights normalised by 2*mean, implicit_reg."""
+    sdf, grad, std, qry = sdf_and_grad(st, mlp, points, nn_k, neighbor_dx, maxd2, weighted_first, True)
+    mask = qry.nn_counts >= nn_k
+    gnorm = np.linalg.norm(grad.astype(np.float64), axis=1)
+    valid = mask & (gnorm < max_grad_norm) & (gnorm > min_grad_norm) & (std < max_sdf_std)
+    cnt = int(valid.sum())
+    if cnt < 10:
+        return np.eye(4), cnt, 0.0, valid, None, None
+    r = sdf[valid].astype(np.float64) - sdf_labels[valid]
+    ga = gnorm[valid] - 1.0
+    w = (GM_grad / (GM_grad ** 2 + ga ** 2)) ** 2 * (GM_dist / (GM_dist ** 2 + r ** 2)) ** 2
+    w = w / (2.0 * w.mean())
+    T, Nm, gv = implicit_reg(points[valid], grad[valid], r, w, lm_lambda)
+    return T, cnt, float(np.mean(np.abs(r)) * 100.0), valid, Nm, gv
+
+
+# ---------------------------------------------------------------- mesher (utils/mesher.py:41-136)
+def mesher_query_points(st: MapState, mlp: MLP, coord: np.ndarray, nn_k: int, neighbor_dx: np.ndarray,
+                        maxd2: float, weighted_first: bool, mask_min_nn_count: int):
+    qry = query_feature(st, coord, nn_k, neighbor_dx, maxd2, weighted_first, False, False)
+    if weighted_first:
+        sdf, _ = mlp.forward(qry.feat)
+    else:
+        sdf_k, _ = mlp.forward(qry.feat)
+        sdf = (sdf_k * qry.weights).sum(1, dtype=np.float32)
+    sdf = np.where(qry.nn_counts >= 1, sdf, np.float32(0)).astype(np.float32)
+    return sdf, qry.nn_counts >= mask_min_nn_count
+
+
+def query_certainty(st: MapState, q: np.ndarray, resolution: float) -> np.ndarray:
+    """model/neural_points.py:511-525 with the own-voxel neighbourhood (utils/mapper.py:283)."""
+    dx = neighbor_offsets(1, 0.0)
+    _, idx = radius_neighborhood_search(st, q, dx, max_valid_dist2(1, resolution), False)
+    c = st.certainties[idx]
+    c[idx < 0] = 0.0
+    return c.max(-1)
+
+
+# ---------------------------------------------------------------- fixture helpers
+def map_from_fixture(z, prefix: str = "map_") -> MapState:
+    g = lambda k: z[prefix + k]  # noqa: E731
+    st = MapState(
+        resolution=float(g("resolution")), buffer_size=int(g("buffer_size")),
+        table=table_from_slots(int(g("buffer_size")), g("table_slots"), g("table_vals")),
+        points=g("neural_points").astype(np.float32), orientations=g("point_orientations").astype(np.float32),
+        geo_features=g("geo_features").astype(np.float32), ts_create=g("point_ts_create").astype(np.int64),
+        ts_update=g("point_ts_update").astype(np.int64), certainties=g("point_certainties").astype(np.float32),
+        travel_dist=g("travel_dist").astype(np.float32), cur_ts=int(g("cur_ts")),
+        diff_travel_dist_local=float(g("diff_travel_dist_local")),
+        local_mask=g("local_mask"), global2local=g("global2local"),
+        local_points=None, local_orientations=None, local_features=None,
+        local_certainties=None, local_ts_update=None)
+    m = st.local_mask
+    st.local_points = st.points[m[:-1]]
+    st.local_orientations = st.orientations[m[:-1]]
+    st.local_certainties = st.certainties[m[:-1]]
+    st.local_ts_update = st.ts_update[m[:-1]]
+    st.local_features = st.geo_features[m].copy()
+    return st
+
+
+def mlp_from_fixture(z, prefix: str = "dec_") -> MLP:
+    return MLP(z[prefix + "W1"].astype(np.float32), z[prefix + "b1"].astype(np.float32),
+               z[prefix + "W2"].astype(np.float32), z[prefix + "b2"].astype(np.float32),
+               float(z[prefix + "sdf_scale"]))

@@ -1,0 +1,460 @@
+#!/usr/bin/env python3
+"""Generate golden input/output vectors from the reference PIN-SLAM Python code.
+
+Runs ONLY in the build container (it imports /root/reference, which does not
+exist on the GPU box).  It writes small seeded ``.npz`` fixtures next to this
+file; the fixtures (data only: inputs and the reference's outputs) are what
+the tests and the oracle are pinned against.
+
+The reference is pure Python on PyTorch.  Its hot path needs no third-party
+native code, but the modules import open3d / roma / wandb / skimage at module
+level, so those are replaced by inert stub modules before import (none of
+them is touched on the query path).  ``get_time`` calls
+``torch.cuda.synchronize`` which raises without a GPU; it is replaced by
+``time.time``.
+
+Reference call sites exercised (file:line in /root/reference):
+  model/neural_points.py:205   NeuralPoints.update (hash insert, collisions)
+  model/neural_points.py:272   reset_local_map
+  model/neural_points.py:430   set_search_neighborhood
+  model/neural_points.py:459   radius_neighborhood_search
+  model/neural_points.py:511   query_certainty
+  model/neural_points.py:528   query_feature (all modes)
+  model/decoder.py:66          Decoder.sdf
+  utils/tools.py:174           get_gradient (autograd)
+  utils/tools.py:89            setup_optimizer (Adam)
+  utils/loss.py:40             sdf_bce_loss
+  utils/mapper.py:443-575      one mapping iteration (re-stated call sequence)
+  utils/mapper.py:683          get_numerical_gradient
+  utils/tracker.py:176         query_source_points
+  utils/tracker.py:277         registration_step / implicit_reg
+  utils/mesher.py:41           query_points
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+import os
+import sys
+import time
+import types
+from unittest import mock
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+sys.dont_write_bytecode = True
+for _name in ["open3d", "roma", "wandb", "skimage", "skimage.measure", "natsort",
+              "pyquaternion", "pypose", "laspy", "gtsam", "evo"]:
+    sys.modules[_name] = mock.MagicMock(name=_name)
+sys.path.insert(0, REF)
+
+import utils.tools as rtools  # noqa: E402
+rtools.get_time = time.time
+from utils.config import Config  # noqa: E402
+import model.neural_points as rnp  # noqa: E402
+rnp.get_time = time.time
+from model.neural_points import NeuralPoints  # noqa: E402
+from model.decoder import Decoder  # noqa: E402
+from utils.tools import get_gradient, setup_optimizer  # noqa: E402
+from utils.loss import sdf_bce_loss  # noqa: E402
+import utils.tracker as rtracker  # noqa: E402
+rtracker.get_time = time.time
+import utils.mapper as rmapper  # noqa: E402
+rmapper.get_time = time.time
+import utils.mesher as rmesher  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def surface_z(x, y):
+    return 0.5 * np.sin(x / 7.0) * np.cos(y / 5.0) + 0.15
+
+
+def make_config(voxel=0.3, cells=2, alpha=0.2, nn_k=8, weighted_first=True, buffer_size=1 << 17,
+                local_map_radius=15.0):
+    c = Config()
+    c.device = "cpu"
+    c.silence = True
+    c.voxel_size_m = voxel
+    c.num_nei_cells = cells
+    c.search_alpha = alpha
+    c.query_nn_k = nn_k
+    c.weighted_first = weighted_first
+    c.buffer_size = buffer_size
+    c.feature_dim = 8
+    c.feature_std = 0.0
+    c.local_map_radius = local_map_radius
+    c.local_map_travel_dist_ratio = 5.0
+    c.infer_bs = 1 << 20
+    c.mesh_min_nn = 8
+    return c
+
+
+def build_map(cfg, n_side, seed):
+    """Surface map through the reference's own insert path (NeuralPoints.update)."""
+    rng = np.random.default_rng(seed)
+    res = cfg.voxel_size_m
+    ii, jj = np.meshgrid(np.arange(n_side), np.arange(n_side), indexing="ij")
+    x = (ii.ravel() + 0.5) * res - n_side * res / 2
+    y = (jj.ravel() + 0.5) * res - n_side * res / 2
+    z = surface_z(x, y)
+    pts = np.stack([x, y, z], 1).astype(np.float32)
+    # jitter a little so the down-sample keeps interesting positions
+    pts += rng.normal(0, res * 0.05, pts.shape).astype(np.float32)
+    npm = NeuralPoints(cfg)
+    T = 10
+    npm.travel_dist = torch.arange(T, dtype=torch.float32) * 10.0
+    pts_t = torch.from_numpy(pts)
+    npm.update(pts_t, torch.zeros(3), torch.eye(3), 0)
+    M = npm.count()
+    # varied timestamps -> exercise the travel-distance filter and local mask
+    g = torch.Generator().manual_seed(seed)
+    npm.point_ts_create = torch.randint(0, T, (M,), generator=g)
+    npm.point_ts_update = npm.point_ts_create.clone()
+    npm.geo_features = torch.randn(M + 1, cfg.feature_dim, generator=g) * 0.05
+    npm.geo_features[-1] = 0.0
+    npm.point_certainties = torch.rand(M, generator=g) * 10.0
+    return npm, pts
+
+
+def random_quats(m, g):
+    q = torch.randn(m, 4, generator=g)
+    q = q / q.norm(dim=1, keepdim=True)
+    q[q[:, 0] < 0] *= -1
+    return q
+
+
+def make_queries(npm, cfg, n_surface, seed):
+    rng = np.random.default_rng(seed + 1)
+    P = npm.neural_points.numpy()
+    M = P.shape[0]
+    res = cfg.voxel_size_m
+    q1 = P[rng.integers(0, M, n_surface)] + rng.normal(0, 0.25, (n_surface, 3))
+    q2 = P[rng.integers(0, M, 128)]                       # coincide with a neural point
+    q3 = rng.uniform(-5, 5, (64, 3)) + np.array([200.0, -300.0, 50.0])  # no neighbours
+    q4 = P[rng.integers(0, M, 128)] + rng.normal(0, 0.1, (128, 3))
+    q4[:, 0] = np.round(q4[:, 0] / res) * res               # on voxel boundaries (x)
+    q4[:, 2] = np.round(q4[:, 2] / res) * res               # and (z)
+    q = np.concatenate([q1, q2, q3, q4], 0).astype(np.float32)
+    return q
+
+
+def decoder(cfg, seed=42):
+    torch.manual_seed(seed)
+    return Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1)
+
+
+def dec_params(dec):
+    return dict(W1=dec.layers[0].weight.detach().numpy().copy(),
+                b1=dec.layers[0].bias.detach().numpy().copy(),
+                W2=dec.lout.weight.detach().numpy().copy(),
+                b2=dec.lout.bias.detach().numpy().copy(),
+                sdf_scale=np.float32(dec.sdf_scale))
+
+
+def map_state(npm):
+    table = npm.buffer_pt_index.numpy()
+    slots = np.nonzero(table >= 0)[0]
+    return dict(
+        buffer_size=np.int64(npm.buffer_size), resolution=np.float32(npm.resolution),
+        table_slots=slots.astype(np.int64), table_vals=table[slots].astype(np.int64),
+        neural_points=npm.neural_points.numpy().copy(),
+        point_orientations=npm.point_orientations.numpy().copy(),
+        geo_features=npm.geo_features.detach().numpy().copy(),
+        point_ts_create=npm.point_ts_create.numpy().copy(),
+        point_ts_update=npm.point_ts_update.numpy().copy(),
+        point_certainties=npm.point_certainties.numpy().copy(),
+        travel_dist=npm.travel_dist.numpy().copy(),
+        cur_ts=np.int64(npm.cur_ts),
+        diff_travel_dist_local=np.float32(npm.diff_travel_dist_local),
+        local_mask=npm.local_mask.numpy().copy(),
+        global2local=npm.global2local.numpy().copy(),
+        neighbor_dx=npm.neighbor_dx.numpy().copy(),
+        max_valid_dist2=np.float64(npm.max_valid_dist2),
+    )
+
+
+def run_query(npm, dec, cfg, q, query_locally, training_mode=False, query_ts=None):
+    """Mirror of the tracker's query_source_points body (utils/tracker.py:226-260)."""
+    qt = torch.from_numpy(q).clone().requires_grad_(True)
+    feat, _, w, nn_counts, cert = npm.query_feature(qt, query_ts, training_mode=training_mode,
+                                                    query_locally=query_locally)
+    sdf = dec.sdf(feat)
+    out = {}
+    if not cfg.weighted_first:
+        sdf_per = sdf
+        mean = torch.sum(sdf * w, dim=1)
+        var = torch.sum(w * (sdf - mean.unsqueeze(-1)) ** 2, dim=1)
+        std = torch.sqrt(var).squeeze(1)
+        sdf = mean.squeeze(1)
+        out["sdf_std"] = std.detach().numpy()
+        out["sdf_per_nb"] = sdf_per.detach().numpy()[..., 0]
+    grad = get_gradient(qt, sdf)
+    out.update(feat=feat.detach().numpy(), weights=w.detach().numpy()[..., 0],
+               nn_counts=nn_counts.numpy(), certainty=cert.detach().numpy(),
+               sdf=sdf.detach().numpy(), grad=grad.detach().numpy())
+    return out
+
+
+def gen_query_case(name, cfg_kwargs, n_side, n_surface, seed):
+    cfg = make_config(**cfg_kwargs)
+    npm, _ = build_map(cfg, n_side, seed)
+    # sensor at origin, current frame 9
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    dec = decoder(cfg)
+    q = make_queries(npm, cfg, n_surface, seed)
+    rec = dict(queries=q, nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
+               num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha))
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    # raw radius search, both filters
+    for tf in (False, True):
+        d2, idx = npm.radius_neighborhood_search(torch.from_numpy(q), time_filtering=tf)
+        rec[f"rns{int(tf)}_dist2"] = d2.numpy()
+        rec[f"rns{int(tf)}_idx"] = idx.numpy()
+    # query modes: global (mesher) and local (tracker/mapper), no pgo
+    for ql in (False, True):
+        out = run_query(npm, dec, cfg, q, ql)
+        rec.update({f"q{int(ql)}_{k}": v for k, v in out.items()})
+    # after pgo: quaternion rotation of the neighbour vectors
+    g = torch.Generator().manual_seed(seed + 7)
+    npm.point_orientations = random_quats(npm.count(), g)
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    npm.after_pgo = True
+    rec["pgo_point_orientations"] = npm.point_orientations.numpy().copy()
+    out = run_query(npm, dec, cfg, q, True)
+    rec.update({f"qpgo_{k}": v for k, v in out.items()})
+    npm.after_pgo = False
+    # training-mode side effects (certainty scatter_add, ts amax)
+    cert0 = npm.local_point_certainties.clone()
+    ts0 = npm.local_point_ts_update.clone()
+    qts = torch.from_numpy(np.random.default_rng(seed + 3).integers(0, 20, q.shape[0]))
+    rec["train_query_ts"] = qts.numpy()
+    out = run_query(npm, dec, cfg, q, True, training_mode=True, query_ts=qts)
+    rec.update({f"qtrain_{k}": v for k, v in out.items()})
+    rec["train_cert_before"] = cert0.numpy()
+    rec["train_cert_after"] = npm.local_point_certainties.numpy().copy()
+    rec["train_ts_before"] = ts0.numpy()
+    rec["train_ts_after"] = npm.local_point_ts_update.numpy().copy()
+    # query_certainty with the own-voxel neighbourhood (utils/mapper.py:283-292)
+    npm.set_search_neighborhood(num_nei_cells=1, search_alpha=0.0)
+    rec["qc_neighbor_dx"] = npm.neighbor_dx.numpy().copy()
+    rec["qc_certainty"] = npm.query_certainty(torch.from_numpy(q)).numpy()
+    npm.set_search_neighborhood(num_nei_cells=cfg.num_nei_cells, search_alpha=cfg.search_alpha)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "M=", npm.count(), "L=", npm.local_count(), "N=", q.shape[0],
+          "Kc=", npm.neighbor_K, "valid rows", int((rec["q1_nn_counts"] > 0).sum()))
+
+
+class _FakeMapper:
+    """Binds the reference Mapper.sdf / get_numerical_gradient to a map + decoder."""
+
+    def __init__(self, cfg, npm, dec):
+        self.config = cfg
+        self.neural_points = npm
+        self.geo_mlp = dec
+        self.sdf = types.MethodType(rmapper.Mapper.sdf, self)
+        self.get_numerical_gradient = types.MethodType(rmapper.Mapper.get_numerical_gradient, self)
+
+
+def gen_mapper_case(name, cfg_kwargs, n_side, n_batch, seed, iters=2):
+    """One mapping() call of `iters` iterations (utils/mapper.py:425-593), re-stated
+    call by call with the reference's own functions (the Mapper object itself needs the
+    dataset stack, which is out of scope)."""
+    cfg = make_config(**cfg_kwargs)
+    npm, _ = build_map(cfg, n_side, seed)
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    dec = decoder(cfg)
+    fm = _FakeMapper(cfg, npm, dec)
+    rng = np.random.default_rng(seed + 11)
+    P = npm.local_neural_points.numpy()
+    rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
+               num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
+               iters=np.int64(iters), lr=np.float64(cfg.lr), adam_eps=np.float64(cfg.adam_eps),
+               weight_e=np.float64(cfg.weight_e), gradient_decimation=np.int64(cfg.gradient_decimation),
+               num_grad_eps=np.float64(cfg.voxel_size_m * cfg.num_grad_step_ratio),
+               sigma=np.float64(dec.sdf_scale))
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    rec["local_features_before"] = npm.local_geo_features.detach().numpy().copy()
+    rec["local_cert_before"] = npm.local_point_certainties.numpy().copy()
+    rec["local_ts_before"] = npm.local_point_ts_update.numpy().copy()
+    opt = setup_optimizer(cfg, list(npm.parameters()), list(dec.parameters()))
+    for it in range(iters):
+        base = P[rng.integers(0, P.shape[0], n_batch)]
+        off = rng.normal(0, 0.25, n_batch).astype(np.float32)
+        coord = base.copy()
+        coord[:, 2] += off
+        coord[:n_batch // 8] += rng.normal(0, 0.05, (n_batch // 8, 3)).astype(np.float32)
+        label = (-off).astype(np.float32)
+        ts = rng.integers(0, 20, n_batch)
+        rec[f"it{it}_coord"] = coord
+        rec[f"it{it}_label"] = label
+        rec[f"it{it}_ts"] = ts
+        coord_t = torch.from_numpy(coord)
+        label_t = torch.from_numpy(label)
+        ts_t = torch.from_numpy(ts)
+        # utils/mapper.py:461-486
+        geo_feature, _, weight_knn, _, _ = npm.query_feature(coord_t, ts_t)
+        sdf_pred = dec.sdf(geo_feature)
+        if not cfg.weighted_first:
+            sdf_pred = torch.sum(sdf_pred * weight_knn, dim=1).squeeze(1)
+        dec_n = cfg.gradient_decimation
+        g = fm.get_numerical_gradient(coord_t[::dec_n], sdf_pred[::dec_n],
+                                      cfg.voxel_size_m * cfg.num_grad_step_ratio)
+        # utils/mapper.py:515-547 (bce, unweighted; eikonal on all samples)
+        weight = torch.ones_like(label_t)
+        sdf_loss = sdf_bce_loss(sdf_pred, label_t, dec.sdf_scale, weight, cfg.loss_weight_on)
+        eik = ((g.norm(2, dim=-1) - 1.0) ** 2).mean()
+        loss = sdf_loss + cfg.weight_e * eik
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        rec[f"it{it}_sdf"] = sdf_pred.detach().numpy()
+        rec[f"it{it}_numgrad"] = g.detach().numpy()
+        rec[f"it{it}_loss"] = np.float64(loss.item())
+        rec[f"it{it}_feat_grad"] = npm.local_geo_features.grad.numpy().copy()
+        for k, p in zip(["W1", "b1", "W2", "b2"], dec.parameters()):
+            rec[f"it{it}_grad_{k}"] = p.grad.numpy().copy()
+        opt.step()
+        rec[f"it{it}_features_after"] = npm.local_geo_features.detach().numpy().copy()
+        for k, p in zip(["W1", "b1", "W2", "b2"], dec.parameters()):
+            rec[f"it{it}_{k}_after"] = p.detach().numpy().copy()
+        rec[f"it{it}_cert_after"] = npm.local_point_certainties.numpy().copy()
+        rec[f"it{it}_ts_after"] = npm.local_point_ts_update.numpy().copy()
+    # utils/neural_points.py:315 assign_local_to_global
+    npm.assign_local_to_global()
+    rec["global_features_after"] = npm.geo_features.detach().numpy().copy()
+    rec["global_cert_after"] = npm.point_certainties.numpy().copy()
+    rec["global_ts_update_after"] = npm.point_ts_update.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "L=", npm.local_count(), "loss", [rec[f"it{i}_loss"] for i in range(iters)])
+
+
+def gen_tracker_case(name, cfg_kwargs, n_side, n_src, seed):
+    """One registration_step (utils/tracker.py:277-452) on a shifted scan."""
+    cfg = make_config(**cfg_kwargs)
+    cfg.local_map_radius = 1e4  # whole map local
+    npm, _ = build_map(cfg, n_side, seed)
+    npm.point_ts_create[:] = 9
+    npm.point_ts_update[:] = 9
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    dec = decoder(cfg)
+    # train the decoder+features a little so the SDF is meaningful near the surface
+    fm = _FakeMapper(cfg, npm, dec)
+    opt = setup_optimizer(cfg, list(npm.parameters()), list(dec.parameters()))
+    rng = np.random.default_rng(seed + 5)
+    P = npm.local_neural_points.numpy()
+    for _ in range(60):
+        base = P[rng.integers(0, P.shape[0], 4096)]
+        off = rng.normal(0, 0.25, 4096).astype(np.float32)
+        coord = base.copy()
+        coord[:, 2] += off
+        ct = torch.from_numpy(coord)
+        feat, _, wk, _, _ = npm.query_feature(ct)
+        sdf = dec.sdf(feat)
+        if not cfg.weighted_first:
+            sdf = torch.sum(sdf * wk, dim=1).squeeze(1)
+        g = fm.get_numerical_gradient(ct[::10], sdf[::10], cfg.voxel_size_m * 0.2)
+        loss = sdf_bce_loss(sdf, torch.from_numpy(-off), dec.sdf_scale, None, False) + \
+            0.5 * ((g.norm(2, dim=-1) - 1.0) ** 2).mean()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    npm.assign_local_to_global()
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    # source scan: surface points within the map, displaced by a known SE(3)
+    src = P[rng.integers(0, P.shape[0], n_src)].astype(np.float64)
+    yaw = np.deg2rad(0.5)
+    R = np.array([[np.cos(yaw), -np.sin(yaw), 0], [np.sin(yaw), np.cos(yaw), 0], [0, 0, 1]])
+    t = np.array([0.05, -0.03, 0.02])
+    src = ((src - t) @ R).astype(np.float32)   # inverse offset: registration should recover R,t
+    tracker = rtracker.Tracker(cfg, npm, dec, None, None)
+    pts = torch.from_numpy(src)
+    out = tracker.query_source_points(pts, None, cfg.infer_bs, True, True, False, False,
+                                      query_locally=True, mask_min_nn_count=cfg.query_nn_k)
+    sdf_pred, sdf_grad, _, _, _, mask, certainty, sdf_std = out
+    res = tracker.registration_step(pts, None, torch.zeros(n_src), None, 9,
+                                    cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
+                                    cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, False)
+    delta_T, _, _, _, valid_points, resid_cm, _ = res
+    rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
+               num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
+               source=src, sdf=sdf_pred.numpy(), grad=sdf_grad.numpy(), mask=mask.numpy(),
+               certainty=certainty.numpy(), sdf_std=sdf_std.numpy(),
+               delta_T=delta_T.numpy(), valid_count=np.int64(valid_points.shape[0]),
+               resid_cm=np.float64(resid_cm),
+               reg_min_grad_norm=np.float64(cfg.reg_min_grad_norm),
+               reg_max_grad_norm=np.float64(cfg.reg_max_grad_norm),
+               reg_GM_dist_m=np.float64(cfg.reg_GM_dist_m), reg_GM_grad=np.float64(cfg.reg_GM_grad),
+               reg_lm_lambda=np.float64(cfg.reg_lm_lambda),
+               surface_sample_range_m=np.float64(cfg.surface_sample_range_m),
+               max_sdf_std_ratio=np.float64(cfg.max_sdf_std_ratio))
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    rec["local_features"] = npm.local_geo_features.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "valid", rec["valid_count"], "resid_cm", resid_cm)
+    print(delta_T)
+
+
+def gen_mesher_case(name, cfg_kwargs, n_side, seed):
+    cfg = make_config(**cfg_kwargs)
+    npm, _ = build_map(cfg, n_side, seed)
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    dec = decoder(cfg)
+    mesher = rmesher.Mesher(cfg, npm, dec, None, None)
+    P = npm.neural_points.numpy()
+    bbx = mock.MagicMock()
+    lo = P.min(0) * 0.3
+    hi = P.max(0) * 0.3
+    bbx.get_min_bound.return_value = lo.astype(np.float64)
+    bbx.get_max_bound.return_value = hi.astype(np.float64)
+    mc_res = 0.1
+    coord, voxel_num_xyz, voxel_origin = mesher.get_query_from_bbx(bbx, mc_res, 2, 2)
+    sdf, _, _, mask = mesher.query_points(coord, cfg.infer_bs, True, False, False, True,
+                                          query_locally=False, mask_min_nn_count=cfg.mesh_min_nn)
+    rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
+               num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
+               bbx_min=lo.astype(np.float64), bbx_max=hi.astype(np.float64), mc_res=np.float64(mc_res),
+               voxel_num_xyz=np.asarray(voxel_num_xyz), voxel_origin=np.asarray(voxel_origin),
+               coord=coord.numpy(), sdf=sdf.astype(np.float32), mc_mask=mask.astype(bool),
+               mesh_min_nn=np.int64(cfg.mesh_min_nn))
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "grid", voxel_num_xyz, "mask", int(mask.sum()))
+
+
+def gen_neighborhoods():
+    cfg = make_config()
+    npm = NeuralPoints(cfg)
+    rec = {}
+    for c, a in [(1, 0.0), (2, 0.2), (2, 0.3), (2, 0.5), (2, 1.0), (2, 2.0), (3, 0.2), (3, 0.5), (3, 1.0)]:
+        npm.set_search_neighborhood(c, a)
+        key = f"c{c}_a{int(round(a * 10))}"
+        rec[f"{key}_dx"] = npm.neighbor_dx.numpy()
+        rec[f"{key}_K"] = np.int64(npm.neighbor_K)
+        rec[f"{key}_max_valid_dist2"] = np.float64(npm.max_valid_dist2)
+    np.savez_compressed(os.path.join(OUT, "neighborhoods.npz"), **rec)
+
+
+def main():
+    meta = {"torch": torch.__version__, "numpy": np.__version__, "generated": time.strftime("%Y-%m-%d")}
+    gen_neighborhoods()
+    gen_query_case("query_wf", dict(weighted_first=True), 120, 1600, seed=1)
+    gen_query_case("query_nwf", dict(weighted_first=False), 120, 1600, seed=2)
+    gen_query_case("query_kitti", dict(voxel=0.4, alpha=0.5, nn_k=6, weighted_first=False), 90, 1200, seed=3)
+    gen_mapper_case("mapper_wf", dict(weighted_first=True), 100, 2000, seed=4)
+    gen_mapper_case("mapper_nwf", dict(weighted_first=False), 100, 2000, seed=5)
+    gen_tracker_case("tracker_wf", dict(weighted_first=True), 100, 3000, seed=6)
+    gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 100, 3000, seed=7)
+    gen_mesher_case("mesher_wf", dict(weighted_first=True), 60, seed=8)
+    with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
+        for k, v in meta.items():
+            f.write(f"{k}: {v}\n")
+
+
+if __name__ == "__main__":
+    main()
