@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Headline benchmark: SDF + analytic gradient queries/s over a 1M-neural-point map.
+
+Workload (BASELINE.json configs[1]): synthetic 1M-point
+surface map (1000 x 1000 voxels of 0.3 m, hash table B = 5e7), 262,144 queries
+per step = map points + N(0, 0.25^2), Kc = 33 cells (num_nei_cells 2, alpha 0.2),
+k = 8, F = 8, decoder 11 -> 64 -> 1, weighted_first, fp32, query_locally=False.
+One step = one fused HIP launch (pin_query_sdf) over the batch, inputs resident
+in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
+batch against its replica of the map ("weak" scaling, no data-path collective);
+the barrier + max-over-ranks timing is the only collective.
+
+Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
+12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
+mean kernel time from HIP events on the launch stream.  cpu_baseline: the numpy oracle
+(oracle/pin_oracle.py, single thread) on one full batch, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import pin_slam_amd as P  # noqa: E402
+from pin_slam_amd.synthetic import surface_map, surface_queries  # noqa: E402
+
+N_SIDE = 1000            # 1,000,000 neural points
+N_QUERY = 262144
+BYTES_PER_QUERY = 944    # SURVEY.md 8(d), Kc=33, k=8, F=8
+HBM_PEAK = 8.0e12        # MI355X_MICROARCH.md (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--nwf", action="store_true", help="weighted_first=False variant (per-neighbour decoding)")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="PMC-measured HBM bytes per launch (from profiles/), reported as roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(nm, dec, q, wf):
+    """Oracle (numpy, 1 thread) on one full batch of the same workload; median of 3."""
+    from threadpoolctl import threadpool_limits
+    from oracle import pin_oracle as O
+    from tests.helpers import oracle_mlp, oracle_state
+    st = oracle_state(nm)
+    mlp = oracle_mlp(dec)
+    qh = q.cpu().numpy()
+    dx = O.neighbor_offsets(2, 0.2)
+    times = []
+    with threadpool_limits(limits=1):
+        for _ in range(3):
+            t0 = time.perf_counter()
+            O.sdf_and_grad(st, mlp, qh, nm.config.query_nn_k, dx, nm.max_valid_dist2, wf, False)
+            times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"one full {qh.shape[0]}-query batch over the same 1M-point map, numpy oracle "
+                      f"single-threaded, median of 3 ({t:.2f} s each)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = f"cuda:{local_rank}"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(dev))
+    wf = not args.nwf
+    nm, dec, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf)
+    q = surface_queries(pts, N_QUERY, seed=7 + rank, device=dev)
+
+    def step():
+        return P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False,
+                           want_std=not wf)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record()
+        step()
+        ends[i].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = statistics.mean(s.elapsed_time(e) for s, e in zip(starts, ends))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    total_q = N_QUERY * args.steps * world
+    value = total_q / elapsed
+    achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
+    out = {
+        "metric": "SDF+grad queries/sec over 1M-point map",
+        "value": value,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "SDF+analytic-grad, 1M-point surface map, 262144 queries/step/GPU (configs[1])",
+                   "map_points": int(pts.shape[0]), "queries_per_step_per_gpu": N_QUERY, "Kc": int(nm.neighbor_K),
+                   "nn_k": 8, "feature_dim": 8, "mlp": "11-64-1", "weighted_first": wf,
+                   "buffer_size": int(nm.buffer_size), "parallelism": f"replicas x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK,
+                     "traffic": args.traffic_bytes,
+                     "kernel": "k_query_sdf", "kernel_ms": kern_ms,
+                     "algorithmic_bytes_per_query": BYTES_PER_QUERY},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * pin_slam_amd.h -- C ABI of the MI355X (gfx950) neural-point SDF engine.
+ *
+ * The reference (kelly7707/PIN_SLAM) has no FFI: its hot path is the Python
+ * class API of model.neural_points.NeuralPoints / model.decoder.Decoder
+ * evaluated by PyTorch ATen ops.  Each entry point below replaces one piece of
+ * that path (reference file:line cited per function); the Python package
+ * pin_slam_amd binds them with ctypes and restores the reference's class API.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer unless its comment says host;
+ *   - the library keeps no state and caches no pointer between calls;
+ *   - every call is stream-ordered on `stream` (a hipStream_t passed as void*),
+ *     never synchronises, and returns PIN_OK or a negative PIN_ERR_* code;
+ *   - sizes are int64_t element counts.
+ */
+#ifndef PIN_SLAM_AMD_H
+#define PIN_SLAM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PIN_OK 0
+#define PIN_ERR_ARG (-1)         /* bad argument (null pointer, size, unsupported shape) */
+#define PIN_ERR_HIP (-2)         /* a HIP launch or runtime call failed */
+#define PIN_ERR_UNSUPPORTED (-3) /* configuration outside what the kernels implement */
+
+#define PIN_FEATURE_DIM 8        /* feature_dim of every reference config */
+#define PIN_MAX_NN_K 8           /* query_nn_k <= 8 in every reference config */
+#define PIN_HIDDEN_DIM 64        /* geo_mlp_hidden_dim, geo_mlp_level = 1 */
+#define PIN_RECORD_UNFAITHFUL (1 << 30) /* record id flag, see pin_build_records */
+
+/* Voxel hash + neighbourhood (model/neural_points.py:69-73, :430-457, :459-476). */
+typedef struct PinHash {
+    const int32_t* table;        /* [buffer_size] slot -> global point index, -1 empty */
+    int64_t buffer_size;         /* B, < 2^31 */
+    float resolution;            /* voxel size; points are floor(p / resolution) in f32 */
+    int32_t num_cells;           /* Kc */
+    const int32_t* cells;        /* [Kc,4]: dx, dy, dz, floor_mod(dx*p0+dy*p1+dz*p2, B) */
+    float max_valid_dist2;       /* candidates with dist2 > this are rejected (f32 compare) */
+    int32_t reserved;
+} PinHash;
+
+/* Per-point candidate records and the arrays the k nearest neighbours are read from. */
+typedef struct PinPoints {
+    const float* records;        /* [M,4]: x, y, z, bits(id); id -1 = rejected (see pin_build_records) */
+    int64_t num_points;          /* M */
+    const float* features;       /* [rows, 8] geo features addressed by id */
+    const float* positions;      /* [rows, 3] positions addressed by id (read for flagged records) */
+    const float* orientations;   /* [rows, 4] quaternions (w,x,y,z); read only if after_pgo */
+    const float* certainties;    /* [rows] */
+    int64_t rows;
+    int32_t after_pgo;           /* rotate neighbour vectors (model/neural_points.py:606-607) */
+    int32_t reserved;
+} PinPoints;
+
+/* Geo decoder, hidden_level = 1 (model/decoder.py:16-88). */
+typedef struct PinMlp {
+    const float* W1;             /* [64, 11] */
+    const float* b1;             /* [64] */
+    const float* W2;             /* [1, 64] */
+    const float* b2;             /* [1] */
+    float sdf_scale;             /* logistic_gaussian_ratio * sigma_sigmoid_m (decoder.py:51-54) */
+    int32_t reserved;
+} PinMlp;
+
+/*
+ * pin_build_records -- per-point candidate records for one query mode.
+ * Replaces the per-candidate work of model/neural_points.py:480-499 + :555:
+ *   record[g] = (x_g, y_g, z_g, id_g) with
+ *     query_locally == 0:  id_g = g
+ *     query_locally == 1:  id_g = -1 if |travel_dist[cur_ts] - travel_dist[ts_create[g]]|
+ *                                      >= diff_travel_dist_local   (time filter, :480-488)
+ *                          id_g = global2local[g] otherwise          (:555)
+ *   and, if id_g >= 0 and local_positions[id_g] != positions[g] bitwise, id_g |= PIN_RECORD_UNFAITHFUL
+ *   (the neighbour vector then reads the local position; the distance keeps the global one).
+ */
+int pin_build_records(const float* positions, int64_t num_points, int32_t query_locally,
+                      const int64_t* global2local, const int64_t* ts_create, const float* travel_dist,
+                      int64_t travel_len, int64_t cur_ts, float diff_travel_dist_local,
+                      const float* local_positions, int64_t local_rows, float* records, void* stream);
+
+/* pin_neighbor_cells -- fill the [Kc,4] cell table from host offsets [Kc,3] (neural_points.py:430-439). */
+int pin_neighbor_cells(const int32_t* host_dx, int32_t num_cells, int64_t buffer_size,
+                       int32_t* cells_out, void* stream);
+
+/*
+ * pin_hash_rebuild -- table[slot(p_i)] = i for i in [0,n), the highest i winning a shared slot
+ * (model/neural_points.py:420-422, recreate_hash with merged points).  The table must be
+ * filled with -1 by the caller.
+ */
+int pin_hash_rebuild(const float* positions, int64_t n, float resolution, int32_t* table,
+                     int64_t buffer_size, void* stream);
+
+/*
+ * pin_radius_search -- model/neural_points.py:459-509 for the records' mode:
+ * dist2 [n,Kc] f32 (max_valid_dist2 for rejected) and idx [n,Kc] int64 (global index or -1).
+ */
+int pin_radius_search(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n,
+                      float* dist2_out, int64_t* idx_out, void* stream);
+
+/*
+ * pin_query_sdf -- fused query_feature + Decoder.sdf + analytic dSDF/dq for inference
+ * (utils/tracker.py:176-260 query_source_points, utils/mesher.py:41-136 query_points,
+ * utils/tools.py:174 get_gradient).  Outputs may be NULL when not wanted:
+ *   sdf [n], grad [n,3], nn_count [n] int32, certainty [n], sdf_std [n] (weighted_first == 0).
+ * zero_empty != 0 gives rows without neighbours sdf 0 (mesher) instead of MLP(0).
+ */
+int pin_query_sdf(const PinHash* hash, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
+                  int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
+                  int32_t* nn_count, float* certainty, float* sdf_std, void* stream);
+
+/*
+ * pin_query_feature_fwd -- model/neural_points.py:528-674 forward (inference outputs):
+ *   feat [n,11] (weighted_first) or [n,nn_k,11]; weights [n,nn_k]; nn_counts [n] int64;
+ *   certainty [n]; saved local ids [n,nn_k] int32 and global ids [n,nn_k] int32 (-1 invalid).
+ */
+int pin_query_feature_fwd(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,
+                          int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts,
+                          float* certainty, int32_t* ids, int32_t* gids, void* stream);
+
+/*
+ * pin_query_feature_bwd -- backward of pin_query_feature_fwd given dL/dfeat and dL/dweights
+ * (either may be NULL): grad_q [n,3] (may be NULL) and grad_features [rows,8] accumulated
+ * with float atomics (may be NULL).  The reference obtains these from autograd through
+ * model/neural_points.py:492-662.
+ */
+int pin_query_feature_bwd(const PinPoints* pts, const float* q, int64_t n, int32_t nn_k, int32_t weighted_first,
+                          const int32_t* ids, const int32_t* gids, const float* weights, const float* grad_feat,
+                          const float* grad_weights, float* grad_q, float* grad_features, void* stream);
+
+/*
+ * pin_train_scatter -- training-mode side effects of query_feature (model/neural_points.py:637-648):
+ * certainties[id] += w (scatter_add_), ts_update[id] = max(ts_update[id], query_ts) (scatter_reduce amax,
+ * only if query_ts and ts_update are non-NULL).
+ */
+int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32_t nn_k, const int64_t* query_ts,
+                      float* certainties, int64_t* ts_update, void* stream);
+
+/*
+ * pin_query_certainty -- model/neural_points.py:511-525: max certainty over the cells of the
+ * hash's neighbourhood (own voxel in utils/mapper.py:283), 0 where empty.
+ */
+int pin_query_certainty(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n,
+                        float* certainty_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIN_SLAM_AMD_H */

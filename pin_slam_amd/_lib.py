@@ -1,0 +1,108 @@
+"""ctypes binding of libpin_slam_amd.so (the C ABI declared in include/pin_slam_amd.h).
+
+The library is REQUIRED: there is no CPU or eager-PyTorch fallback for the hot
+path.  If the shared object is missing or a call fails, this module raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpin_slam_amd.so")
+
+PIN_OK = 0
+_ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
+
+FEATURE_DIM = 8
+MAX_NN_K = 8
+HIDDEN_DIM = 64
+RECORD_UNFAITHFUL = 1 << 30
+
+c_void_p = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f32 = ctypes.c_float
+
+
+class PinHash(ctypes.Structure):
+    _fields_ = [("table", c_void_p), ("buffer_size", i64), ("resolution", f32), ("num_cells", i32),
+                ("cells", c_void_p), ("max_valid_dist2", f32), ("reserved", i32)]
+
+
+class PinPoints(ctypes.Structure):
+    _fields_ = [("records", c_void_p), ("num_points", i64), ("features", c_void_p), ("positions", c_void_p),
+                ("orientations", c_void_p), ("certainties", c_void_p), ("rows", i64), ("after_pgo", i32),
+                ("reserved", i32)]
+
+
+class PinMlp(ctypes.Structure):
+    _fields_ = [("W1", c_void_p), ("b1", c_void_p), ("W2", c_void_p), ("b2", c_void_p), ("sdf_scale", f32),
+                ("reserved", i32)]
+
+
+_P = ctypes.POINTER
+# name -> (argtypes) ; every function returns int
+_SIGS = {
+    "pin_build_records": [c_void_p, i64, i32, c_void_p, c_void_p, c_void_p, i64, i64, f32, c_void_p, i64,
+                          c_void_p, c_void_p],
+    "pin_neighbor_cells": [c_void_p, i32, i64, c_void_p, c_void_p],
+    "pin_hash_rebuild": [c_void_p, i64, f32, c_void_p, i64, c_void_p],
+    "pin_radius_search": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_query_sdf": [_P(PinHash), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
+                      c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_feature_fwd": [_P(PinHash), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_feature_bwd": [_P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_train_scatter": [c_void_p, c_void_p, i64, i32, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_certainty": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p],
+}
+
+_lib = None
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def load():
+    """Load the shared library (no GPU needed to load).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"pin_slam_amd: native library not built ({LIB_PATH}); run `python -m pin_slam_amd.build` "
+                           "or __graft_entry__.build(). There is no fallback path.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != PIN_OK:
+        raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  The tensor must be contiguous."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("pin_slam_amd: kernels need contiguous tensors")
+    return c_void_p(t.data_ptr())
+
+
+def stream(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t):
+    if not t.is_cuda:
+        raise RuntimeError("pin_slam_amd: the HIP kernels need tensors on a ROCm device (got %s); the hot path has "
+                           "no CPU implementation" % t.device)

@@ -1,0 +1,561 @@
+// pin_query.hip -- neural-point query kernels for gfx950 (MI355X) and their C ABI.
+//
+// One lane owns one query.  The lane hashes its voxel once, then probes the Kc
+// neighbour cells in chunks (all probes of a chunk in flight before their records
+// are read), keeps the k nearest candidates in a register top-k, gathers the k
+// feature rows (2 x 16 B loads each), and -- in the fused path -- evaluates the
+// 11->64->1 decoder with its weights in scalar registers (wave-uniform loads) and
+// the closed-form dSDF/dq.  See DESIGN.md for the roofline and data layout.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "pin_device.h"
+
+using namespace pin;
+
+namespace {
+
+constexpr int kChunk = 12;
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int launch_status() { return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP; }
+
+bool hash_ok(const PinHash* h) {
+    return h && h->table && h->cells && h->num_cells > 0 && h->buffer_size > 0 && h->buffer_size < (1ll << 31) &&
+           h->resolution > 0.f;
+}
+bool points_ok(const PinPoints* p) { return p && p->records && p->num_points >= 0; }
+
+// ------------------------------------------------------------------ records
+__global__ void __launch_bounds__(kBlock)
+k_build_records(const float* __restrict__ pos, int64_t M, int32_t local, const int64_t* __restrict__ g2l,
+                const int64_t* __restrict__ ts_create, const float* __restrict__ travel, int64_t cur_ts,
+                float diff_local, const float* __restrict__ lpos, int64_t lrows, float4* __restrict__ out) {
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= M) return;
+    const float x = pos[3 * g], y = pos[3 * g + 1], z = pos[3 * g + 2];
+    int id = (int)g;
+    if (local) {
+        if (travel) {
+            const float dtd = fabsf(travel[cur_ts] - travel[ts_create[g]]);
+            if (!(dtd < diff_local)) id = -1;
+        }
+        if (id >= 0 && g2l) {
+            const int64_t l = g2l[g];
+            id = (int)l;
+            if (l >= 0 && lpos && l < lrows) {
+                const bool same = __float_as_int(lpos[3 * l]) == __float_as_int(x) &&
+                                  __float_as_int(lpos[3 * l + 1]) == __float_as_int(y) &&
+                                  __float_as_int(lpos[3 * l + 2]) == __float_as_int(z);
+                if (!same) id |= PIN_RECORD_UNFAITHFUL;
+            }
+        }
+    }
+    out[g] = make_float4(x, y, z, __int_as_float(id));
+}
+
+// ------------------------------------------------------------------ hash rebuild
+__global__ void __launch_bounds__(kBlock)
+k_hash_rebuild(const float* __restrict__ pos, int64_t n, float res, int32_t* __restrict__ table, int64_t B) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = base_slot(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], res, B);
+    atomicMax(table + s, (int)i);  // last writer of the CPU reference = highest index
+}
+
+// ------------------------------------------------------------------ radius search
+__global__ void __launch_bounds__(kBlock)
+k_radius_search(const PinHash h, const float4* __restrict__ rec, const float* __restrict__ q, int64_t n,
+                float* __restrict__ dist2_out, int64_t* __restrict__ idx_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const uint32_t B = (uint32_t)h.buffer_size;
+    const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
+    const int Kc = h.num_cells;
+    for (int c = 0; c < Kc; ++c) {
+        uint32_t s = base + (uint32_t)h.cells[4 * c + 3];
+        s = s >= B ? s - B : s;
+        int g = h.table[s];
+        float d2 = h.max_valid_dist2;
+        if (g >= 0) {
+            const float4 r = rec[g];
+            if (__float_as_int(r.w) == -1) {
+                g = -1;  // time-filtered before the distance (neural_points.py:488)
+            } else {
+                d2 = dist2(r.x, r.y, r.z, qx, qy, qz);
+                if (d2 > h.max_valid_dist2) g = -1;
+            }
+        }
+        dist2_out[i * Kc + c] = d2;
+        idx_out[i * Kc + c] = g;
+    }
+}
+
+// ------------------------------------------------------------------ certainty
+__global__ void __launch_bounds__(kBlock)
+k_query_certainty(const PinHash h, const float4* __restrict__ rec, const float* __restrict__ cert,
+                  const float* __restrict__ q, int64_t n, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const uint32_t B = (uint32_t)h.buffer_size;
+    const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
+    float m = -INFINITY;
+    for (int c = 0; c < h.num_cells; ++c) {
+        uint32_t s = base + (uint32_t)h.cells[4 * c + 3];
+        s = s >= B ? s - B : s;
+        const int g = h.table[s];
+        float val = 0.f;
+        if (g >= 0) {
+            const float4 r = rec[g];
+            if (dist2(r.x, r.y, r.z, qx, qy, qz) <= h.max_valid_dist2) val = cert[g];
+        }
+        m = fmaxf(m, val);
+    }
+    out[i] = m;
+}
+
+// ------------------------------------------------------------------ fused SDF (+grad)
+// Tracker / mesher inference: query_feature + Decoder.sdf + get_gradient in one pass.
+template <bool WF, bool PGO, bool GRAD>
+__global__ void __launch_bounds__(kBlock)
+k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n, int nn_k,
+            int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out, int* __restrict__ nn_out,
+            float* __restrict__ cert_out, float* __restrict__ std_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    TopK tk;
+    tk.init();
+    const int nn = scan_candidates<kChunk>(h, (const float4*)p.records, qx, qy, qz, tk);
+    Neighbours nb;
+    load_topk(p, tk, nn, nn_k, qx, qy, qz, nb);
+
+    float cert = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        const float c = nb.id[j] >= 0 ? p.certainties[nb.id[j]] : 0.f;
+        cert = cert + c * nb.w[j];
+    }
+
+    float sdf = 0.f, std_v = 0.f;
+    float gq[3] = {0.f, 0.f, 0.f};
+    if constexpr (WF) {
+        // x = sum_j w_j [f_j, v_j]   (neural_points.py:660-662)
+        float x[kD];
+#pragma unroll
+        for (int d = 0; d < kD; ++d) x[d] = 0.f;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            if (nb.id[j] < 0) continue;
+            float xj[kD];
+            float4 qt;
+            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
+#pragma unroll
+            for (int d = 0; d < kD; ++d) x[d] = x[d] + xj[d] * nb.w[j];
+        }
+        float gx[kD];
+        sdf = mlp_sdf<GRAD, 0, kD>(m, x, gx);
+        if (nn == 0 && zero_empty) sdf = 0.f;
+        if (GRAD && nn > 0) {
+            // dsdf/dq = sum_j (a_j - abar)/S du_j/dq + sum_j w_j R_j gx[F:],  a_j = gx . [f_j, v_j]
+            float abar = 0.f;
+#pragma unroll
+            for (int d = 0; d < kD; ++d) abar = fmaf(gx[d], x[d], abar);
+            const float invS = 1.f / nb.S;
+#pragma unroll
+            for (int j = 0; j < kK; ++j) {
+                if (nb.id[j] < 0) continue;
+                float xj[kD];
+                float4 qt;
+                neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
+                float a = 0.f;
+#pragma unroll
+                for (int d = 0; d < kD; ++d) a = fmaf(gx[d], xj[d], a);
+                const float coef = -2.f * nb.u[j] * nb.u[j] * (a - abar) * invS;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, nb.pg[j][d], gq[d]);
+                float r0 = gx[kF], r1 = gx[kF + 1], r2 = gx[kF + 2];
+                if (PGO) quat_rotate_active(qt, gx[kF], gx[kF + 1], gx[kF + 2], r0, r1, r2);
+                gq[0] = fmaf(nb.w[j], r0, gq[0]);
+                gq[1] = fmaf(nb.w[j], r1, gq[1]);
+                gq[2] = fmaf(nb.w[j], r2, gq[2]);
+            }
+        }
+    } else {
+        // per-neighbour decoding, then the weighted mean / std (utils/tracker.py:245-249)
+        float sk[kK];
+        float gv[kK][3];
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            sk[j] = 0.f;
+            gv[j][0] = gv[j][1] = gv[j][2] = 0.f;
+            if (nb.id[j] < 0) continue;
+            float xj[kD];
+            float4 qt;
+            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
+            float g3[3];
+            sk[j] = mlp_sdf<GRAD, kF, 3>(m, xj, g3);
+            if (GRAD) {
+                if (PGO) quat_rotate_active(qt, g3[0], g3[1], g3[2], gv[j][0], gv[j][1], gv[j][2]);
+                else { gv[j][0] = g3[0]; gv[j][1] = g3[1]; gv[j][2] = g3[2]; }
+            }
+        }
+        float mean = 0.f;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) mean = mean + sk[j] * nb.w[j];
+        float var = 0.f;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            const float dv = sk[j] - mean;
+            var = var + nb.w[j] * (dv * dv);
+        }
+        sdf = mean;
+        std_v = sqrtf(var);
+        if (GRAD && nn > 0) {
+            const float invS = 1.f / nb.S;
+#pragma unroll
+            for (int j = 0; j < kK; ++j) {
+                if (nb.id[j] < 0) continue;
+                const float coef = -2.f * nb.u[j] * nb.u[j] * (sk[j] - mean) * invS;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, nb.pg[j][d], gq[d]);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) gq[d] = fmaf(nb.w[j], gv[j][d], gq[d]);
+            }
+        }
+    }
+    if (sdf_out) sdf_out[i] = sdf;
+    if (GRAD && grad_out) {
+        grad_out[3 * i] = gq[0];
+        grad_out[3 * i + 1] = gq[1];
+        grad_out[3 * i + 2] = gq[2];
+    }
+    if (nn_out) nn_out[i] = nn;
+    if (cert_out) cert_out[i] = cert;
+    if (std_out) std_out[i] = std_v;
+}
+
+// ------------------------------------------------------------------ drop-in query_feature
+template <bool WF, bool PGO>
+__global__ void __launch_bounds__(kBlock)
+k_query_feature_fwd(const PinHash h, const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k,
+                    float* __restrict__ feat, float* __restrict__ weights, int64_t* __restrict__ nn_counts,
+                    float* __restrict__ cert_out, int* __restrict__ ids, int* __restrict__ gids) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    TopK tk;
+    tk.init();
+    const int nn = scan_candidates<kChunk>(h, (const float4*)p.records, qx, qy, qz, tk);
+    Neighbours nb;
+    load_topk(p, tk, nn, nn_k, qx, qy, qz, nb);
+    float cert = 0.f;
+    if (cert_out && p.certainties) {
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            const float c = nb.id[j] >= 0 ? p.certainties[nb.id[j]] : 0.f;
+            cert = cert + c * nb.w[j];
+        }
+    }
+    float x[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) x[d] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        if (j >= nn_k) break;
+        float xj[kD];
+#pragma unroll
+        for (int d = 0; d < kD; ++d) xj[d] = 0.f;
+        if (nb.id[j] >= 0) {
+            float4 qt;
+            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
+        }
+        if (WF) {
+#pragma unroll
+            for (int d = 0; d < kD; ++d) x[d] = x[d] + xj[d] * nb.w[j];
+        } else {
+            float* o = feat + (i * nn_k + j) * kD;
+#pragma unroll
+            for (int d = 0; d < kD; ++d) o[d] = xj[d];
+        }
+        weights[i * nn_k + j] = nb.w[j];
+        if (ids) ids[i * nn_k + j] = nb.id[j];
+        if (gids) gids[i * nn_k + j] = nb.id[j] >= 0 ? tk.g[j] : -1;
+    }
+    if (WF) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) feat[i * kD + d] = x[d];
+    }
+    if (nn_counts) nn_counts[i] = nn;
+    if (cert_out) cert_out[i] = cert;
+}
+
+template <bool WF, bool PGO>
+__global__ void __launch_bounds__(kBlock)
+k_query_feature_bwd(const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k, const int* __restrict__ ids,
+                    const int* __restrict__ gids, const float* __restrict__ weights,
+                    const float* __restrict__ gfeat, const float* __restrict__ gw, float* __restrict__ gq_out,
+                    float* __restrict__ gF) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const float4* __restrict__ rec = (const float4*)p.records;
+    float gx[kD];
+    if (WF) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) gx[d] = gfeat ? gfeat[i * kD + d] : 0.f;
+    }
+    float u[kK], w[kK], dw[kK], pg[kK][3];
+    int id[kK];
+    float S = 0.f;
+    float gq[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        id[j] = -1;
+        u[j] = 0.f;
+        w[j] = 0.f;
+        dw[j] = 0.f;
+        pg[j][0] = pg[j][1] = pg[j][2] = 0.f;
+        if (j >= nn_k) continue;
+        const int g = gids[i * nn_k + j];
+        if (g < 0) continue;
+        id[j] = ids[i * nn_k + j];
+        const float4 r = rec[g];
+        const float d2 = dist2(r.x, r.y, r.z, qx, qy, qz);
+        u[j] = 1.0f / (d2 + kIdwEps);
+        S = S + u[j];
+        w[j] = weights[i * nn_k + j];
+        pg[j][0] = qx - r.x;
+        pg[j][1] = qy - r.y;
+        pg[j][2] = qz - r.z;
+        float v[3];
+        float px = r.x, py = r.y, pz = r.z;
+        if (__float_as_int(r.w) & PIN_RECORD_UNFAITHFUL) {
+            px = p.positions[3 * (int64_t)id[j]];
+            py = p.positions[3 * (int64_t)id[j] + 1];
+            pz = p.positions[3 * (int64_t)id[j] + 2];
+        }
+        v[0] = qx - px;
+        v[1] = qy - py;
+        v[2] = qz - pz;
+        float4 qt = make_float4(1.f, 0.f, 0.f, 0.f);
+        if (PGO) {
+            qt = ((const float4*)p.orientations)[id[j]];
+            quat_rotate_passive(qt, v[0], v[1], v[2]);
+        }
+        // dL/dw_j and the direct gradients through feature and vector
+        float gvec[3];
+        float gfe[kF];
+        if (WF) {
+            const float4* fr = (const float4*)(p.features + (int64_t)id[j] * kF);
+            const float4 f0 = fr[0], f1 = fr[1];
+            const float f[kF] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            float s = 0.f;
+#pragma unroll
+            for (int d = 0; d < kF; ++d) s = fmaf(gx[d], f[d], s);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) s = fmaf(gx[kF + d], v[d], s);
+            dw[j] = s;
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gfe[d] = w[j] * gx[d];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) gvec[d] = w[j] * gx[kF + d];
+        } else {
+            const float* G = gfeat ? gfeat + (i * nn_k + j) * kD : nullptr;
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gfe[d] = G ? G[d] : 0.f;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) gvec[d] = G ? G[kF + d] : 0.f;
+        }
+        if (gw) dw[j] += gw[i * nn_k + j];
+        if (gF) {
+            float* dst = gF + (int64_t)id[j] * kF;
+#pragma unroll
+            for (int d = 0; d < kF; ++d) atomicAdd(dst + d, gfe[d]);
+        }
+        float r0 = gvec[0], r1 = gvec[1], r2 = gvec[2];
+        if (PGO) quat_rotate_active(qt, gvec[0], gvec[1], gvec[2], r0, r1, r2);
+        gq[0] += r0;
+        gq[1] += r1;
+        gq[2] += r2;
+    }
+    if (!gq_out) return;
+    if (S > 0.f) {
+        float wbar = 0.f;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) wbar = fmaf(w[j], dw[j], wbar);
+        const float invS = 1.f / S;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            if (id[j] < 0) continue;
+            const float coef = -2.f * u[j] * u[j] * (dw[j] - wbar) * invS;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, pg[j][d], gq[d]);
+        }
+    }
+    gq_out[3 * i] = gq[0];
+    gq_out[3 * i + 1] = gq[1];
+    gq_out[3 * i + 2] = gq[2];
+}
+
+// ------------------------------------------------------------------ training side effects
+__global__ void __launch_bounds__(kBlock)
+k_train_scatter(const int* __restrict__ ids, const float* __restrict__ w, int64_t total, int nn_k,
+                const int64_t* __restrict__ qts, float* __restrict__ cert, int64_t* __restrict__ ts) {
+    const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= total) return;
+    const int id = ids[e];
+    if (id < 0) return;
+    if (cert) atomicAdd(cert + id, w[e]);
+    if (qts && ts) atomicMax((unsigned long long*)(ts + id), (unsigned long long)qts[e / nn_k]);
+}
+
+}  // namespace
+
+// ===================================================================== C ABI
+extern "C" {
+
+int pin_build_records(const float* positions, int64_t num_points, int32_t query_locally, const int64_t* global2local,
+                      const int64_t* ts_create, const float* travel_dist, int64_t travel_len, int64_t cur_ts,
+                      float diff_travel_dist_local, const float* local_positions, int64_t local_rows, float* records,
+                      void* stream) {
+    if (num_points < 0 || (num_points > 0 && (!positions || !records))) return PIN_ERR_ARG;
+    if (query_locally && travel_dist && (!ts_create || cur_ts < 0 || cur_ts >= travel_len)) return PIN_ERR_ARG;
+    if (num_points == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_build_records, grid_for(num_points), dim3(kBlock), 0, as_stream(stream), positions,
+                       num_points, query_locally, global2local, ts_create, travel_dist, cur_ts, diff_travel_dist_local,
+                       local_positions, local_rows, (float4*)records);
+    return launch_status();
+}
+
+int pin_neighbor_cells(const int32_t* host_dx, int32_t num_cells, int64_t buffer_size, int32_t* cells_out,
+                       void* stream) {
+    if (!host_dx || !cells_out || num_cells <= 0 || buffer_size <= 0 || buffer_size >= (1ll << 31)) return PIN_ERR_ARG;
+    std::vector<int32_t> cells(4 * (size_t)num_cells);
+    for (int c = 0; c < num_cells; ++c) {
+        const int64_t dx = host_dx[3 * c], dy = host_dx[3 * c + 1], dz = host_dx[3 * c + 2];
+        int64_t r = (dx * kP0 + dy * kP1 + dz * kP2) % buffer_size;
+        if (r < 0) r += buffer_size;
+        cells[4 * c] = (int32_t)dx;
+        cells[4 * c + 1] = (int32_t)dy;
+        cells[4 * c + 2] = (int32_t)dz;
+        cells[4 * c + 3] = (int32_t)r;
+    }
+    // pageable source: the copy is staged before the call returns
+    if (hipMemcpyAsync(cells_out, cells.data(), cells.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                       as_stream(stream)) != hipSuccess)
+        return PIN_ERR_HIP;
+    return PIN_OK;
+}
+
+int pin_hash_rebuild(const float* positions, int64_t n, float resolution, int32_t* table, int64_t buffer_size,
+                     void* stream) {
+    if (n < 0 || !table || buffer_size <= 0 || buffer_size >= (1ll << 31) || resolution <= 0.f) return PIN_ERR_ARG;
+    if (n > (int64_t)INT32_MAX) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!positions) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_hash_rebuild, grid_for(n), dim3(kBlock), 0, as_stream(stream), positions, n, resolution,
+                       table, buffer_size);
+    return launch_status();
+}
+
+int pin_radius_search(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n, float* dist2_out,
+                      int64_t* idx_out, void* stream) {
+    if (!hash_ok(hash) || !points_ok(pts) || n < 0 || (n > 0 && (!q || !dist2_out || !idx_out))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_radius_search, grid_for(n), dim3(kBlock), 0, as_stream(stream), *hash,
+                       (const float4*)pts->records, q, n, dist2_out, idx_out);
+    return launch_status();
+}
+
+int pin_query_certainty(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n, float* certainty_out,
+                        void* stream) {
+    if (!hash_ok(hash) || !points_ok(pts) || !pts->certainties || n < 0 || (n > 0 && (!q || !certainty_out)))
+        return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_query_certainty, grid_for(n), dim3(kBlock), 0, as_stream(stream), *hash,
+                       (const float4*)pts->records, pts->certainties, q, n, certainty_out);
+    return launch_status();
+}
+
+int pin_query_sdf(const PinHash* hash, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
+                  int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad, int32_t* nn_count,
+                  float* certainty, float* sdf_std, void* stream) {
+    if (!hash_ok(hash) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
+        return PIN_ERR_ARG;
+    if (!pts->features || !pts->certainties || (pts->after_pgo && !pts->orientations)) return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q) return PIN_ERR_ARG;
+    const bool g = grad != nullptr;
+    const bool pgo = pts->after_pgo != 0;
+    auto s = as_stream(stream);
+#define PIN_LAUNCH_SDF(WF, PGO, GRAD)                                                                          \
+    hipLaunchKernelGGL((k_query_sdf<WF, PGO, GRAD>), grid_for(n), dim3(kBlock), 0, s, *hash, *pts, *mlp, q, n, \
+                       nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std)
+    if (weighted_first) {
+        if (pgo) { if (g) PIN_LAUNCH_SDF(true, true, true); else PIN_LAUNCH_SDF(true, true, false); }
+        else { if (g) PIN_LAUNCH_SDF(true, false, true); else PIN_LAUNCH_SDF(true, false, false); }
+    } else {
+        if (pgo) { if (g) PIN_LAUNCH_SDF(false, true, true); else PIN_LAUNCH_SDF(false, true, false); }
+        else { if (g) PIN_LAUNCH_SDF(false, false, true); else PIN_LAUNCH_SDF(false, false, false); }
+    }
+#undef PIN_LAUNCH_SDF
+    return launch_status();
+}
+
+int pin_query_feature_fwd(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,
+                          int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts, float* certainty,
+                          int32_t* ids, int32_t* gids, void* stream) {
+    if (!hash_ok(hash) || !points_ok(pts) || !pts->features || n < 0) return PIN_ERR_ARG;
+    if (pts->after_pgo && !pts->orientations) return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q || !feat || !weights) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    const bool pgo = pts->after_pgo != 0;
+#define PIN_LAUNCH_FWD(WF, PGO)                                                                          \
+    hipLaunchKernelGGL((k_query_feature_fwd<WF, PGO>), grid_for(n), dim3(kBlock), 0, s, *hash, *pts, q, n, \
+                       nn_k, feat, weights, nn_counts, certainty, ids, gids)
+    if (weighted_first) { if (pgo) PIN_LAUNCH_FWD(true, true); else PIN_LAUNCH_FWD(true, false); }
+    else { if (pgo) PIN_LAUNCH_FWD(false, true); else PIN_LAUNCH_FWD(false, false); }
+#undef PIN_LAUNCH_FWD
+    return launch_status();
+}
+
+int pin_query_feature_bwd(const PinPoints* pts, const float* q, int64_t n, int32_t nn_k, int32_t weighted_first,
+                          const int32_t* ids, const int32_t* gids, const float* weights, const float* grad_feat,
+                          const float* grad_weights, float* grad_q, float* grad_features, void* stream) {
+    if (!points_ok(pts) || !pts->features || n < 0) return PIN_ERR_ARG;
+    if (pts->after_pgo && !pts->orientations) return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q || !ids || !gids || !weights) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    const bool pgo = pts->after_pgo != 0;
+#define PIN_LAUNCH_BWD(WF, PGO)                                                                                \
+    hipLaunchKernelGGL((k_query_feature_bwd<WF, PGO>), grid_for(n), dim3(kBlock), 0, s, *pts, q, n, nn_k, ids, \
+                       gids, weights, grad_feat, grad_weights, grad_q, grad_features)
+    if (weighted_first) { if (pgo) PIN_LAUNCH_BWD(true, true); else PIN_LAUNCH_BWD(true, false); }
+    else { if (pgo) PIN_LAUNCH_BWD(false, true); else PIN_LAUNCH_BWD(false, false); }
+#undef PIN_LAUNCH_BWD
+    return launch_status();
+}
+
+int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32_t nn_k, const int64_t* query_ts,
+                      float* certainties, int64_t* ts_update, void* stream) {
+    if (n < 0 || nn_k < 1) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    if (!ids || !weights) return PIN_ERR_ARG;
+    const int64_t total = n * nn_k;
+    hipLaunchKernelGGL(k_train_scatter, grid_for(total), dim3(kBlock), 0, as_stream(stream), ids, weights, total,
+                       nn_k, query_ts, certainties, ts_update);
+    return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+"""Host side of the query kernels: views passed across the C ABI, the autograd
+Function behind ``NeuralPoints.query_feature`` and the fused SDF(+gradient) call
+used by the tracker and mesher paths."""
+import ctypes
+
+import numpy as np
+import torch
+from torch.autograd.function import once_differentiable
+
+from . import _lib
+
+
+class _View:
+    """A ctypes struct plus the tensors it points into (kept alive with it)."""
+
+    def __init__(self, struct, keep):
+        self.struct = struct
+        self.keep = keep
+
+    def ref(self):
+        return ctypes.byref(self.struct)
+
+
+def _f32(t):
+    return None if t is None else t.detach().to(torch.float32).contiguous()
+
+
+def hash_view(nm) -> _View:
+    table = nm.buffer_pt_index
+    cells = nm._cell_table()
+    s = _lib.PinHash(table=table.data_ptr(), buffer_size=nm.buffer_size,
+                     resolution=float(np.float32(nm.resolution)), num_cells=int(nm.neighbor_K),
+                     cells=cells.data_ptr(), max_valid_dist2=float(np.float32(nm.max_valid_dist2)), reserved=0)
+    return _View(s, (table, cells))
+
+
+def points_view(records, features, positions, orientations, certainties, after_pgo) -> _View:
+    features = _f32(features)
+    positions = _f32(positions)
+    orientations = _f32(orientations) if after_pgo else None
+    certainties = _f32(certainties)
+    s = _lib.PinPoints(records=records.data_ptr(), num_points=records.shape[0], features=features.data_ptr(),
+                       positions=positions.data_ptr() if positions is not None else None,
+                       orientations=orientations.data_ptr() if orientations is not None else None,
+                       certainties=certainties.data_ptr() if certainties is not None else None,
+                       rows=features.shape[0], after_pgo=int(bool(after_pgo)), reserved=0)
+    v = _View(s, (records, features, positions, orientations, certainties))
+    v.features = features
+    return v
+
+
+def mlp_view(decoder) -> _View:
+    """PinMlp over a hidden_level=1, out_dim=1 geo decoder (model/decoder.py:16-57)."""
+    if len(decoder.layers) != 1 or decoder.out_dim != 1 or decoder.layers[0].bias is None:
+        raise NotImplementedError("fused SDF kernels implement geo_mlp_level=1, out_dim=1, bias on")
+    W1 = _f32(decoder.layers[0].weight)
+    if tuple(W1.shape) != (_lib.HIDDEN_DIM, _lib.FEATURE_DIM + 3):
+        raise NotImplementedError("fused SDF kernels implement an 11 -> 64 -> 1 decoder")
+    b1 = _f32(decoder.layers[0].bias)
+    W2 = _f32(decoder.lout.weight)
+    b2 = _f32(decoder.lout.bias)
+    s = _lib.PinMlp(W1=W1.data_ptr(), b1=b1.data_ptr(), W2=W2.data_ptr(), b2=b2.data_ptr(),
+                    sdf_scale=float(np.float32(decoder.sdf_scale)), reserved=0)
+    return _View(s, (W1, b1, W2, b2))
+
+
+class QueryFeatureFn(torch.autograd.Function):
+    """neural_points.py:528-674 forward on the GPU; backward = dL/dq and a float-atomic
+    scatter of dL/dfeatures (the reference's autograd through index_put / gather)."""
+
+    @staticmethod
+    def forward(ctx, q, feats, hv, pv, nn_k, weighted_first):
+        qd = q.detach().to(torch.float32).contiguous()
+        n = qd.shape[0]
+        dev = qd.device
+        D = _lib.FEATURE_DIM + 3
+        feat = torch.empty((n, D) if weighted_first else (n, nn_k, D), dtype=torch.float32, device=dev)
+        weights = torch.empty((n, nn_k), dtype=torch.float32, device=dev)
+        nn_counts = torch.empty((n,), dtype=torch.int64, device=dev)
+        cert = torch.empty((n,), dtype=torch.float32, device=dev)
+        ids = torch.empty((n, nn_k), dtype=torch.int32, device=dev)
+        gids = torch.empty((n, nn_k), dtype=torch.int32, device=dev)
+        _lib.call("pin_query_feature_fwd", hv.ref(), pv.ref(), _lib.ptr(qd), n, nn_k, int(weighted_first),
+                  _lib.ptr(feat), _lib.ptr(weights), _lib.ptr(nn_counts), _lib.ptr(cert), _lib.ptr(ids),
+                  _lib.ptr(gids), _lib.stream())
+        ctx.save_for_backward(qd, ids, gids, weights)
+        ctx.pv = pv
+        ctx.nn_k = nn_k
+        ctx.wf = weighted_first
+        ctx.q_dtype = q.dtype
+        ctx.mark_non_differentiable(nn_counts, cert, ids)
+        return feat, weights, nn_counts, cert, ids
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_feat, g_w, _g_nn, _g_cert, _g_ids):
+        qd, ids, gids, weights = ctx.saved_tensors
+        need_q, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if not (need_q or need_f):
+            return None, None, None, None, None, None
+        n = qd.shape[0]
+        grad_q = torch.empty_like(qd) if need_q else None
+        grad_f = torch.zeros_like(ctx.pv.features) if need_f else None
+        gf = g_feat.contiguous() if g_feat is not None else None
+        gw = g_w.contiguous() if g_w is not None else None
+        _lib.call("pin_query_feature_bwd", ctx.pv.ref(), _lib.ptr(qd), n, ctx.nn_k, int(ctx.wf), _lib.ptr(ids),
+                  _lib.ptr(gids), _lib.ptr(weights), _lib.ptr(gf), _lib.ptr(gw), _lib.ptr(grad_q), _lib.ptr(grad_f),
+                  _lib.stream())
+        if grad_q is not None and ctx.q_dtype != torch.float32:
+            grad_q = grad_q.to(ctx.q_dtype)
+        return grad_q, grad_f, None, None, None, None
+
+
+def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
+              want_certainty=True, nn_k=None, weighted_first=None):
+    """Fused query_feature + Decoder.sdf (+ analytic dSDF/dq) in one kernel.
+
+    Returns (sdf [N], grad [N,3] or None, nn_count [N] int32, certainty [N] or None,
+    sdf_std [N] or None).  Semantics: utils/tracker.py:176-260 (query_locally=True) and
+    utils/mesher.py:41-136 (query_locally=False, zero_empty=True)."""
+    _lib.require_device(points)
+    q = points.detach().to(torch.float32).contiguous()
+    n = q.shape[0]
+    dev = q.device
+    nn_k = int(nm.config.query_nn_k if nn_k is None else nn_k)
+    wf = bool(nm.config.weighted_first if weighted_first is None else weighted_first)
+    hv, pv = nm._views("local" if query_locally else "global", query_locally)
+    mv = mlp_view(decoder)
+    sdf = torch.empty(n, dtype=torch.float32, device=dev)
+    grad = torch.empty((n, 3), dtype=torch.float32, device=dev) if want_grad else None
+    nn_count = torch.empty(n, dtype=torch.int32, device=dev)
+    cert = torch.empty(n, dtype=torch.float32, device=dev) if want_certainty else None
+    std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
+    _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
+              _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
+    if want_std and wf:
+        std = torch.zeros(n, dtype=torch.float32, device=dev)
+    return sdf, grad, nn_count, cert, std

@@ -1,0 +1,55 @@
+"""Synthetic workloads of SURVEY.md 8(d) (the KITTI example data is not available offline).
+
+Map: one neural point per ``res`` voxel column on z = 0.5 sin(x/7) cos(y/5) + 0.15 over
+an n x n grid, xy = (i + 0.5) * res; features ~ N(0, 0.05^2) (the reference default
+feature_std = 0 would make the benchmark degenerate); decoder = nn.Linear default init
+under torch.manual_seed(seed).  Queries: random map points + N(0, sigma^2) per axis.
+"""
+import torch
+
+from .config import Config
+from .decoder import Decoder
+from .neural_points import NeuralPoints
+
+
+def surface_points(n_side, res=0.3):
+    i = torch.arange(n_side, dtype=torch.float64)
+    x, y = torch.meshgrid((i + 0.5) * res, (i + 0.5) * res, indexing="ij")
+    x, y = x.reshape(-1), y.reshape(-1)
+    z = 0.5 * torch.sin(x / 7.0) * torch.cos(y / 5.0) + 0.15
+    return torch.stack([x, y, z], 1).to(torch.float32)
+
+
+def surface_map(n_side, res=0.3, seed=42, device="cuda", buffer_size=int(5e7), nn_k=8, weighted_first=True,
+                feature_std=0.05, num_nei_cells=2, search_alpha=0.2, **cfg_kw):
+    """Returns (NeuralPoints with the whole map local, Decoder, host points [M,3])."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    pts = surface_points(n_side, res)
+    cfg = Config(device=device, voxel_size_m=res, buffer_size=buffer_size, query_nn_k=nn_k,
+                 weighted_first=weighted_first, local_map_radius=1e9, num_nei_cells=num_nei_cells,
+                 search_alpha=search_alpha, **cfg_kw)
+    nm = NeuralPoints(cfg)
+    M = pts.shape[0]
+    nm.neural_points = pts.to(device)
+    quat = torch.zeros(M, 4, device=device)
+    quat[:, 0] = 1.0
+    nm.point_orientations = quat
+    nm.point_ts_create = torch.zeros(M, dtype=torch.int64, device=device)
+    nm.point_ts_update = torch.zeros(M, dtype=torch.int64, device=device)
+    feats = torch.randn(M + 1, 8, generator=g) * feature_std
+    feats[-1] = 0
+    nm.geo_features = feats.to(device)
+    nm.point_certainties = (torch.rand(M, generator=g) * 10).to(device)
+    nm.travel_dist = torch.zeros(1, device=device)
+    nm.rebuild_hash()
+    nm.reset_local_map(torch.zeros(3, device=device), torch.eye(3, device=device), 0)
+    torch.manual_seed(seed)
+    dec = Decoder(cfg, 64, 1, 1)
+    return nm, dec, pts
+
+
+def surface_queries(pts, n, seed=7, sigma=0.25, device="cuda"):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    idx = torch.randint(0, pts.shape[0], (n,), generator=g)
+    q = pts[idx] + torch.randn(n, 3, generator=g) * sigma
+    return q.to(device)

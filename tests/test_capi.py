@@ -1,0 +1,75 @@
+"""CPU checks of the native boundary and host logic (no GPU calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import torch
+
+from oracle import pin_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "pin_slam_amd.h")).read()
+    return sorted(set(re.findall(r"^int (pin_\w+)\(", hdr, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pin_slam_amd import _lib
+    lib = _lib.load()
+    decl = declared_symbols()
+    assert decl, "no entry points parsed from the header"
+    for name in decl:
+        assert hasattr(lib, name), f"{name} declared in include/pin_slam_amd.h but not exported"
+    assert sorted(_lib.exported_symbols()) == decl, "ctypes signature table out of sync with the header"
+
+
+def test_struct_layouts_match_header():
+    from pin_slam_amd import _lib
+    # field order/size as declared in include/pin_slam_amd.h (x86-64 SysV layout)
+    assert ctypes.sizeof(_lib.PinHash) == 8 + 8 + 4 + 4 + 8 + 4 + 4
+    assert ctypes.sizeof(_lib.PinPoints) == 8 * 7 + 4 + 4
+    assert ctypes.sizeof(_lib.PinMlp) == 8 * 4 + 4 + 4
+
+
+def test_neighbor_offsets_host(golden):
+    from pin_slam_amd.neural_points import neighbor_offsets
+    z = golden("neighborhoods")
+    for key in [k for k in z if k.endswith("_dx")]:
+        c, a = key.split("_")[:2]
+        got = neighbor_offsets(int(c[1:]), int(a[1:]) / 10).numpy()
+        np.testing.assert_array_equal(got, z[key])
+
+
+def test_hash_slots_host_matches_oracle():
+    from pin_slam_amd.neural_points import hash_slots
+    rng = np.random.default_rng(0)
+    p = rng.uniform(-500, 500, (10000, 3)).astype(np.float32)
+    for B in (1 << 17, int(5e7)):
+        got = hash_slots(torch.from_numpy(p), 0.3, B).numpy()
+        np.testing.assert_array_equal(got, O.hash_slots(O.voxel_coords(p, 0.3), B))
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from pin_slam_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    try:
+        _lib.load()
+    except RuntimeError as e:
+        assert "no fallback" in str(e)
+    else:
+        raise AssertionError("load() must raise when the native library is missing")
+
+
+def test_cpu_tensors_are_rejected():
+    import pin_slam_amd as P
+    nm = P.NeuralPoints(P.Config(device="cpu", buffer_size=1 << 10))
+    try:
+        nm.query_feature(torch.zeros(4, 3))
+    except RuntimeError as e:
+        assert "ROCm device" in str(e)
+    else:
+        raise AssertionError("CPU tensors must not silently run a fallback")
