@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nwf", action="store_true", help="weighted_first=False variant (per-neighbour decoding)")
+    ap.add_argument("--backend", default="auto", choices=["auto", "hash", "grid"])
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per launch (from profiles/), reported as roofline.traffic")
     return ap.parse_args()
@@ -84,8 +85,18 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device(dev))
     wf = not args.nwf
-    nm, dec, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf)
+    nm, dec, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf,
+                               query_backend=args.backend)
     q = surface_queries(pts, N_QUERY, seed=7 + rank, device=dev)
+    # derived map state (occupancy grid + compact records) is built once per map version,
+    # like the hash table itself; time it separately
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    backend = nm.backend()
+    if backend == "grid":
+        nm.compact_records("global", True)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - tb) * 1e3
 
     def step():
         return P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False,
@@ -132,7 +143,8 @@ def main():
         "config": {"workload": "SDF+analytic-grad, 1M-point surface map, 262144 queries/step/GPU (configs[1])",
                    "map_points": int(pts.shape[0]), "queries_per_step_per_gpu": N_QUERY, "Kc": int(nm.neighbor_K),
                    "nn_k": 8, "feature_dim": 8, "mlp": "11-64-1", "weighted_first": wf,
-                   "buffer_size": int(nm.buffer_size), "parallelism": f"replicas x{world}"},
+                   "buffer_size": int(nm.buffer_size), "parallelism": f"replicas x{world}",
+                   "candidate_backend": backend, "map_index_build_ms": round(build_ms, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": args.traffic_bytes,

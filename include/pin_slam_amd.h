@@ -39,7 +39,7 @@ typedef struct PinHash {
     int64_t buffer_size;         /* B, < 2^31 */
     float resolution;            /* voxel size; points are floor(p / resolution) in f32 */
     int32_t num_cells;           /* Kc */
-    const int32_t* cells;        /* [Kc,4]: dx, dy, dz, floor_mod(dx*p0+dy*p1+dz*p2, B) */
+    const int32_t* cells;        /* [pin_cells_padded(Kc)]: floor_mod(dx*p0+dy*p1+dz*p2, B) per cell, 0-padded */
     float max_valid_dist2;       /* candidates with dist2 > this are rejected (f32 compare) */
     int32_t reserved;
 } PinHash;
@@ -56,6 +56,27 @@ typedef struct PinPoints {
     int32_t after_pgo;           /* rotate neighbour vectors (model/neural_points.py:606-607) */
     int32_t reserved;
 } PinPoints;
+
+/* Occupancy-grid box: origin cell (ox,oy,oz) and extent in 4x4x4-cell bricks. */
+typedef struct PinGridDims {
+    int64_t ox, oy, oz;
+    int32_t nbx, nby, nbz;
+    int32_t reserved;
+} PinGridDims;
+
+/* Occupancy grid + compact 64-byte records (see pin_grid_mark / pin_grid_fill). */
+typedef struct PinGrid {
+    const uint32_t* bricks;      /* [nb,4]: bits lo, bits hi, exclusive prefix, 0 */
+    PinGridDims dims;
+    const float* crec;           /* [n_occ,16]: {x,y,z,bits(id)} {f0..f3} {f4..f7} {certainty,0,0,0} */
+    const int32_t* cgid;         /* [n_occ] global point index of each compact record */
+    int64_t n_occ;
+    const int32_t* offsets;      /* [pin_cells_padded(Kc)] packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 */
+    float resolution;
+    int32_t num_cells;           /* Kc, reference cell order (model/neural_points.py:430-439) */
+    float max_valid_dist2;
+    int32_t fat;                 /* 1: features/certainty read from crec; 0: from PinPoints */
+} PinGrid;
 
 /* Geo decoder, hidden_level = 1 (model/decoder.py:16-88). */
 typedef struct PinMlp {
@@ -83,7 +104,11 @@ int pin_build_records(const float* positions, int64_t num_points, int32_t query_
                       int64_t travel_len, int64_t cur_ts, float diff_travel_dist_local,
                       const float* local_positions, int64_t local_rows, float* records, void* stream);
 
-/* pin_neighbor_cells -- fill the [Kc,4] cell table from host offsets [Kc,3] (neural_points.py:430-439). */
+/* Cell-delta table length for Kc cells: Kc rounded up to a multiple of 16. */
+static inline int32_t pin_cells_padded(int32_t num_cells) { return (num_cells + 15) / 16 * 16; }
+
+/* pin_neighbor_cells -- fill the cell-delta table (pin_cells_padded(Kc) int32) from host
+ * offsets [Kc,3] (neural_points.py:430-439): slot(cell + dx) = floor_mod(base + delta, B). */
 int pin_neighbor_cells(const int32_t* host_dx, int32_t num_cells, int64_t buffer_size,
                        int32_t* cells_out, void* stream);
 
@@ -146,6 +171,43 @@ int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32
  */
 int pin_query_certainty(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n,
                         float* certainty_out, void* stream);
+
+/* Workspace bytes pin_grid_mark needs for a grid of nb bricks. */
+static inline int64_t pin_grid_workspace_bytes(int64_t num_bricks) {
+    return ((num_bricks + 4095) / 4096) * 4 + 16;
+}
+
+/*
+ * pin_grid_mark -- build the occupancy bricks of the map box: bit(cell) = 1 iff some point g
+ * has floor(p_g / res) == cell and table[slot(cell)] == g ("own-cell" entries), then the
+ * per-brick exclusive prefix of the bit counts.  counters[0] = own-cell entries marked,
+ * counters[1] = occupied table slots.  The grid equals the table on every candidate that
+ * can pass the distance test iff counters[0] == counters[1] (no displaced entries, e.g.
+ * after adjust_map without recreate_hash) and no two cells within the reachable window
+ * collide under the hash (host check).  workspace: pin_grid_workspace_bytes(nb) bytes.
+ */
+int pin_grid_mark(const float* positions, int64_t num_points, float resolution, const int32_t* table,
+                  int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks, unsigned long long* counters,
+                  void* workspace, void* stream);
+
+/*
+ * pin_grid_fill -- compact records in brick order for one query mode: crec[rank(cell_g)] =
+ * {record_g, features[id_g], certainty[id_g]} and cgid[rank] = g, for every own-cell point.
+ */
+int pin_grid_fill(const float* positions, int64_t num_points, float resolution, const int32_t* table,
+                  int64_t buffer_size, const PinGridDims* dims, const uint32_t* bricks, const float* records,
+                  const float* features, const float* certainties, float* crec, int32_t* cgid, void* stream);
+
+/* pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid. */
+int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
+                       int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
+                       int32_t* nn_count, float* certainty, float* sdf_std, void* stream);
+
+/* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
+ * (features always read live from pts->features; gids from grid->cgid). */
+int pin_query_feature_fwd_grid(const PinGrid* grid, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,
+                               int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts,
+                               float* certainty, int32_t* ids, int32_t* gids, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,16 @@ class PinPoints(ctypes.Structure):
                 ("reserved", i32)]
 
 
+class PinGridDims(ctypes.Structure):
+    _fields_ = [("ox", i64), ("oy", i64), ("oz", i64), ("nbx", i32), ("nby", i32), ("nbz", i32), ("reserved", i32)]
+
+
+class PinGrid(ctypes.Structure):
+    _fields_ = [("bricks", c_void_p), ("dims", PinGridDims), ("crec", c_void_p), ("cgid", c_void_p), ("n_occ", i64),
+                ("offsets", c_void_p), ("resolution", f32), ("num_cells", i32), ("max_valid_dist2", f32),
+                ("fat", i32)]
+
+
 class PinMlp(ctypes.Structure):
     _fields_ = [("W1", c_void_p), ("b1", c_void_p), ("W2", c_void_p), ("b2", c_void_p), ("sdf_scale", f32),
                 ("reserved", i32)]
@@ -57,6 +67,13 @@ _SIGS = {
                               c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_scatter": [c_void_p, c_void_p, i64, i32, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_certainty": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p],
+    "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_grid_fill": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p,
+                      c_void_p, c_void_p, c_void_p],
+    "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
 }
 
 _lib = None

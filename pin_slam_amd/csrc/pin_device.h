@@ -49,63 +49,164 @@ struct TopK {
 #pragma unroll
         for (int j = 0; j < kK; ++j) { d[j] = kInvalidDist2; g[j] = -1; }
     }
+    // Branch-free insertion (pure selects).  x = +inf is a no-op, so callers insert every
+    // candidate unconditionally with rejected ones mapped to +inf.
     __device__ __forceinline__ void insert(float x, int gi) {
         bool c[kK];
 #pragma unroll
         for (int j = 0; j < kK; ++j) c[j] = d[j] <= x;
 #pragma unroll
         for (int j = kK - 1; j > 0; --j) {
-            const float nd = c[j] ? d[j] : (c[j - 1] ? x : d[j - 1]);
-            const int ng = c[j] ? g[j] : (c[j - 1] ? gi : g[j - 1]);
-            d[j] = nd;
-            g[j] = ng;
+            const float dj = c[j - 1] ? x : d[j - 1];
+            const int gj = c[j - 1] ? gi : g[j - 1];
+            d[j] = c[j] ? d[j] : dj;
+            g[j] = c[j] ? g[j] : gj;
         }
-        if (!c[0]) { d[0] = x; g[0] = gi; }
+        d[0] = c[0] ? d[0] : x;
+        g[0] = c[0] ? g[0] : gi;
     }
 };
 
-// Probe every neighbour cell of q, reject empty / filtered / too-far candidates and keep
-// the k nearest (neural_points.py:459-509, :555-565).  Returns nn_count (valid candidates
-// before truncation, :557).  CH table probes are issued before their records are read.
-template <int CH>
-__device__ __forceinline__ int scan_candidates(const PinHash& h, const float4* __restrict__ rec,
-                                               float qx, float qy, float qz, TopK& tk) {
-    const uint32_t B = (uint32_t)h.buffer_size;
-    const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
-    const float maxd2 = h.max_valid_dist2;
-    const int Kc = h.num_cells;
-    int nn = 0;
-    for (int c0 = 0; c0 < Kc; c0 += CH) {
-        int gi[CH];
+// ---------------------------------------------------------------------------------------
+// Candidate sources.  Both enumerate the neighbour cells of q in the reference's cell order
+// (model/neural_points.py:430-439), reject empty / filtered / too-far candidates, keep the
+// k nearest in a TopK whose payload is source specific, and return nn_count (valid
+// candidates before truncation, :557).  Latency structure per chunk of CH cells: the CH
+// cell lookups are issued back to back, then the CH record gathers are issued back to back
+// with clamped (never branched) addresses -- an empty cell reads entry 0, a hot line -- so
+// each chunk costs two memory round trips, not 2*CH.
+
+// The reference structure: hash every neighbour cell into the slot table (:465-476).
+// Payload = global point index; records indexed by it.
+struct HashSource {
+    const PinHash& h;
+    const PinPoints& p;
+    __device__ HashSource(const PinHash& h_, const PinPoints& p_) : h(h_), p(p_) {}
+
+    template <int CH>
+    __device__ __forceinline__ int scan(float qx, float qy, float qz, TopK& tk) const {
+        const float4* __restrict__ rec = (const float4*)p.records;
+        const uint32_t B = (uint32_t)h.buffer_size;
+        const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
+        const float maxd2 = h.max_valid_dist2;
+        const int Kc = h.num_cells;
+        const int32_t* __restrict__ delta = h.cells;  // padded to a multiple of 16 entries
+        const int32_t* __restrict__ table = h.table;
+        int nn = 0;
+        for (int c0 = 0; c0 < Kc; c0 += CH) {
+            int dl[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            gi[t] = -1;
-            if (c0 + t < Kc) {
-                uint32_t s = base + (uint32_t)h.cells[4 * (c0 + t) + 3];
+            for (int t = 0; t < CH; ++t) dl[t] = delta[c0 + t];
+            int gi[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                uint32_t s = base + (uint32_t)dl[t];
                 s = s >= B ? s - B : s;
-                gi[t] = h.table[s];
+                gi[t] = (c0 + t < Kc) ? table[s] : -1;
             }
-        }
-        float4 r[CH];
+            float4 r[CH];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            r[t] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-            if (gi[t] >= 0) r[t] = rec[gi[t]];
-        }
+            for (int t = 0; t < CH; ++t) r[t] = rec[gi[t] > 0 ? gi[t] : 0];
 #pragma unroll
-        for (int t = 0; t < CH; ++t) {
-            const int id = __float_as_int(r[t].w);
-            if (gi[t] >= 0 && id != -1) {
+            for (int t = 0; t < CH; ++t) {
+                const int id = __float_as_int(r[t].w);
                 const float d2 = dist2(r[t].x, r[t].y, r[t].z, qx, qy, qz);
-                if (d2 <= maxd2) {
-                    ++nn;
-                    tk.insert(d2, gi[t]);
-                }
+                const bool ok = gi[t] >= 0 && id != -1 && d2 <= maxd2;
+                nn += ok ? 1 : 0;
+                tk.insert(ok ? d2 : INFINITY, gi[t]);
             }
+        }
+        return nn;
+    }
+    __device__ __forceinline__ float4 record(int pay) const { return ((const float4*)p.records)[pay > 0 ? pay : 0]; }
+    __device__ __forceinline__ void features(int pay, int64_t id, float4& f0, float4& f1) const {
+        const float4* __restrict__ feat = (const float4*)p.features;
+        f0 = feat[2 * id];
+        f1 = feat[2 * id + 1];
+    }
+    __device__ __forceinline__ float certainty(int pay, int64_t id) const { return p.certainties[id]; }
+    __device__ __forceinline__ int gid(int pay) const { return pay; }
+};
+
+// The occupancy grid (pin_grid.hip): cell -> brick bit -> rank -> 64-byte compact record.
+// Payload = compact record index.  FAT: features / certainty come from the compact record
+// (one line per candidate); otherwise from the live PinPoints arrays.
+template <bool FAT>
+struct GridSource {
+    const PinGrid& gr;
+    const PinPoints& p;
+    __device__ GridSource(const PinGrid& g_, const PinPoints& p_) : gr(g_), p(p_) {}
+
+    template <int CH>
+    __device__ __forceinline__ int scan(float qx, float qy, float qz, TopK& tk) const {
+        const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
+        const float4* __restrict__ crec = (const float4*)gr.crec;
+        const int32_t* __restrict__ offs = gr.offsets;  // padded to a multiple of 16 entries
+        const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
+        const int64_t lx = (int64_t)floorf(qx / res) - gr.dims.ox;
+        const int64_t ly = (int64_t)floorf(qy / res) - gr.dims.oy;
+        const int64_t lz = (int64_t)floorf(qz / res) - gr.dims.oz;
+        const int64_t ex = 4ll * gr.dims.nbx, ey = 4ll * gr.dims.nby, ez = 4ll * gr.dims.nbz;
+        const int Kc = gr.num_cells;
+        int nn = 0;
+        for (int c0 = 0; c0 < Kc; c0 += CH) {
+            int of[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) of[t] = offs[c0 + t];
+            uint4 w[CH];
+            int bit[CH];
+            bool in[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int64_t cx = lx + ((of[t] & 255) - 128);
+                const int64_t cy = ly + (((of[t] >> 8) & 255) - 128);
+                const int64_t cz = lz + (((of[t] >> 16) & 255) - 128);
+                in[t] = (c0 + t < Kc) && cx >= 0 && cy >= 0 && cz >= 0 && cx < ex && cy < ey && cz < ez;
+                const int64_t b = in[t] ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * (int64_t)gr.dims.nbx + (cx >> 2) : 0;
+                bit[t] = (int)(((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3));
+                w[t] = bricks[b];
+            }
+            int ci[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const uint64_t bits = ((uint64_t)w[t].y << 32) | w[t].x;
+                const bool set = in[t] && ((bits >> bit[t]) & 1ull);
+                ci[t] = set ? (int)(w[t].z + (uint32_t)__popcll(bits & ((1ull << bit[t]) - 1ull))) : -1;
+            }
+            float4 r[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) r[t] = crec[4 * (int64_t)(ci[t] > 0 ? ci[t] : 0)];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int id = __float_as_int(r[t].w);
+                const float d2 = dist2(r[t].x, r[t].y, r[t].z, qx, qy, qz);
+                const bool ok = ci[t] >= 0 && id != -1 && d2 <= maxd2;
+                nn += ok ? 1 : 0;
+                tk.insert(ok ? d2 : INFINITY, ci[t]);
+            }
+        }
+        return nn;
+    }
+    __device__ __forceinline__ float4 record(int pay) const {
+        return ((const float4*)gr.crec)[4 * (int64_t)(pay > 0 ? pay : 0)];
+    }
+    __device__ __forceinline__ void features(int pay, int64_t id, float4& f0, float4& f1) const {
+        if (FAT) {
+            const float4* r = (const float4*)gr.crec + 4 * (int64_t)(pay > 0 ? pay : 0);
+            f0 = r[1];
+            f1 = r[2];
+        } else {
+            const float4* __restrict__ feat = (const float4*)p.features;
+            f0 = feat[2 * id];
+            f1 = feat[2 * id + 1];
         }
     }
-    return nn;
-}
+    __device__ __forceinline__ float certainty(int pay, int64_t id) const {
+        if (FAT) return ((const float4*)gr.crec)[4 * (int64_t)(pay > 0 ? pay : 0) + 3].x;
+        return p.certainties[id];
+    }
+    __device__ __forceinline__ int gid(int pay) const { return pay >= 0 ? gr.cgid[pay] : -1; }
+};
 
 // passive quaternion rotation, utils/tools.py:316-323 (same op order)
 __device__ __forceinline__ void quat_rotate_passive(float4 qt, float& vx, float& vy, float& vz) {
@@ -121,6 +222,14 @@ __device__ __forceinline__ void quat_rotate_passive(float4 qt, float& vx, float&
     vz = (vz + w * tz) + cz;
 }
 
+// active rotation matrix R(q) (w,x,y,z); the passive rotation of tools.py:316 is R(q)^T v
+__device__ __forceinline__ void quat_rotmat(float4 qt, float (&R)[3][3]) {
+    const float w = qt.x, x = qt.y, y = qt.z, z = qt.w;
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - w * z); R[0][2] = 2.f * (x * z + w * y);
+    R[1][0] = 2.f * (x * y + w * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - w * x);
+    R[2][0] = 2.f * (x * z - w * y); R[2][1] = 2.f * (y * z + w * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+}
+
 // R(q) g: transpose of the passive rotation's Jacobian applied to g (d vec/dq = R(q)^T)
 __device__ __forceinline__ void quat_rotate_active(float4 qt, float gx, float gy, float gz, float& ox, float& oy,
                                                    float& oz) {
@@ -130,69 +239,101 @@ __device__ __forceinline__ void quat_rotate_active(float4 qt, float gx, float gy
     oz = 2.f * (x * z - w * y) * gx + 2.f * (y * z + w * x) * gy + (1.f - 2.f * (x * x + y * y)) * gz;
 }
 
-// Neighbour set of one query after the scan (weights and distance terms only; feature
-// rows are streamed per neighbour by neighbour_input so they never stay live).
+// Neighbour set of one query after the scan (weights, distance terms, neighbour vectors;
+// feature rows are gathered by gather_inputs when needed so they do not stay live).
 struct Neighbours {
     float w[kK];      // normalised IDW weights (0 for invalid)
     float u[kK];      // un-normalised 1/(d2+eps) (0 for invalid)
     float S;          // sum of u
     float pg[kK][3];  // q - global position (drives the distance gradient)
+    float v[kK][3];   // q - local position (decoder input before the optional rotation)
     int id[kK];       // feature row, -1 invalid
-    int raw[kK];      // record id bits (flag = local position differs from the global one)
+    int pay[kK];      // source payload of the candidate (global index or compact record)
 };
 
-// neural_points.py:618-632 on the top-k: u = 1/(d2+eps), S = sum u, w = u/S (0 when invalid)
-__device__ __forceinline__ void load_topk(const PinPoints& p, const TopK& tk, int nn, int nn_k, float qx, float qy,
-                                          float qz, Neighbours& nb) {
-    const float4* __restrict__ rec = (const float4*)p.records;
+// neural_points.py:618-632 on the top-k: u = 1/(d2+eps), S = sum u, w = u/S (0 when invalid).
+// All record gathers are unconditional; the rare "unfaithful" records (local position !=
+// global one, the global2local quirk) take a wave-uniform branch for their extra gather.
+template <class Src>
+__device__ __forceinline__ void load_topk(const Src& src, const PinPoints& p, const TopK& tk, int nn, int nn_k,
+                                          float qx, float qy, float qz, Neighbours& nb) {
     float4 r[kK];
 #pragma unroll
-    for (int j = 0; j < kK; ++j) {
-        r[j] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-        if (j < nn_k && tk.g[j] >= 0) r[j] = rec[tk.g[j]];
-    }
+    for (int j = 0; j < kK; ++j) r[j] = src.record(tk.g[j]);
     float S = 0.f;
+    bool unf = false;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         const int raw = __float_as_int(r[j].w);
         const bool valid = j < nn_k && tk.g[j] >= 0;
-        nb.raw[j] = raw;
         nb.id[j] = valid ? (raw & kIdMask) : -1;
+        nb.pay[j] = valid ? tk.g[j] : -1;
+        unf |= valid && (raw & PIN_RECORD_UNFAITHFUL);
         nb.u[j] = valid ? 1.0f / (tk.d[j] + kIdwEps) : 0.f;
         S = S + nb.u[j];
         nb.pg[j][0] = qx - r[j].x;
         nb.pg[j][1] = qy - r[j].y;
         nb.pg[j][2] = qz - r[j].z;
+        nb.v[j][0] = nb.pg[j][0];
+        nb.v[j][1] = nb.pg[j][1];
+        nb.v[j][2] = nb.pg[j][2];
     }
     nb.S = S;
 #pragma unroll
     for (int j = 0; j < kK; ++j) nb.w[j] = (nb.id[j] >= 0 && nn > 0) ? nb.u[j] / S : 0.f;
+    if (__any(unf)) {
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            const int raw = __float_as_int(r[j].w);
+            if (nb.id[j] >= 0 && (raw & PIN_RECORD_UNFAITHFUL)) {
+                const int64_t id = nb.id[j];
+                nb.v[j][0] = qx - p.positions[3 * id];
+                nb.v[j][1] = qy - p.positions[3 * id + 1];
+                nb.v[j][2] = qz - p.positions[3 * id + 2];
+            }
+        }
+    }
 }
 
-// Decoder input of neighbour j: feature row and neighbour vector q - p (local position,
-// passively rotated by the point's quaternion after pgo: neural_points.py:577-608).
-template <bool PGO>
-__device__ __forceinline__ void neighbour_input(const PinPoints& p, const Neighbours& nb, int j, float qx, float qy,
-                                                float qz, float (&x)[kD], float4& quat) {
-    const int64_t id = nb.id[j];
-    const float4* fr = (const float4*)(p.features + id * kF);
-    const float4 f0 = fr[0], f1 = fr[1];
-    x[0] = f0.x; x[1] = f0.y; x[2] = f0.z; x[3] = f0.w;
-    x[4] = f1.x; x[5] = f1.y; x[6] = f1.z; x[7] = f1.w;
-    if (nb.raw[j] & PIN_RECORD_UNFAITHFUL) {
-        x[8] = qx - p.positions[3 * id];
-        x[9] = qy - p.positions[3 * id + 1];
-        x[10] = qz - p.positions[3 * id + 2];
-    } else {
-        x[8] = nb.pg[j][0];
-        x[9] = nb.pg[j][1];
-        x[10] = nb.pg[j][2];
+// Decoder inputs of neighbours [J0, J0+NJ): feature rows (2 x 16 B each) and neighbour
+// vectors, passively rotated by the point quaternion after pgo (neural_points.py:577-614).
+// Gathers are unconditional (invalid neighbours read row 0) and zeroed afterwards.
+template <bool PGO, int J0, int NJ, class Src>
+__device__ __forceinline__ void gather_inputs(const Src& src, const PinPoints& p, const Neighbours& nb,
+                                              float (&x)[NJ][kD], float4 (&quat)[NJ]) {
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+        const int j = J0 + t;
+        const int64_t id = nb.id[j] > 0 ? nb.id[j] : 0;
+        float4 f0, f1;
+        src.features(nb.pay[j], id, f0, f1);
+        x[t][0] = f0.x; x[t][1] = f0.y; x[t][2] = f0.z; x[t][3] = f0.w;
+        x[t][4] = f1.x; x[t][5] = f1.y; x[t][6] = f1.z; x[t][7] = f1.w;
+        x[t][8] = nb.v[j][0];
+        x[t][9] = nb.v[j][1];
+        x[t][10] = nb.v[j][2];
+        quat[t] = make_float4(1.f, 0.f, 0.f, 0.f);
+        if (PGO) quat[t] = ((const float4*)p.orientations)[id];
     }
-    quat = make_float4(1.f, 0.f, 0.f, 0.f);
-    if (PGO) {
-        quat = ((const float4*)p.orientations)[id];
-        quat_rotate_passive(quat, x[8], x[9], x[10]);
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+        const bool valid = nb.id[J0 + t] >= 0;
+        if (PGO) quat_rotate_passive(quat[t], x[t][8], x[t][9], x[t][10]);
+#pragma unroll
+        for (int d = 0; d < kD; ++d) x[t][d] = valid ? x[t][d] : 0.f;
     }
+}
+
+// sum_j cert_j * w_j with unconditional gathers (neural_points.py:651-656)
+template <class Src>
+__device__ __forceinline__ float gather_certainty(const Src& src, const Neighbours& nb) {
+    float c[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) c[j] = src.certainty(nb.pay[j], nb.id[j] > 0 ? nb.id[j] : 0);
+    float cert = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) cert = cert + (nb.id[j] >= 0 ? c[j] : 0.f) * nb.w[j];
+    return cert;
 }
 
 // Decoder forward fused with its input gradient (model/decoder.py:66-88):
@@ -203,7 +344,7 @@ __device__ __forceinline__ float mlp_sdf(const PinMlp& m, const float (&x)[kD], 
     float out = 0.f;
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) gx[i] = 0.f;
-#pragma unroll 8
+#pragma unroll 2
     for (int c = 0; c < kH; ++c) {
         const float* wr = m.W1 + c * kD;
         float acc = 0.f;

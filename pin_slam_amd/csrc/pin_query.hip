@@ -77,7 +77,7 @@ k_radius_search(const PinHash h, const float4* __restrict__ rec, const float* __
     const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
     const int Kc = h.num_cells;
     for (int c = 0; c < Kc; ++c) {
-        uint32_t s = base + (uint32_t)h.cells[4 * c + 3];
+        uint32_t s = base + (uint32_t)h.cells[c];
         s = s >= B ? s - B : s;
         int g = h.table[s];
         float d2 = h.max_valid_dist2;
@@ -106,7 +106,7 @@ k_query_certainty(const PinHash h, const float4* __restrict__ rec, const float* 
     const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
     float m = -INFINITY;
     for (int c = 0; c < h.num_cells; ++c) {
-        uint32_t s = base + (uint32_t)h.cells[4 * c + 3];
+        uint32_t s = base + (uint32_t)h.cells[c];
         s = s >= B ? s - B : s;
         const int g = h.table[s];
         float val = 0.f;
@@ -121,69 +121,90 @@ k_query_certainty(const PinHash h, const float4* __restrict__ rec, const float* 
 
 // ------------------------------------------------------------------ fused SDF (+grad)
 // Tracker / mesher inference: query_feature + Decoder.sdf + get_gradient in one pass.
-template <bool WF, bool PGO, bool GRAD>
-__global__ void __launch_bounds__(kBlock)
-k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n, int nn_k,
-            int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out, int* __restrict__ nn_out,
-            float* __restrict__ cert_out, float* __restrict__ std_out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+template <bool WF, bool PGO, bool GRAD, class Src>
+__device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const PinMlp& m,
+                                               const float* __restrict__ q, int64_t i, int nn_k, int zero_empty,
+                                               float* __restrict__ sdf_out, float* __restrict__ grad_out,
+                                               int* __restrict__ nn_out, float* __restrict__ cert_out,
+                                               float* __restrict__ std_out) {
     const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
     TopK tk;
     tk.init();
-    const int nn = scan_candidates<kChunk>(h, (const float4*)p.records, qx, qy, qz, tk);
+    const int nn = src.template scan<kChunk>(qx, qy, qz, tk);
     Neighbours nb;
-    load_topk(p, tk, nn, nn_k, qx, qy, qz, nb);
-
-    float cert = 0.f;
-#pragma unroll
-    for (int j = 0; j < kK; ++j) {
-        const float c = nb.id[j] >= 0 ? p.certainties[nb.id[j]] : 0.f;
-        cert = cert + c * nb.w[j];
-    }
+    load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
+    const float cert = cert_out ? gather_certainty(src, nb) : 0.f;
+    // c_j = d w_j-part: -2 u_j^2 (q - p_j) / S   (du_j/dq scaled by 1/S; 0 for invalid)
+    const float invS = nn > 0 ? 1.f / nb.S : 0.f;
 
     float sdf = 0.f, std_v = 0.f;
     float gq[3] = {0.f, 0.f, 0.f};
     if constexpr (WF) {
-        // x = sum_j w_j [f_j, v_j]   (neural_points.py:660-662)
-        float x[kD];
+        // One pass over the neighbours accumulates
+        //   x  = sum_j w_j x_j                      (neural_points.py:660-662)
+        //   J  = sum_j x_j (x) c_j,  C = sum_j c_j   so that  sum_j (a_j - abar) c_j = J^T gx - (gx.x) C
+        //   Wr = sum_j w_j R_j  (rotation term of d x / d q after pgo; scalar sum w otherwise)
+        float x[kD], J[kD][3], C[3] = {0.f, 0.f, 0.f}, Wr[3][3];
 #pragma unroll
-        for (int d = 0; d < kD; ++d) x[d] = 0.f;
+        for (int d = 0; d < kD; ++d) { x[d] = 0.f; J[d][0] = J[d][1] = J[d][2] = 0.f; }
 #pragma unroll
-        for (int j = 0; j < kK; ++j) {
-            if (nb.id[j] < 0) continue;
-            float xj[kD];
-            float4 qt;
-            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
+        for (int a = 0; a < 3; ++a) Wr[a][0] = Wr[a][1] = Wr[a][2] = 0.f;
 #pragma unroll
-            for (int d = 0; d < kD; ++d) x[d] = x[d] + xj[d] * nb.w[j];
+        for (int half = 0; half < kK / 4; ++half) {
+            float xk[4][kD];
+            float4 qt[4];
+            if (half == 0) gather_inputs<PGO, 0, 4>(src, p, nb, xk, qt);
+            else gather_inputs<PGO, 4, 4>(src, p, nb, xk, qt);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int j = half * 4 + t;
+#pragma unroll
+                for (int d = 0; d < kD; ++d) x[d] = x[d] + xk[t][d] * nb.w[j];
+                if (GRAD) {
+                    const float cu = -2.f * nb.u[j] * nb.u[j] * invS;
+                    const float c3[3] = {cu * nb.pg[j][0], cu * nb.pg[j][1], cu * nb.pg[j][2]};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) C[a] += c3[a];
+#pragma unroll
+                    for (int d = 0; d < kD; ++d) {
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) J[d][a] = fmaf(xk[t][d], c3[a], J[d][a]);
+                    }
+                    if (PGO) {
+                        float R[3][3];
+                        quat_rotmat(qt[t], R);
+#pragma unroll
+                        for (int a = 0; a < 3; ++a)
+#pragma unroll
+                            for (int b = 0; b < 3; ++b) Wr[a][b] = fmaf(nb.w[j], R[a][b], Wr[a][b]);
+                    } else {
+                        Wr[0][0] += nb.w[j];
+                    }
+                }
+            }
         }
         float gx[kD];
         sdf = mlp_sdf<GRAD, 0, kD>(m, x, gx);
         if (nn == 0 && zero_empty) sdf = 0.f;
         if (GRAD && nn > 0) {
-            // dsdf/dq = sum_j (a_j - abar)/S du_j/dq + sum_j w_j R_j gx[F:],  a_j = gx . [f_j, v_j]
             float abar = 0.f;
 #pragma unroll
             for (int d = 0; d < kD; ++d) abar = fmaf(gx[d], x[d], abar);
-            const float invS = 1.f / nb.S;
 #pragma unroll
-            for (int j = 0; j < kK; ++j) {
-                if (nb.id[j] < 0) continue;
-                float xj[kD];
-                float4 qt;
-                neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
-                float a = 0.f;
+            for (int a = 0; a < 3; ++a) {
+                float s = -abar * C[a];
 #pragma unroll
-                for (int d = 0; d < kD; ++d) a = fmaf(gx[d], xj[d], a);
-                const float coef = -2.f * nb.u[j] * nb.u[j] * (a - abar) * invS;
+                for (int d = 0; d < kD; ++d) s = fmaf(gx[d], J[d][a], s);
+                gq[a] = s;
+            }
+            if (PGO) {
 #pragma unroll
-                for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, nb.pg[j][d], gq[d]);
-                float r0 = gx[kF], r1 = gx[kF + 1], r2 = gx[kF + 2];
-                if (PGO) quat_rotate_active(qt, gx[kF], gx[kF + 1], gx[kF + 2], r0, r1, r2);
-                gq[0] = fmaf(nb.w[j], r0, gq[0]);
-                gq[1] = fmaf(nb.w[j], r1, gq[1]);
-                gq[2] = fmaf(nb.w[j], r2, gq[2]);
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) gq[a] = fmaf(Wr[a][b], gx[kF + b], gq[a]);
+            } else {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) gq[a] = fmaf(Wr[0][0], gx[kF + a], gq[a]);
             }
         }
     } else {
@@ -191,18 +212,23 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
         float sk[kK];
         float gv[kK][3];
 #pragma unroll
-        for (int j = 0; j < kK; ++j) {
-            sk[j] = 0.f;
-            gv[j][0] = gv[j][1] = gv[j][2] = 0.f;
-            if (nb.id[j] < 0) continue;
-            float xj[kD];
-            float4 qt;
-            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
-            float g3[3];
-            sk[j] = mlp_sdf<GRAD, kF, 3>(m, xj, g3);
-            if (GRAD) {
-                if (PGO) quat_rotate_active(qt, g3[0], g3[1], g3[2], gv[j][0], gv[j][1], gv[j][2]);
-                else { gv[j][0] = g3[0]; gv[j][1] = g3[1]; gv[j][2] = g3[2]; }
+        for (int half = 0; half < kK / 4; ++half) {
+            float xk[4][kD];
+            float4 qt[4];
+            if (half == 0) gather_inputs<PGO, 0, 4>(src, p, nb, xk, qt);
+            else gather_inputs<PGO, 4, 4>(src, p, nb, xk, qt);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int j = half * 4 + t;
+                sk[j] = 0.f;
+                gv[j][0] = gv[j][1] = gv[j][2] = 0.f;
+                if (nb.id[j] < 0) continue;
+                float g3[3];
+                sk[j] = mlp_sdf<GRAD, kF, 3>(m, xk[t], g3);
+                if (GRAD) {
+                    if (PGO) quat_rotate_active(qt[t], g3[0], g3[1], g3[2], gv[j][0], gv[j][1], gv[j][2]);
+                    else { gv[j][0] = g3[0]; gv[j][1] = g3[1]; gv[j][2] = g3[2]; }
+                }
             }
         }
         float mean = 0.f;
@@ -217,10 +243,8 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
         sdf = mean;
         std_v = sqrtf(var);
         if (GRAD && nn > 0) {
-            const float invS = 1.f / nb.S;
 #pragma unroll
             for (int j = 0; j < kK; ++j) {
-                if (nb.id[j] < 0) continue;
                 const float coef = -2.f * nb.u[j] * nb.u[j] * (sk[j] - mean) * invS;
 #pragma unroll
                 for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, nb.pg[j][d], gq[d]);
@@ -240,7 +264,80 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
     if (std_out) std_out[i] = std_v;
 }
 
+template <bool WF, bool PGO, bool GRAD>
+__global__ void __launch_bounds__(kBlock)
+k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n, int nn_k,
+            int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out, int* __restrict__ nn_out,
+            float* __restrict__ cert_out, float* __restrict__ std_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const HashSource src(h, p);
+    query_sdf_body<WF, PGO, GRAD>(src, p, m, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+}
+
+template <bool WF, bool PGO, bool GRAD, bool FAT>
+__global__ void __launch_bounds__(kBlock)
+k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n,
+                 int nn_k, int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out,
+                 int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const GridSource<FAT> src(g, p);
+    query_sdf_body<WF, PGO, GRAD>(src, p, m, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+}
+
 // ------------------------------------------------------------------ drop-in query_feature
+template <bool WF, bool PGO, class Src>
+__device__ __forceinline__ void query_feature_body(const Src& src, const PinPoints& p, const float* __restrict__ q,
+                                                   int64_t i, int nn_k, float* __restrict__ feat,
+                                                   float* __restrict__ weights, int64_t* __restrict__ nn_counts,
+                                                   float* __restrict__ cert_out, int* __restrict__ ids,
+                                                   int* __restrict__ gids) {
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    TopK tk;
+    tk.init();
+    const int nn = src.template scan<kChunk>(qx, qy, qz, tk);
+    Neighbours nb;
+    load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
+    const float cert = (cert_out && p.certainties) ? gather_certainty(src, nb) : 0.f;
+    float x[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) x[d] = 0.f;
+#pragma unroll
+    for (int half = 0; half < kK / 4; ++half) {
+        float xk[4][kD];
+        float4 qt[4];
+        if (half == 0) gather_inputs<PGO, 0, 4>(src, p, nb, xk, qt);
+        else gather_inputs<PGO, 4, 4>(src, p, nb, xk, qt);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = half * 4 + t;
+            if (j >= nn_k) break;
+            if (WF) {
+#pragma unroll
+                for (int d = 0; d < kD; ++d) x[d] = x[d] + xk[t][d] * nb.w[j];
+            } else {
+                float* o = feat + (i * nn_k + j) * kD;
+#pragma unroll
+                for (int d = 0; d < kD; ++d) o[d] = xk[t][d];
+            }
+        }
+    }
+    if (WF) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) feat[i * kD + d] = x[d];
+    }
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        if (j >= nn_k) break;
+        weights[i * nn_k + j] = nb.w[j];
+        if (ids) ids[i * nn_k + j] = nb.id[j];
+        if (gids) gids[i * nn_k + j] = nb.id[j] >= 0 ? src.gid(tk.g[j]) : -1;
+    }
+    if (nn_counts) nn_counts[i] = nn;
+    if (cert_out) cert_out[i] = cert;
+}
+
 template <bool WF, bool PGO>
 __global__ void __launch_bounds__(kBlock)
 k_query_feature_fwd(const PinHash h, const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k,
@@ -248,51 +345,19 @@ k_query_feature_fwd(const PinHash h, const PinPoints p, const float* __restrict_
                     float* __restrict__ cert_out, int* __restrict__ ids, int* __restrict__ gids) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
-    TopK tk;
-    tk.init();
-    const int nn = scan_candidates<kChunk>(h, (const float4*)p.records, qx, qy, qz, tk);
-    Neighbours nb;
-    load_topk(p, tk, nn, nn_k, qx, qy, qz, nb);
-    float cert = 0.f;
-    if (cert_out && p.certainties) {
-#pragma unroll
-        for (int j = 0; j < kK; ++j) {
-            const float c = nb.id[j] >= 0 ? p.certainties[nb.id[j]] : 0.f;
-            cert = cert + c * nb.w[j];
-        }
-    }
-    float x[kD];
-#pragma unroll
-    for (int d = 0; d < kD; ++d) x[d] = 0.f;
-#pragma unroll
-    for (int j = 0; j < kK; ++j) {
-        if (j >= nn_k) break;
-        float xj[kD];
-#pragma unroll
-        for (int d = 0; d < kD; ++d) xj[d] = 0.f;
-        if (nb.id[j] >= 0) {
-            float4 qt;
-            neighbour_input<PGO>(p, nb, j, qx, qy, qz, xj, qt);
-        }
-        if (WF) {
-#pragma unroll
-            for (int d = 0; d < kD; ++d) x[d] = x[d] + xj[d] * nb.w[j];
-        } else {
-            float* o = feat + (i * nn_k + j) * kD;
-#pragma unroll
-            for (int d = 0; d < kD; ++d) o[d] = xj[d];
-        }
-        weights[i * nn_k + j] = nb.w[j];
-        if (ids) ids[i * nn_k + j] = nb.id[j];
-        if (gids) gids[i * nn_k + j] = nb.id[j] >= 0 ? tk.g[j] : -1;
-    }
-    if (WF) {
-#pragma unroll
-        for (int d = 0; d < kD; ++d) feat[i * kD + d] = x[d];
-    }
-    if (nn_counts) nn_counts[i] = nn;
-    if (cert_out) cert_out[i] = cert;
+    const HashSource src(h, p);
+    query_feature_body<WF, PGO>(src, p, q, i, nn_k, feat, weights, nn_counts, cert_out, ids, gids);
+}
+
+template <bool WF, bool PGO>
+__global__ void __launch_bounds__(kBlock)
+k_query_feature_fwd_grid(const PinGrid g, const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k,
+                         float* __restrict__ feat, float* __restrict__ weights, int64_t* __restrict__ nn_counts,
+                         float* __restrict__ cert_out, int* __restrict__ ids, int* __restrict__ gids) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const GridSource<false> src(g, p);
+    query_feature_body<WF, PGO>(src, p, q, i, nn_k, feat, weights, nn_counts, cert_out, ids, gids);
 }
 
 template <bool WF, bool PGO>
@@ -436,15 +501,12 @@ int pin_build_records(const float* positions, int64_t num_points, int32_t query_
 int pin_neighbor_cells(const int32_t* host_dx, int32_t num_cells, int64_t buffer_size, int32_t* cells_out,
                        void* stream) {
     if (!host_dx || !cells_out || num_cells <= 0 || buffer_size <= 0 || buffer_size >= (1ll << 31)) return PIN_ERR_ARG;
-    std::vector<int32_t> cells(4 * (size_t)num_cells);
+    std::vector<int32_t> cells((size_t)pin_cells_padded(num_cells), 0);
     for (int c = 0; c < num_cells; ++c) {
         const int64_t dx = host_dx[3 * c], dy = host_dx[3 * c + 1], dz = host_dx[3 * c + 2];
         int64_t r = (dx * kP0 + dy * kP1 + dz * kP2) % buffer_size;
         if (r < 0) r += buffer_size;
-        cells[4 * c] = (int32_t)dx;
-        cells[4 * c + 1] = (int32_t)dy;
-        cells[4 * c + 2] = (int32_t)dz;
-        cells[4 * c + 3] = (int32_t)r;
+        cells[c] = (int32_t)r;
     }
     // pageable source: the copy is staged before the call returns
     if (hipMemcpyAsync(cells_out, cells.data(), cells.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -555,6 +617,61 @@ int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32
     const int64_t total = n * nn_k;
     hipLaunchKernelGGL(k_train_scatter, grid_for(total), dim3(kBlock), 0, as_stream(stream), ids, weights, total,
                        nn_k, query_ts, certainties, ts_update);
+    return launch_status();
+}
+
+static bool grid_ok(const PinGrid* g) {
+    return g && g->bricks && g->crec && g->cgid && g->offsets && g->num_cells > 0 && g->resolution > 0.f &&
+           g->dims.nbx > 0 && g->dims.nby > 0 && g->dims.nbz > 0;
+}
+
+int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
+                       int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
+                       int32_t* nn_count, float* certainty, float* sdf_std, void* stream) {
+    if (!grid_ok(grid) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
+        return PIN_ERR_ARG;
+    const bool fat = grid->fat != 0;
+    if ((!fat && (!pts->features || !pts->certainties)) || (pts->after_pgo && !pts->orientations))
+        return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q) return PIN_ERR_ARG;
+    const bool g = grad != nullptr;
+    const bool pgo = pts->after_pgo != 0;
+    auto s = as_stream(stream);
+#define PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT)                                                                     \
+    hipLaunchKernelGGL((k_query_sdf_grid<WF, PGO, GRAD, FAT>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, *mlp, \
+                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std)
+#define PIN_SDFG_FAT(WF, PGO, GRAD) \
+    do { if (fat) PIN_LAUNCH_SDFG(WF, PGO, GRAD, true); else PIN_LAUNCH_SDFG(WF, PGO, GRAD, false); } while (0)
+    if (weighted_first) {
+        if (pgo) { if (g) PIN_SDFG_FAT(true, true, true); else PIN_SDFG_FAT(true, true, false); }
+        else { if (g) PIN_SDFG_FAT(true, false, true); else PIN_SDFG_FAT(true, false, false); }
+    } else {
+        if (pgo) { if (g) PIN_SDFG_FAT(false, true, true); else PIN_SDFG_FAT(false, true, false); }
+        else { if (g) PIN_SDFG_FAT(false, false, true); else PIN_SDFG_FAT(false, false, false); }
+    }
+#undef PIN_SDFG_FAT
+#undef PIN_LAUNCH_SDFG
+    return launch_status();
+}
+
+int pin_query_feature_fwd_grid(const PinGrid* grid, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,
+                               int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts,
+                               float* certainty, int32_t* ids, int32_t* gids, void* stream) {
+    if (!grid_ok(grid) || !points_ok(pts) || !pts->features || n < 0) return PIN_ERR_ARG;
+    if (pts->after_pgo && !pts->orientations) return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q || !feat || !weights) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    const bool pgo = pts->after_pgo != 0;
+#define PIN_LAUNCH_FWDG(WF, PGO)                                                                                \
+    hipLaunchKernelGGL((k_query_feature_fwd_grid<WF, PGO>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, q, n, \
+                       nn_k, feat, weights, nn_counts, certainty, ids, gids)
+    if (weighted_first) { if (pgo) PIN_LAUNCH_FWDG(true, true); else PIN_LAUNCH_FWDG(true, false); }
+    else { if (pgo) PIN_LAUNCH_FWDG(false, true); else PIN_LAUNCH_FWDG(false, false); }
+#undef PIN_LAUNCH_FWDG
     return launch_status();
 }
 

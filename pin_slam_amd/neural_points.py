@@ -20,6 +20,7 @@ is all ONES, so a point outside the local map that survives the time filter is
 read as local point 1.  ``strict_global2local=True`` in the config gives -1
 instead (not the reference's behaviour).
 """
+import ctypes
 import math
 import weakref
 
@@ -75,6 +76,20 @@ def voxel_down_sample_min_value(points: torch.Tensor, voxel_size: float, value: 
     best = torch.empty(uniq.shape, dtype=torch.int64, device=points.device)
     best.scatter_reduce_(0, inv, packed, reduce="amin", include_self=False)
     return best % scale
+
+
+def grid_window_collision_free(buffer_size: int, num_nei_cells: int) -> bool:
+    """True iff no two cells whose difference d has |d_i| <= W collide in the hash, where W
+    bounds how far (in cells) a neighbour cell can be from the voxel of a candidate that passes
+    the distance test: W = c + ceil(sqrt(3) (c + 1)) + 1.  Then a table slot reached from a
+    neighbour cell either holds the point whose own voxel it is, or a point too far away to be
+    accepted -- which is what makes the occupancy grid exact (pin_grid.hip)."""
+    W = num_nei_cells + math.ceil(math.sqrt(3) * (num_nei_cells + 1)) + 1
+    r = np.arange(-W, W + 1, dtype=np.int64)
+    d = np.stack(np.meshgrid(r, r, r, indexing="ij"), -1).reshape(-1, 3)
+    d = d[(d != 0).any(1)]
+    h = (d * np.array(PRIMES, dtype=np.int64)).sum(1)
+    return not bool((np.mod(h, int(buffer_size)) == 0).any())
 
 
 def hash_slots(points: torch.Tensor, resolution: float, buffer_size: int) -> torch.Tensor:
@@ -167,7 +182,7 @@ class NeuralPoints(nn.Module):
         self.local_mask = None
         self.global2local = None
 
-        self._records = {}
+        self._cache = {}
         self.set_search_neighborhood(num_nei_cells=config.num_nei_cells, search_alpha=config.search_alpha)
         self.memory_footprint = []
         self.to(self.device)
@@ -199,16 +214,44 @@ class NeuralPoints(nn.Module):
         self.max_valid_dist2 = 3 * ((num_nei_cells + 1) * self.resolution) ** 2
         dx_host = np.ascontiguousarray(self.neighbor_dx.cpu().numpy().astype(np.int32))
         self._cells_host = dx_host
-        self._cells = None  # device table built lazily (needs the HIP runtime)
+        self._cells = None  # device tables built lazily (need the HIP runtime)
+        self._offsets = None
+        self._grid_exact = grid_window_collision_free(self.buffer_size, num_nei_cells)
 
     def _cell_table(self):
         if self._cells is None:
-            cells = torch.empty((self.neighbor_K, 4), dtype=torch.int32, device=self.device)
+            cells = torch.empty(((self.neighbor_K + 15) // 16 * 16,), dtype=torch.int32, device=self.device)
             _lib.require_device(cells)
             _lib.call("pin_neighbor_cells", self._cells_host.ctypes.data_as(_lib.c_void_p), int(self.neighbor_K),
                       self.buffer_size, _lib.ptr(cells), _lib.stream())
             self._cells = cells
         return self._cells
+
+    def _offset_table(self):
+        """Packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 per neighbour cell, reference order."""
+        if self._offsets is None:
+            dx = self._cells_host.astype(np.int64)
+            packed = (dx[:, 0] + 128) | ((dx[:, 1] + 128) << 8) | ((dx[:, 2] + 128) << 16)
+            pad = np.zeros((self.neighbor_K + 15) // 16 * 16, dtype=np.int32)
+            pad[:self.neighbor_K] = packed
+            self._offsets = torch.from_numpy(pad).to(self.device)
+        return self._offsets
+
+    # ------------------------------------------------------------------ derived-state cache
+    def _cached(self, name, deps, scalars, build):
+        """Value of ``build()`` cached under ``name`` until a dependency tensor is replaced or
+        modified in place (identity + ``Tensor._version``) or a scalar in ``scalars`` changes."""
+        hit = self._cache.get(name)
+        if hit is not None:
+            val, refs, vers, key = hit
+            if key == scalars and len(refs) == len(deps) and all(
+                    (r() is d) and (d is None or d._version == v) for r, d, v in zip(refs, deps, vers)):
+                return val
+        val = build()
+        refs = tuple(weakref.ref(d) if d is not None else (lambda: None) for d in deps)
+        vers = tuple(d._version if d is not None else None for d in deps)
+        self._cache[name] = (val, refs, vers, scalars)
+        return val
 
     # ------------------------------------------------------------------ candidate records
     def _deps(self, mode):
@@ -221,19 +264,8 @@ class NeuralPoints(nn.Module):
 
     def records(self, mode: str) -> torch.Tensor:
         """[M,4] f32 candidate records for ``mode`` in {"global", "global_tf", "local"}."""
-        deps = self._deps(mode)
-        key = (self.cur_ts, float(self.diff_travel_dist_local))
-        hit = self._records.get(mode)
-        if hit is not None:
-            rec, refs, vers, k = hit
-            if k == key and all((r() is d) and (d is None or d._version == v)
-                                for r, d, v in zip(refs, deps, vers)):
-                return rec
-        rec = self._build_records(mode)
-        refs = tuple(weakref.ref(d) if d is not None else (lambda: None) for d in deps)
-        vers = tuple(d._version if d is not None else None for d in deps)
-        self._records[mode] = (rec, refs, vers, key)
-        return rec
+        return self._cached("records:" + mode, self._deps(mode),
+                            (self.cur_ts, float(self.diff_travel_dist_local)), lambda: self._build_records(mode))
 
     def _build_records(self, mode):
         pts = self.neural_points.contiguous()
@@ -256,6 +288,84 @@ class NeuralPoints(nn.Module):
                   float(np.float32(self.diff_travel_dist_local)), _lib.ptr(lpos),
                   int(lpos.shape[0]) if lpos is not None else 0, _lib.ptr(rec), _lib.stream())
         return rec
+
+    # ------------------------------------------------------------------ occupancy grid
+    MAX_GRID_BRICKS = 1 << 26
+
+    def backend(self) -> str:
+        """"grid" when the occupancy grid reproduces the hash probes exactly, else "hash"."""
+        want = getattr(self.config, "query_backend", "auto")
+        if want == "hash" or self.count() == 0 or not self._grid_exact:
+            return "hash"
+        occ = self.occupancy()
+        if occ is None:
+            if want == "grid":
+                raise RuntimeError("occupancy grid not exact for this map (displaced table entries or box too big)")
+            return "hash"
+        return "grid"
+
+    def occupancy(self):
+        """(bricks [nb,4] u32, PinGridDims, n_occ) or None when the table holds entries that are
+        not at their point's own voxel slot (then only the hash path is exact)."""
+        return self._cached("occupancy", (self.neural_points, self.buffer_pt_index),
+                            (float(self.resolution), self.buffer_size), self._build_occupancy)
+
+    def _build_occupancy(self):
+        pts = self.neural_points.contiguous()
+        _lib.require_device(pts)
+        res = float(np.float32(self.resolution))
+        cells = torch.floor(pts / res).to(torch.int64)
+        lo = cells.min(0)[0]
+        hi = cells.max(0)[0]
+        ext = ((hi - lo + 1 + 3) // 4).cpu().tolist()
+        lo = lo.cpu().tolist()
+        nb = ext[0] * ext[1] * ext[2]
+        if nb > self.MAX_GRID_BRICKS:
+            return None
+        dims = _lib.PinGridDims(ox=lo[0], oy=lo[1], oz=lo[2], nbx=ext[0], nby=ext[1], nbz=ext[2], reserved=0)
+        bricks = torch.empty((nb, 4), dtype=torch.int32, device=pts.device)
+        counters = torch.empty(2, dtype=torch.int64, device=pts.device)
+        ws = torch.empty(((nb + 4095) // 4096 * 4 + 16,), dtype=torch.uint8, device=pts.device)
+        _lib.call("pin_grid_mark", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(self.buffer_pt_index), self.buffer_size,
+                  ctypes.byref(dims), _lib.ptr(bricks), _lib.ptr(counters), _lib.ptr(ws), _lib.stream())
+        marked, occupied = counters.cpu().tolist()
+        if marked != occupied:
+            return None
+        return bricks, dims, int(marked)
+
+    def compact_records(self, mode: str, fat: bool):
+        """(crec [n_occ,16] f32, cgid [n_occ] i32) in brick order for a query mode."""
+        occ = self.occupancy()
+        local = mode == "local"
+        feats = (self.local_geo_features if local else self.geo_features) if fat else None
+        cert = (self.local_point_certainties if local else self.point_certainties) if fat else None
+        rec = self.records(mode)
+        deps = (self.neural_points, self.buffer_pt_index, rec, feats, cert)
+        return self._cached(f"crec:{mode}:{int(fat)}", deps, (float(self.resolution),),
+                            lambda: self._build_compact(occ, rec, feats, cert))
+
+    def _build_compact(self, occ, rec, feats, cert):
+        bricks, dims, n_occ = occ
+        pts = self.neural_points.contiguous()
+        crec = torch.zeros((max(n_occ, 1), 16), dtype=torch.float32, device=pts.device)
+        cgid = torch.full((max(n_occ, 1),), -1, dtype=torch.int32, device=pts.device)
+        f = feats.detach().contiguous() if feats is not None else None
+        c = cert.detach().contiguous() if cert is not None else None
+        _lib.call("pin_grid_fill", _lib.ptr(pts), pts.shape[0], float(np.float32(self.resolution)),
+                  _lib.ptr(self.buffer_pt_index), self.buffer_size, ctypes.byref(dims), _lib.ptr(bricks),
+                  _lib.ptr(rec), _lib.ptr(f), _lib.ptr(c), _lib.ptr(crec), _lib.ptr(cgid), _lib.stream())
+        return crec, cgid
+
+    def grid_view(self, mode: str, fat: bool):
+        from .query import _View
+        bricks, dims, n_occ = self.occupancy()
+        crec, cgid = self.compact_records(mode, fat)
+        offs = self._offset_table()
+        g = _lib.PinGrid(bricks=bricks.data_ptr(), dims=dims, crec=crec.data_ptr(), cgid=cgid.data_ptr(),
+                         n_occ=n_occ, offsets=offs.data_ptr(), resolution=float(np.float32(self.resolution)),
+                         num_cells=int(self.neighbor_K), max_valid_dist2=float(np.float32(self.max_valid_dist2)),
+                         fat=int(fat))
+        return _View(g, (bricks, crec, cgid, offs))
 
     # ------------------------------------------------------------------ map update
     def update(self, points: torch.Tensor, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor, cur_ts):
@@ -413,7 +523,7 @@ class NeuralPoints(nn.Module):
         self.local_point_ts_update = None
         self.local_mask = None
         self.global2local = None
-        self._records = {}
+        self._cache = {}
         if clean_more:
             self.point_ts_create = None
             self.point_ts_update = None
@@ -464,7 +574,8 @@ class NeuralPoints(nn.Module):
         mode = "local" if query_locally else "global"
         hv, pv = self._views(mode, query_locally)
         feats = self.local_geo_features if query_locally else self.geo_features
-        out = QueryFeatureFn.apply(query_points, feats, hv, pv, nn_k, bool(self.config.weighted_first))
+        gv = self.grid_view(mode, False) if self.backend() == "grid" else None
+        out = QueryFeatureFn.apply(query_points, feats, hv, pv, nn_k, bool(self.config.weighted_first), gv)
         geo_vec, weights, nn_counts, certainty, ids = out
         if training_mode:
             cert_t = self.local_point_certainties if query_locally else self.point_certainties

@@ -69,7 +69,7 @@ class QueryFeatureFn(torch.autograd.Function):
     scatter of dL/dfeatures (the reference's autograd through index_put / gather)."""
 
     @staticmethod
-    def forward(ctx, q, feats, hv, pv, nn_k, weighted_first):
+    def forward(ctx, q, feats, hv, pv, nn_k, weighted_first, gv=None):
         qd = q.detach().to(torch.float32).contiguous()
         n = qd.shape[0]
         dev = qd.device
@@ -80,9 +80,14 @@ class QueryFeatureFn(torch.autograd.Function):
         cert = torch.empty((n,), dtype=torch.float32, device=dev)
         ids = torch.empty((n, nn_k), dtype=torch.int32, device=dev)
         gids = torch.empty((n, nn_k), dtype=torch.int32, device=dev)
-        _lib.call("pin_query_feature_fwd", hv.ref(), pv.ref(), _lib.ptr(qd), n, nn_k, int(weighted_first),
-                  _lib.ptr(feat), _lib.ptr(weights), _lib.ptr(nn_counts), _lib.ptr(cert), _lib.ptr(ids),
-                  _lib.ptr(gids), _lib.stream())
+        if gv is not None:
+            _lib.call("pin_query_feature_fwd_grid", gv.ref(), pv.ref(), _lib.ptr(qd), n, nn_k, int(weighted_first),
+                      _lib.ptr(feat), _lib.ptr(weights), _lib.ptr(nn_counts), _lib.ptr(cert), _lib.ptr(ids),
+                      _lib.ptr(gids), _lib.stream())
+        else:
+            _lib.call("pin_query_feature_fwd", hv.ref(), pv.ref(), _lib.ptr(qd), n, nn_k, int(weighted_first),
+                      _lib.ptr(feat), _lib.ptr(weights), _lib.ptr(nn_counts), _lib.ptr(cert), _lib.ptr(ids),
+                      _lib.ptr(gids), _lib.stream())
         ctx.save_for_backward(qd, ids, gids, weights)
         ctx.pv = pv
         ctx.nn_k = nn_k
@@ -97,7 +102,7 @@ class QueryFeatureFn(torch.autograd.Function):
         qd, ids, gids, weights = ctx.saved_tensors
         need_q, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_q or need_f):
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None
         n = qd.shape[0]
         grad_q = torch.empty_like(qd) if need_q else None
         grad_f = torch.zeros_like(ctx.pv.features) if need_f else None
@@ -108,7 +113,7 @@ class QueryFeatureFn(torch.autograd.Function):
                   _lib.stream())
         if grad_q is not None and ctx.q_dtype != torch.float32:
             grad_q = grad_q.to(ctx.q_dtype)
-        return grad_q, grad_f, None, None, None, None
+        return grad_q, grad_f, None, None, None, None, None
 
 
 def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
@@ -124,15 +129,21 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     dev = q.device
     nn_k = int(nm.config.query_nn_k if nn_k is None else nn_k)
     wf = bool(nm.config.weighted_first if weighted_first is None else weighted_first)
-    hv, pv = nm._views("local" if query_locally else "global", query_locally)
+    mode = "local" if query_locally else "global"
+    hv, pv = nm._views(mode, query_locally)
     mv = mlp_view(decoder)
     sdf = torch.empty(n, dtype=torch.float32, device=dev)
     grad = torch.empty((n, 3), dtype=torch.float32, device=dev) if want_grad else None
     nn_count = torch.empty(n, dtype=torch.int32, device=dev)
     cert = torch.empty(n, dtype=torch.float32, device=dev) if want_certainty else None
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
-    _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
-              _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
+    if nm.backend() == "grid":
+        gv = nm.grid_view(mode, True)
+        _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
+                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
+    else:
+        _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
+                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
     if want_std and wf:
         std = torch.zeros(n, dtype=torch.float32, device=dev)
     return sdf, grad, nn_count, cert, std

@@ -6,16 +6,16 @@ import pin_slam_amd as P
 from oracle import pin_oracle as O
 
 
-def config_from_fixture(z, device="cuda"):
+def config_from_fixture(z, device="cuda", backend="auto"):
     res = round(float(z["map_resolution"]), 6)
     return P.Config(device=device, voxel_size_m=res, num_nei_cells=int(z["num_nei_cells"]),
                     search_alpha=float(z["search_alpha"]), query_nn_k=int(z["nn_k"]),
                     weighted_first=bool(z["weighted_first"]), buffer_size=int(z["map_buffer_size"]),
-                    local_map_radius=15.0)
+                    local_map_radius=15.0, query_backend=backend)
 
 
-def neural_points_from_fixture(z, device="cuda", orientations=None, after_pgo=False):
-    cfg = config_from_fixture(z, device)
+def neural_points_from_fixture(z, device="cuda", orientations=None, after_pgo=False, backend="auto"):
+    cfg = config_from_fixture(z, device, backend)
     nm = P.NeuralPoints(cfg)
     t = lambda a, dt=None: torch.as_tensor(np.ascontiguousarray(a), device=device, dtype=dt)  # noqa: E731
     nm.diff_travel_dist_local = float(z["map_diff_travel_dist_local"])

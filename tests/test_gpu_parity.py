@@ -15,6 +15,7 @@ from tests import helpers as H
 pytestmark = pytest.mark.gpu
 
 QUERY_CASES = ["query_wf", "query_nwf", "query_kitti"]
+BACKENDS = ["hash", "grid"]
 SDF_ATOL = 1e-5
 
 
@@ -47,11 +48,12 @@ def test_radius_search_exact(golden, dev, case, tf):
 
 @pytest.mark.parametrize("case", QUERY_CASES)
 @pytest.mark.parametrize("ql", [0, 1])
-def test_query_feature_dropin(golden, dev, case, ql):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_query_feature_dropin(golden, dev, backend, case, ql):
     """NeuralPoints.query_feature + Decoder.sdf + autograd (the reference's own call
     sequence, utils/tracker.py:230-252) through the HIP forward/backward kernels."""
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     dec = H.decoder_from_fixture(z, nm.config)
     q = torch.as_tensor(z["queries"], device=dev).requires_grad_(True)
     feat, _, w, nn_counts, cert = nm.query_feature(q, training_mode=False, query_locally=bool(ql))
@@ -70,9 +72,10 @@ def test_query_feature_dropin(golden, dev, case, ql):
 
 @pytest.mark.parametrize("case", QUERY_CASES)
 @pytest.mark.parametrize("ql", [0, 1])
-def test_query_sdf_fused(golden, dev, case, ql):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_query_sdf_fused(golden, dev, backend, case, ql):
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     dec = H.decoder_from_fixture(z, nm.config)
     import pin_slam_amd as P
     sdf, grad, nn, cert, std = P.query_sdf(nm, dec, torch.as_tensor(z["queries"], device=dev),
@@ -87,9 +90,11 @@ def test_query_sdf_fused(golden, dev, case, ql):
 
 
 @pytest.mark.parametrize("case", QUERY_CASES)
-def test_after_pgo(golden, dev, case):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_after_pgo(golden, dev, backend, case):
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev, orientations=z["pgo_point_orientations"], after_pgo=True)
+    nm = H.neural_points_from_fixture(z, dev, orientations=z["pgo_point_orientations"], after_pgo=True,
+                                      backend=backend)
     dec = H.decoder_from_fixture(z, nm.config)
     import pin_slam_amd as P
     sdf, grad, nn, cert, std = P.query_sdf(nm, dec, torch.as_tensor(z["queries"], device=dev),
@@ -107,9 +112,10 @@ def test_after_pgo(golden, dev, case):
 
 
 @pytest.mark.parametrize("case", QUERY_CASES)
-def test_training_side_effects(golden, dev, case):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_training_side_effects(golden, dev, backend, case):
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     np.testing.assert_array_equal(_np(nm.local_point_certainties), z["train_cert_before"])
     q = torch.as_tensor(z["queries"], device=dev)
     ts = torch.as_tensor(z["train_query_ts"], device=dev)
@@ -127,9 +133,10 @@ def test_query_certainty(golden, dev, case):
     np.testing.assert_array_equal(_np(c), z["qc_certainty"])
 
 
-def test_mesher_fixture(golden, dev):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_mesher_fixture(golden, dev, backend):
     z = golden("mesher_wf")
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     dec = H.decoder_from_fixture(z, nm.config)
     import pin_slam_amd as P
     sdf, _, nn, _, _ = P.query_sdf(nm, dec, torch.as_tensor(z["coord"], device=dev), query_locally=False,
@@ -139,9 +146,10 @@ def test_mesher_fixture(golden, dev):
 
 
 @pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
-def test_tracker_fixture_queries(golden, dev, case):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_tracker_fixture_queries(golden, dev, backend, case):
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     nm.local_geo_features = torch.nn.Parameter(torch.as_tensor(z["local_features"], device=dev))
     dec = H.decoder_from_fixture(z, nm.config)
     import pin_slam_amd as P
@@ -155,11 +163,12 @@ def test_tracker_fixture_queries(golden, dev, case):
 
 
 @pytest.mark.parametrize("case", ["mapper_wf", "mapper_nwf"])
-def test_mapper_dropin_backward(golden, dev, case):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_mapper_dropin_backward(golden, dev, backend, case):
     """One reference mapping iteration through the drop-in classes (query_feature in
     training mode, numerical gradient, BCE + eikonal, backward): feature and MLP grads."""
     z = golden(case)
-    nm = H.neural_points_from_fixture(z, dev)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
     dec = H.decoder_from_fixture(z, nm.config)
     cfg = nm.config
     coord = torch.as_tensor(z["it0_coord"], device=dev)
@@ -193,11 +202,13 @@ def test_mapper_dropin_backward(golden, dev, case):
     np.testing.assert_array_equal(_np(nm.local_point_ts_update), z["it0_ts_after"])
 
 
+@pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("wf", [True, False])
-def test_random_map_vs_oracle(dev, wf):
+def test_random_map_vs_oracle(dev, wf, backend):
     """Larger seeded map (250K points, 20K queries) against the oracle: exact neighbour
     counts and k-NN ids, SDF within 1e-5, gradients within tolerance."""
-    nm, dec, pts = H.surface_map(500, device=dev, weighted_first=wf, buffer_size=1 << 22)
+    nm, dec, pts = H.surface_map(500, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend=backend)
+    assert nm.backend() == backend
     q = H.surface_queries(pts, 20000, device=dev)
     import pin_slam_amd as P
     sdf, grad, nn, cert, std = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True, want_std=True)
@@ -210,3 +221,14 @@ def test_random_map_vs_oracle(dev, wf):
     assert_grad_close(_np(grad), ograd)
     feat, _, w, nnc, _ = nm.query_feature(q, training_mode=False)
     np.testing.assert_allclose(_np(w)[..., 0], oq.weights, rtol=2e-6, atol=1e-7)
+
+
+def test_backend_selection(golden, dev):
+    """The grid is used only when it is exact: after adjust_map (points moved, table not
+    rebuilt) the table holds entries off their own voxel and the hash path must be taken."""
+    z = golden("query_wf")
+    nm = H.neural_points_from_fixture(z, dev)
+    assert nm.backend() == "grid"
+    with torch.no_grad():
+        nm.neural_points += 0.37
+    assert nm.backend() == "hash"
