@@ -79,6 +79,7 @@ struct TopK {
 // The reference structure: hash every neighbour cell into the slot table (:465-476).
 // Payload = global point index; records indexed by it.
 struct HashSource {
+    static constexpr int kChunk = 12;
     const PinHash& h;
     const PinPoints& p;
     __device__ HashSource(const PinHash& h_, const PinPoints& p_) : h(h_), p(p_) {}
@@ -133,6 +134,7 @@ struct HashSource {
 // (one line per candidate); otherwise from the live PinPoints arrays.
 template <bool FAT>
 struct GridSource {
+    static constexpr int kChunk = 8;
     const PinGrid& gr;
     const PinPoints& p;
     __device__ GridSource(const PinGrid& g_, const PinPoints& p_) : gr(g_), p(p_) {}
@@ -143,10 +145,16 @@ struct GridSource {
         const float4* __restrict__ crec = (const float4*)gr.crec;
         const int32_t* __restrict__ offs = gr.offsets;  // padded to a multiple of 16 entries
         const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
-        const int64_t lx = (int64_t)floorf(qx / res) - gr.dims.ox;
-        const int64_t ly = (int64_t)floorf(qy / res) - gr.dims.oy;
-        const int64_t lz = (int64_t)floorf(qz / res) - gr.dims.oz;
-        const int64_t ex = 4ll * gr.dims.nbx, ey = 4ll * gr.dims.nby, ez = 4ll * gr.dims.nbz;
+        const int ex = 4 * gr.dims.nbx, ey = 4 * gr.dims.nby, ez = 4 * gr.dims.nbz;
+        // query cell relative to the box, clamped so that every offset stays representable in
+        // int32 and a far-away query still lands outside the box for every offset
+        auto rel = [](float v, float r, int64_t o, int e) -> int {
+            const int64_t l = (int64_t)floorf(v / r) - o;
+            return (int)(l < -256 ? -256 : (l > (int64_t)e + 256 ? (int64_t)e + 256 : l));
+        };
+        const int lx = rel(qx, res, gr.dims.ox, ex);
+        const int ly = rel(qy, res, gr.dims.oy, ey);
+        const int lz = rel(qz, res, gr.dims.oz, ez);
         const int Kc = gr.num_cells;
         int nn = 0;
         for (int c0 = 0; c0 < Kc; c0 += CH) {
@@ -158,12 +166,13 @@ struct GridSource {
             bool in[CH];
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
-                const int64_t cx = lx + ((of[t] & 255) - 128);
-                const int64_t cy = ly + (((of[t] >> 8) & 255) - 128);
-                const int64_t cz = lz + (((of[t] >> 16) & 255) - 128);
-                in[t] = (c0 + t < Kc) && cx >= 0 && cy >= 0 && cz >= 0 && cx < ex && cy < ey && cz < ez;
-                const int64_t b = in[t] ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * (int64_t)gr.dims.nbx + (cx >> 2) : 0;
-                bit[t] = (int)(((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3));
+                const int cx = lx + ((of[t] & 255) - 128);
+                const int cy = ly + (((of[t] >> 8) & 255) - 128);
+                const int cz = lz + (((of[t] >> 16) & 255) - 128);
+                in[t] = (c0 + t < Kc) && (unsigned)cx < (unsigned)ex && (unsigned)cy < (unsigned)ey &&
+                        (unsigned)cz < (unsigned)ez;
+                const int b = in[t] ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * gr.dims.nbx + (cx >> 2) : 0;
+                bit[t] = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
                 w[t] = bricks[b];
             }
             int ci[CH];
@@ -175,7 +184,7 @@ struct GridSource {
             }
             float4 r[CH];
 #pragma unroll
-            for (int t = 0; t < CH; ++t) r[t] = crec[4 * (int64_t)(ci[t] > 0 ? ci[t] : 0)];
+            for (int t = 0; t < CH; ++t) r[t] = crec[4 * (ci[t] > 0 ? ci[t] : 0)];
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int id = __float_as_int(r[t].w);
@@ -339,30 +348,45 @@ __device__ __forceinline__ float gather_certainty(const Src& src, const Neighbou
 // Decoder forward fused with its input gradient (model/decoder.py:66-88):
 //   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
 // One pass over the hidden units; weights are wave-uniform (scalar loads).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Decoder forward fused with its input gradient (model/decoder.py:66-88):
+//   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
+// One pass over the hidden units, two at a time with packed FMAs (v_pk_fma_f32); weights
+// are wave-uniform (scalar loads).
 template <bool GRAD, int OFF, int NOUT>
 __device__ __forceinline__ float mlp_sdf(const PinMlp& m, const float (&x)[kD], float (&gx)[NOUT]) {
-    float out = 0.f;
+    f32x2 out2 = {0.f, 0.f};
+    f32x2 g2[NOUT];
 #pragma unroll
-    for (int i = 0; i < NOUT; ++i) gx[i] = 0.f;
+    for (int i = 0; i < NOUT; ++i) g2[i] = (f32x2){0.f, 0.f};
 #pragma unroll 2
-    for (int c = 0; c < kH; ++c) {
-        const float* wr = m.W1 + c * kD;
-        float acc = 0.f;
+    for (int c = 0; c < kH; c += 2) {
+        const float* w0 = m.W1 + c * kD;
+        const float* w1 = w0 + kD;
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < kD; ++i) acc = fmaf(wr[i], x[i], acc);
-        const float pre = acc + m.b1[c];
-        const float a = pre > 0.f ? m.W2[c] : 0.f;
-        out = fmaf(a, pre, out);
+        for (int i = 0; i < kD; ++i) {
+            const f32x2 wv = {w0[i], w1[i]};
+            const f32x2 xv = {x[i], x[i]};
+            acc = __builtin_elementwise_fma(wv, xv, acc);
+        }
+        const f32x2 pre = acc + (f32x2){m.b1[c], m.b1[c + 1]};
+        const f32x2 a = {pre.x > 0.f ? m.W2[c] : 0.f, pre.y > 0.f ? m.W2[c + 1] : 0.f};
+        out2 = __builtin_elementwise_fma(a, pre, out2);
         if (GRAD) {
 #pragma unroll
-            for (int i = 0; i < NOUT; ++i) gx[i] = fmaf(a, wr[OFF + i], gx[i]);
+            for (int i = 0; i < NOUT; ++i) {
+                const f32x2 wv = {w0[OFF + i], w1[OFF + i]};
+                g2[i] = __builtin_elementwise_fma(a, wv, g2[i]);
+            }
         }
     }
     if (GRAD) {
 #pragma unroll
-        for (int i = 0; i < NOUT; ++i) gx[i] *= m.sdf_scale;
+        for (int i = 0; i < NOUT; ++i) gx[i] = (g2[i].x + g2[i].y) * m.sdf_scale;
     }
-    return (out + m.b2[0]) * m.sdf_scale;
+    return ((out2.x + out2.y) + m.b2[0]) * m.sdf_scale;
 }
 
 }  // namespace pin

@@ -121,6 +121,44 @@ k_query_certainty(const PinHash h, const float4* __restrict__ rec, const float* 
 
 // ------------------------------------------------------------------ fused SDF (+grad)
 // Tracker / mesher inference: query_feature + Decoder.sdf + get_gradient in one pass.
+// One neighbour of the top-k list, streamed: its record (position, id), decoder input
+// x = [f, v] (v rotated after pgo), quaternion and certainty.  Invalid -> zeros.
+struct NbInput {
+    float x[kD];
+    float pg[3];   // q - global position
+    float4 quat;
+    float cert;
+};
+
+template <bool PGO, bool CERT, class Src>
+__device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints& p, int pay, bool valid, float qx,
+                                                 float qy, float qz, NbInput& o) {
+    const float4 r = src.record(pay);
+    const int raw = __float_as_int(r.w);
+    const int64_t id = valid ? (raw & kIdMask) : 0;
+    float4 f0, f1;
+    src.features(pay, id, f0, f1);
+    o.pg[0] = qx - r.x;
+    o.pg[1] = qy - r.y;
+    o.pg[2] = qz - r.z;
+    float v0 = o.pg[0], v1 = o.pg[1], v2 = o.pg[2];
+    if (valid && (raw & PIN_RECORD_UNFAITHFUL)) {  // global2local quirk: local position differs
+        v0 = qx - p.positions[3 * id];
+        v1 = qy - p.positions[3 * id + 1];
+        v2 = qz - p.positions[3 * id + 2];
+    }
+    o.quat = make_float4(1.f, 0.f, 0.f, 0.f);
+    if (PGO) {
+        o.quat = ((const float4*)p.orientations)[id];
+        quat_rotate_passive(o.quat, v0, v1, v2);
+    }
+    o.cert = CERT ? src.certainty(pay, id) : 0.f;
+    const float f[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
+#pragma unroll
+    for (int d = 0; d < kD; ++d) o.x[d] = valid ? f[d] : 0.f;
+    if (!valid) o.cert = 0.f;
+}
+
 template <bool WF, bool PGO, bool GRAD, class Src>
 __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const PinMlp& m,
                                                const float* __restrict__ q, int64_t i, int nn_k, int zero_empty,
@@ -130,56 +168,65 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
     const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
     TopK tk;
     tk.init();
-    const int nn = src.template scan<kChunk>(qx, qy, qz, tk);
-    Neighbours nb;
-    load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
-    const float cert = cert_out ? gather_certainty(src, nb) : 0.f;
-    // c_j = d w_j-part: -2 u_j^2 (q - p_j) / S   (du_j/dq scaled by 1/S; 0 for invalid)
-    const float invS = nn > 0 ? 1.f / nb.S : 0.f;
+    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    // IDW weights from the top-k distances alone (neural_points.py:618-632)
+    float u[kK];
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        u[j] = (j < nn_k && tk.g[j] >= 0) ? 1.0f / (tk.d[j] + kIdwEps) : 0.f;
+        S = S + u[j];
+    }
+    const float invS = nn > 0 ? 1.f / S : 0.f;
+    const bool want_cert = cert_out != nullptr;
 
+    float cert = 0.f;
     float sdf = 0.f, std_v = 0.f;
     float gq[3] = {0.f, 0.f, 0.f};
     if constexpr (WF) {
-        // One pass over the neighbours accumulates
+        // One streamed pass over the neighbours accumulates
         //   x  = sum_j w_j x_j                      (neural_points.py:660-662)
-        //   J  = sum_j x_j (x) c_j,  C = sum_j c_j   so that  sum_j (a_j - abar) c_j = J^T gx - (gx.x) C
-        //   Wr = sum_j w_j R_j  (rotation term of d x / d q after pgo; scalar sum w otherwise)
+        //   J  = sum_j x_j (x) c_j,  C = sum_j c_j,  c_j = -2 u_j^2 (q - p_j) / S
+        //        so that sum_j (a_j - abar) c_j = J^T gx - (gx . x) C  with a_j = gx . x_j
+        //        (the same un-centred form autograd evaluates for d(u/S)/du)
+        //   Wr = sum_j w_j R_j  (pgo; the scalar sum_j w_j otherwise)
         float x[kD], J[kD][3], C[3] = {0.f, 0.f, 0.f}, Wr[3][3];
 #pragma unroll
         for (int d = 0; d < kD; ++d) { x[d] = 0.f; J[d][0] = J[d][1] = J[d][2] = 0.f; }
 #pragma unroll
         for (int a = 0; a < 3; ++a) Wr[a][0] = Wr[a][1] = Wr[a][2] = 0.f;
 #pragma unroll
-        for (int half = 0; half < kK / 4; ++half) {
-            float xk[4][kD];
-            float4 qt[4];
-            if (half == 0) gather_inputs<PGO, 0, 4>(src, p, nb, xk, qt);
-            else gather_inputs<PGO, 4, 4>(src, p, nb, xk, qt);
+        for (int j = 0; j < kK; ++j) {
+            // neighbours stream in two groups of four: bounds the registers held by gathers
+            // in flight while keeping four lines outstanding per lane
+            if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
+            const bool valid = u[j] > 0.f;
+            NbInput in;
+            if (want_cert) stream_neighbour<PGO, true>(src, p, tk.g[j], valid, qx, qy, qz, in);
+            else stream_neighbour<PGO, false>(src, p, tk.g[j], valid, qx, qy, qz, in);
+            const float w = valid && nn > 0 ? u[j] / S : 0.f;
+            cert = cert + in.cert * w;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int j = half * 4 + t;
+            for (int d = 0; d < kD; ++d) x[d] = x[d] + in.x[d] * w;
+            if (GRAD) {
+                const float cu = valid ? -2.f * u[j] * u[j] * invS : 0.f;
+                const float c3[3] = {cu * in.pg[0], cu * in.pg[1], cu * in.pg[2]};
 #pragma unroll
-                for (int d = 0; d < kD; ++d) x[d] = x[d] + xk[t][d] * nb.w[j];
-                if (GRAD) {
-                    const float cu = -2.f * nb.u[j] * nb.u[j] * invS;
-                    const float c3[3] = {cu * nb.pg[j][0], cu * nb.pg[j][1], cu * nb.pg[j][2]};
+                for (int a = 0; a < 3; ++a) C[a] += c3[a];
 #pragma unroll
-                    for (int a = 0; a < 3; ++a) C[a] += c3[a];
+                for (int d = 0; d < kD; ++d) {
 #pragma unroll
-                    for (int d = 0; d < kD; ++d) {
+                    for (int a = 0; a < 3; ++a) J[d][a] = fmaf(in.x[d], c3[a], J[d][a]);
+                }
+                if (PGO) {
+                    float R[3][3];
+                    quat_rotmat(in.quat, R);
 #pragma unroll
-                        for (int a = 0; a < 3; ++a) J[d][a] = fmaf(xk[t][d], c3[a], J[d][a]);
-                    }
-                    if (PGO) {
-                        float R[3][3];
-                        quat_rotmat(qt[t], R);
+                    for (int a = 0; a < 3; ++a)
 #pragma unroll
-                        for (int a = 0; a < 3; ++a)
-#pragma unroll
-                            for (int b = 0; b < 3; ++b) Wr[a][b] = fmaf(nb.w[j], R[a][b], Wr[a][b]);
-                    } else {
-                        Wr[0][0] += nb.w[j];
-                    }
+                        for (int b = 0; b < 3; ++b) Wr[a][b] = fmaf(w, R[a][b], Wr[a][b]);
+                } else {
+                    Wr[0][0] += w;
                 }
             }
         }
@@ -208,49 +255,52 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
             }
         }
     } else {
-        // per-neighbour decoding, then the weighted mean / std (utils/tracker.py:245-249)
+        // per-neighbour decoding, weighted mean / std (utils/tracker.py:245-249);
+        // gradient = sum_j sk_j c_j - mean C + sum_j w_j R_j gv_j
         float sk[kK];
-        float gv[kK][3];
+        float w[kK];
+        float A[3] = {0.f, 0.f, 0.f}, C[3] = {0.f, 0.f, 0.f}, G[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-        for (int half = 0; half < kK / 4; ++half) {
-            float xk[4][kD];
-            float4 qt[4];
-            if (half == 0) gather_inputs<PGO, 0, 4>(src, p, nb, xk, qt);
-            else gather_inputs<PGO, 4, 4>(src, p, nb, xk, qt);
+        for (int j = 0; j < kK; ++j) {
+            const bool valid = u[j] > 0.f;
+            NbInput in;
+            if (want_cert) stream_neighbour<PGO, true>(src, p, tk.g[j], valid, qx, qy, qz, in);
+            else stream_neighbour<PGO, false>(src, p, tk.g[j], valid, qx, qy, qz, in);
+            w[j] = valid && nn > 0 ? u[j] / S : 0.f;
+            cert = cert + in.cert * w[j];
+            sk[j] = 0.f;
+            if (!valid) continue;
+            float g3[3];
+            sk[j] = mlp_sdf<GRAD, kF, 3>(m, in.x, g3);
+            if (GRAD) {
+                float r0 = g3[0], r1 = g3[1], r2 = g3[2];
+                if (PGO) quat_rotate_active(in.quat, g3[0], g3[1], g3[2], r0, r1, r2);
+                G[0] = fmaf(w[j], r0, G[0]);
+                G[1] = fmaf(w[j], r1, G[1]);
+                G[2] = fmaf(w[j], r2, G[2]);
+                const float cu = -2.f * u[j] * u[j] * invS;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int j = half * 4 + t;
-                sk[j] = 0.f;
-                gv[j][0] = gv[j][1] = gv[j][2] = 0.f;
-                if (nb.id[j] < 0) continue;
-                float g3[3];
-                sk[j] = mlp_sdf<GRAD, kF, 3>(m, xk[t], g3);
-                if (GRAD) {
-                    if (PGO) quat_rotate_active(qt[t], g3[0], g3[1], g3[2], gv[j][0], gv[j][1], gv[j][2]);
-                    else { gv[j][0] = g3[0]; gv[j][1] = g3[1]; gv[j][2] = g3[2]; }
+                for (int a = 0; a < 3; ++a) {
+                    const float c = cu * in.pg[a];
+                    C[a] += c;
+                    A[a] = fmaf(sk[j], c, A[a]);
                 }
             }
         }
         float mean = 0.f;
 #pragma unroll
-        for (int j = 0; j < kK; ++j) mean = mean + sk[j] * nb.w[j];
+        for (int j = 0; j < kK; ++j) mean = mean + sk[j] * w[j];
         float var = 0.f;
 #pragma unroll
         for (int j = 0; j < kK; ++j) {
             const float dv = sk[j] - mean;
-            var = var + nb.w[j] * (dv * dv);
+            var = var + w[j] * (dv * dv);
         }
         sdf = mean;
         std_v = sqrtf(var);
         if (GRAD && nn > 0) {
 #pragma unroll
-            for (int j = 0; j < kK; ++j) {
-                const float coef = -2.f * nb.u[j] * nb.u[j] * (sk[j] - mean) * invS;
-#pragma unroll
-                for (int d = 0; d < 3; ++d) gq[d] = fmaf(coef, nb.pg[j][d], gq[d]);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) gq[d] = fmaf(nb.w[j], gv[j][d], gq[d]);
-            }
+            for (int a = 0; a < 3; ++a) gq[a] = A[a] - mean * C[a] + G[a];
         }
     }
     if (sdf_out) sdf_out[i] = sdf;
@@ -296,7 +346,7 @@ __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoin
     const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
     TopK tk;
     tk.init();
-    const int nn = src.template scan<kChunk>(qx, qy, qz, tk);
+    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
     Neighbours nb;
     load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
     const float cert = (cert_out && p.certainties) ? gather_certainty(src, nb) : 0.f;
