@@ -172,6 +172,35 @@ int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32
 int pin_query_certainty(const PinHash* hash, const PinPoints* pts, const float* q, int64_t n,
                         float* certainty_out, void* stream);
 
+/* Registration validity / robust-weight parameters (utils/tracker.py:277-394). */
+typedef struct PinRegParams {
+    int32_t min_nn_count;        /* mask = nn_count >= query_nn_k (:286-287) */
+    float min_grad_norm;         /* reg_min_grad_norm */
+    float max_grad_norm;         /* reg_max_grad_norm */
+    float max_sdf_std;           /* surface_sample_range_m * max_sdf_std_ratio (only if sdf_std given) */
+    float gm_dist;               /* reg_GM_dist_m, <= 0: no residual weight */
+    float gm_grad;               /* reg_GM_grad, <= 0: no gradient weight */
+} PinRegParams;
+
+/* accumulator layout of pin_reg_normal_eq's output */
+#define PIN_REG_NACC 31          /* [0] sum w, [1] sum |r|, [2] sum w r^2, [3] n_valid,
+                                    [4..24] sum w J^T J (upper triangle, row major),
+                                    [25..30] sum w r J,  J = [p x g, g] */
+#define PIN_REG_WORKSPACE_DOUBLES (1024 * PIN_REG_NACC)
+
+/*
+ * pin_reg_normal_eq -- fused validity mask + Geman-McClure weights + f64 normal-equation
+ * accumulation of one registration step (utils/tracker.py:303-394 and implicit_reg :468-480),
+ * deterministic (fixed-order two-level reduction).  sdf_std / sdf_label may be NULL (no std
+ * test / zero labels); valid_out (n bytes, may be NULL) receives the validity mask.
+ * weight != NULL: every point is valid and w_i = weight[i] (implicit_reg on pre-filtered,
+ * pre-weighted rows, :468-496); nn_count may then be NULL.
+ * out[PIN_REG_NACC] doubles (device); workspace PIN_REG_WORKSPACE_DOUBLES doubles.
+ */
+int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, const int32_t* nn_count,
+                      const float* sdf_std, const float* sdf_label, const float* weight, int64_t n,
+                      const PinRegParams* prm, double* workspace, double* out, uint8_t* valid_out, void* stream);
+
 /* Workspace bytes pin_grid_mark needs for a grid of nb bricks. */
 static inline int64_t pin_grid_workspace_bytes(int64_t num_bricks) {
     return ((num_bricks + 4095) / 4096) * 4 + 16;

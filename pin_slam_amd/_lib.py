@@ -46,6 +46,15 @@ class PinGrid(ctypes.Structure):
                 ("fat", i32)]
 
 
+class PinRegParams(ctypes.Structure):
+    _fields_ = [("min_nn_count", i32), ("min_grad_norm", f32), ("max_grad_norm", f32), ("max_sdf_std", f32),
+                ("gm_dist", f32), ("gm_grad", f32)]
+
+
+REG_NACC = 31
+REG_WORKSPACE_DOUBLES = 1024 * REG_NACC
+
+
 class PinMlp(ctypes.Structure):
     _fields_ = [("W1", c_void_p), ("b1", c_void_p), ("W2", c_void_p), ("b2", c_void_p), ("sdf_scale", f32),
                 ("reserved", i32)]
@@ -67,6 +76,8 @@ _SIGS = {
                               c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_scatter": [c_void_p, c_void_p, i64, i32, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_certainty": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p],
+    "pin_reg_normal_eq": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64,
+                          _P(PinRegParams), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_fill": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_void_p],

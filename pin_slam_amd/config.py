@@ -65,6 +65,10 @@ class Config:
         self.reg_GM_grad = 0.2
         self.reg_lm_lambda = 1e-4
         self.reg_iter_n = 50
+        self.reg_term_thre_deg = 0.01
+        self.reg_term_thre_m = 0.0005
+        self.eigenvalue_check = True
+        self.photometric_loss_on = False
         # mesher (:296-308)
         self.mc_res_m = 0.1
         self.mesh_min_nn = 8

@@ -1,0 +1,244 @@
+"""Drop-in ``Tracker`` (utils/tracker.py:19): point-to-implicit registration on the GPU.
+
+Per Gauss-Newton / LM iteration the reference evaluates ``query_feature`` + ``Decoder.sdf``
++ autograd ``get_gradient`` on every source point, filters, weights and forms a 6x6 system
+with torch ops (:176-496).  Here one iteration is:
+
+1. ``pin_query_sdf{,_grid}``: fused k-NN gather, IDW, decoder and closed-form dSDF/dq;
+2. ``pin_reg_normal_eq``: validity mask, Geman-McClure weights and the f64 normal equations
+   in one deterministic reduction;
+3. a 6x6 f64 solve on the host (the reference also moves these 36 numbers around with
+   ``.item()``-style syncs every iteration).
+
+The control flow of ``tracking`` (convergence, validity checks, fall-back to the initial
+guess) follows :39-174 line by line.  Colour / photometric registration is out of scope
+(off in every lidar config).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .query import query_sdf as fused_query_sdf
+
+
+def transform_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
+    """utils/tools.py:386-399: homogeneous [N,4] x T^T in the points' dtype."""
+    homo = torch.cat([points, torch.ones(points.shape[0], 1, device=points.device, dtype=points.dtype)], dim=1)
+    return torch.matmul(homo, transformation.to(points).T)[:, :3]
+
+
+def skew(v):
+    S = torch.zeros(3, 3, device=v.device, dtype=v.dtype)
+    S[0, 1] = -v[2]
+    S[0, 2] = v[1]
+    S[1, 2] = -v[0]
+    return S - S.T
+
+
+def expmap(axis_angle: torch.Tensor) -> torch.Tensor:
+    """utils/tracker.py:580-589 (Rodrigues)."""
+    angle = axis_angle.norm()
+    axis = axis_angle / angle
+    eye = torch.eye(3, device=axis_angle.device, dtype=axis_angle.dtype)
+    S = skew(axis)
+    return eye + S * torch.sin(angle) + (S @ S) * (1.0 - torch.cos(angle))
+
+
+def rotation_matrix_to_axis_angle(R: torch.Tensor):
+    """utils/tracker.py:591-599: rotation angle (rad) of R."""
+    return torch.acos((torch.trace(R) - 1) / 2)
+
+
+def _solve(acc: np.ndarray, lm_lambda: float, require_cov: bool, require_eigen: bool, device):
+    """Normal equations from the kernel accumulators -> (dT 4x4 f64, cov, eigenvalues).
+    The weight normalisation w /= 2 mean(w) (utils/tracker.py:394) is the factor
+    n / (2 sum w) on N and g."""
+    s_w, s_r, s_wr2, cnt = acc[0], acc[1], acc[2], acc[3]
+    scale = cnt / (2.0 * s_w)
+    N = np.zeros((6, 6))
+    k = 4
+    for a in range(6):
+        for b in range(a, 6):
+            N[a, b] = N[b, a] = acc[k]
+            k += 1
+    N *= scale
+    g = -acc[25:31] * scale
+    N_old = N.copy()
+    N = N + lm_lambda * np.diag(np.diag(N))
+    t = np.linalg.inv(N) @ g
+    tt = torch.tensor(t, dtype=torch.float64, device=device)
+    T = torch.eye(4, dtype=torch.float64, device=device)
+    T[:3, :3] = expmap(tt[:3])
+    T[:3, 3] = tt[3:]
+    eig = None
+    if require_eigen:
+        eig = torch.linalg.eigvals(torch.tensor(N_old[3:, 3:], dtype=torch.float64, device=device)).real
+    cov = None
+    if require_cov:
+        mse = s_wr2 / (2.0 * s_w)  # mean(w_norm * r^2)
+        cov = torch.tensor(np.linalg.inv(N_old) * mse, dtype=torch.float64, device=device)
+    return T, cov, eig
+
+
+def implicit_reg(points, sdf_grad, sdf_residual, weight, lm_lambda=0.0, require_cov=False, require_eigen=False):
+    """utils/tracker.py:468-520 on pre-filtered rows with given weights (HIP accumulation,
+    f64 6x6 solve).  Returns (T, cov_mat, eigenvalues)."""
+    _lib.require_device(points)
+    p = points.detach().to(torch.float32).contiguous()
+    g = sdf_grad.detach().to(torch.float32).contiguous()
+    r = sdf_residual.detach().to(torch.float32).contiguous().view(-1)
+    w = weight.detach().to(torch.float32).contiguous().view(-1)
+    acc = _reg_accumulate(p, r, g, None, None, None, w, _lib.PinRegParams())
+    # the caller's weights are already normalised: undo the kernel-side n/(2 sum w) factor
+    a = acc.copy()
+    a[4:] *= 2.0 * a[0] / a[3]
+    T, cov, eig = _solve(a, lm_lambda, require_cov, require_eigen, points.device)
+    if require_cov:
+        cov = cov * (2.0 * a[0] / a[3])
+    return T, cov, eig
+
+
+def _reg_accumulate(points, sdf, grad, nn_count, sdf_std, label, weight, prm, valid_out=None):
+    dev = points.device
+    ws = torch.empty(_lib.REG_WORKSPACE_DOUBLES, dtype=torch.float64, device=dev)
+    out = torch.empty(_lib.REG_NACC, dtype=torch.float64, device=dev)
+    _lib.call("pin_reg_normal_eq", _lib.ptr(points), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count),
+              _lib.ptr(sdf_std), _lib.ptr(label), _lib.ptr(weight), points.shape[0], prm, _lib.ptr(ws),
+              _lib.ptr(out), _lib.ptr(valid_out), _lib.stream())
+    return out.cpu().numpy()
+
+
+class Tracker:
+
+    def __init__(self, config, neural_points, geo_decoder, sem_decoder=None, color_decoder=None):
+        self.config = config
+        self.silence = config.silence
+        self.neural_points = neural_points
+        self.geo_decoder = geo_decoder
+        self.sem_decoder = sem_decoder
+        self.color_decoder = color_decoder
+        self.device = config.device
+        self.dtype = config.dtype
+        self.sdf_scale = config.logistic_gaussian_ratio * config.sigma_sigmoid_m
+
+    # ------------------------------------------------------------------ utils/tracker.py:39-174
+    def tracking(self, source_points, init_pose=None, source_colors=None, source_normals=None,
+                 source_semantics=None, source_sdf=None, cur_ts=None, loop_reg: bool = False,
+                 vis_result: bool = False):
+        cfg = self.config
+        T = torch.eye(4, dtype=torch.float64, device=self.device) if init_pose is None else init_pose
+        cov_mat = None
+        min_grad_norm = cfg.reg_min_grad_norm
+        max_grad_norm = cfg.reg_max_grad_norm
+        cur_GM_dist_m = cfg.reg_GM_dist_m if cfg.reg_GM_dist_m > 0 else None
+        cur_GM_grad = cfg.reg_GM_grad if cfg.reg_GM_grad > 0 else None
+        lm_lambda = cfg.reg_lm_lambda
+        iter_n = cfg.reg_iter_n
+        term_thre_deg = cfg.reg_term_thre_deg
+        term_thre_m = cfg.reg_term_thre_m
+        max_valid_final_sdf_residual_cm = cfg.surface_sample_range_m * 0.5 * 100.0
+        min_valid_ratio = 0.2
+        if loop_reg:
+            max_valid_final_sdf_residual_cm = cfg.surface_sample_range_m * 0.6 * 100.0
+            min_valid_ratio = 0.15
+        max_increment_sdf_residual_ratio = 1.1
+        eigenvalue_ratio_thre = 0.01
+        min_valid_points = 30
+        converged = False
+        valid_flag = True
+        last_sdf_residual_cm = 1e5
+        source_point_count = source_points.shape[0]
+        if source_sdf is None:
+            source_sdf = torch.zeros(source_point_count, device=self.device)
+        weight_point_cloud = None
+        eigenvalues = None
+        sdf_residual_cm = 0.0
+        valid_point_count = 0
+        for i in range(iter_n):
+            cur_points = transform_torch(source_points, T)
+            reg = self.registration_step(cur_points, source_normals, source_sdf, source_colors, cur_ts,
+                                         min_grad_norm, max_grad_norm, cur_GM_dist_m, cur_GM_grad, lm_lambda,
+                                         (vis_result and converged))
+            delta_T, cov_mat, eigenvalues, weight_point_cloud, valid_points, sdf_residual_cm, _ = reg
+            T = delta_T @ T
+            if (sdf_residual_cm - last_sdf_residual_cm) / last_sdf_residual_cm > max_increment_sdf_residual_ratio:
+                if not self.silence:
+                    print("(Warning) registration failed: wrong optimization")
+                valid_flag = False
+            else:
+                last_sdf_residual_cm = sdf_residual_cm
+            valid_point_count = valid_points.shape[0]
+            if valid_point_count < min_valid_points or 1.0 * valid_point_count / source_point_count < min_valid_ratio:
+                if not self.silence:
+                    print("(Warning) registration failed: not enough valid points")
+                valid_flag = False
+            if not valid_flag or converged:
+                break
+            rot_angle_deg = rotation_matrix_to_axis_angle(delta_T[:3, :3]) * 180.0 / np.pi
+            tran_m = delta_T[:3, 3].norm()
+            if abs(rot_angle_deg) < term_thre_deg and tran_m < term_thre_m or i == iter_n - 2:
+                converged = True
+        if sdf_residual_cm > max_valid_final_sdf_residual_cm:
+            if not self.silence:
+                print("(Warning) registration failed: too large final residual")
+            valid_flag = False
+        if eigenvalues is not None:
+            min_eigenvalue = torch.min(eigenvalues).item()
+            if cfg.eigenvalue_check and min_eigenvalue < valid_point_count * eigenvalue_ratio_thre:
+                if not self.silence:
+                    print("(Warning) registration failed: eigenvalue check failed")
+                valid_flag = False
+        if cov_mat is not None:
+            cov_mat = cov_mat.detach().cpu().numpy()
+        if not valid_flag:
+            T = init_pose
+            cov_mat = None
+        return T, cov_mat, weight_point_cloud, valid_flag
+
+    # ------------------------------------------------------------------ utils/tracker.py:176-275
+    def query_source_points(self, coord, ts, bs, query_sdf=True, query_sdf_grad=True, query_color=False,
+                            query_color_grad=False, query_sem=False, query_mask=True, query_certainty=True,
+                            query_locally=True, mask_min_nn_count: int = 4):
+        """Returns (sdf_pred, sdf_grad, color_pred, color_grad, sem_pred, mc_mask, certainty, sdf_std).
+        One fused launch covers all points (the reference's bs batching is a memory bound, not a
+        semantic one)."""
+        if query_color or query_color_grad or query_sem:
+            raise NotImplementedError("colour / semantic heads are out of scope")
+        sdf, grad, nn, cert, std = fused_query_sdf(self.neural_points, self.geo_decoder, coord, query_locally=query_locally,
+                                             want_grad=query_sdf_grad, want_std=True, want_certainty=query_certainty)
+        mc_mask = nn >= mask_min_nn_count if query_mask else None
+        if not query_sdf:
+            sdf, std = None, None
+        return sdf, grad, None, None, None, mc_mask, cert, std
+
+    # ------------------------------------------------------------------ utils/tracker.py:277-452
+    def registration_step(self, points, normals, sdf_labels, colors, cur_ts, min_grad_norm, max_grad_norm,
+                          GM_dist=None, GM_grad=None, lm_lambda=0.0, vis_weight_pc=False):
+        if colors is not None and getattr(self.config, "photometric_loss_on", False):
+            raise NotImplementedError("photometric registration is out of scope")
+        if normals is not None:
+            raise NotImplementedError("normal-consistency weights are not used by any reference config")
+        cfg = self.config
+        pts = points.detach().to(torch.float32).contiguous()
+        sdf, grad, nn, _, std = fused_query_sdf(self.neural_points, self.geo_decoder, pts, query_locally=True,
+                                          want_grad=True, want_std=not cfg.weighted_first, want_certainty=False)
+        max_sdf_std = cfg.surface_sample_range_m * cfg.max_sdf_std_ratio
+        prm = _lib.PinRegParams(min_nn_count=int(cfg.query_nn_k), min_grad_norm=float(min_grad_norm),
+                                max_grad_norm=float(max_grad_norm), max_sdf_std=float(max_sdf_std),
+                                gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
+                                gm_grad=float(GM_grad) if GM_grad is not None else 0.0)
+        if cfg.weighted_first:
+            std = None  # reference: sdf_std stays 0 < max_sdf_std
+        labels = sdf_labels.detach().to(torch.float32).contiguous() if sdf_labels is not None else None
+        valid = torch.empty(pts.shape[0], dtype=torch.uint8, device=pts.device)
+        acc = _reg_accumulate(pts, sdf, grad, nn, std, labels, None, prm, valid)
+        valid_points = points[valid.bool()]
+        cnt = int(acc[3])
+        if cnt < 10:
+            T = torch.eye(4, device=points.device, dtype=torch.float64)
+            return T, None, None, None, valid_points, 0.0, 0.0
+        sdf_residual_cm = float(acc[1] / cnt) * 100.0
+        T, cov, eig = _solve(acc, lm_lambda, vis_weight_pc, vis_weight_pc, points.device)
+        return T, cov, eig, None, valid_points, sdf_residual_cm, None

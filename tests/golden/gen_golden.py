@@ -379,11 +379,16 @@ def gen_tracker_case(name, cfg_kwargs, n_side, n_src, seed):
                                     cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
                                     cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, False)
     delta_T, _, _, _, valid_points, resid_cm, _ = res
+    # the whole registration loop (utils/tracker.py:39-174) from the identity guess
+    T_track, _, _, valid_track = tracker.tracking(pts, torch.eye(4, dtype=torch.float64), cur_ts=9)
     rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
                num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
                source=src, sdf=sdf_pred.numpy(), grad=sdf_grad.numpy(), mask=mask.numpy(),
                certainty=certainty.numpy(), sdf_std=sdf_std.numpy(),
                delta_T=delta_T.numpy(), valid_count=np.int64(valid_points.shape[0]),
+               tracking_T=T_track.numpy(), tracking_valid=np.bool_(valid_track),
+               reg_iter_n=np.int64(cfg.reg_iter_n), reg_term_thre_deg=np.float64(cfg.reg_term_thre_deg),
+               reg_term_thre_m=np.float64(cfg.reg_term_thre_m),
                resid_cm=np.float64(resid_cm),
                reg_min_grad_norm=np.float64(cfg.reg_min_grad_norm),
                reg_max_grad_norm=np.float64(cfg.reg_max_grad_norm),
@@ -397,6 +402,7 @@ def gen_tracker_case(name, cfg_kwargs, n_side, n_src, seed):
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
     print(name, "valid", rec["valid_count"], "resid_cm", resid_cm)
     print(delta_T)
+    print("tracking", valid_track, T_track)
 
 
 def gen_mesher_case(name, cfg_kwargs, n_side, seed):

@@ -232,3 +232,45 @@ def test_backend_selection(golden, dev):
     with torch.no_grad():
         nm.neural_points += 0.37
     assert nm.backend() == "hash"
+
+
+@pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_registration_step_fixture(golden, dev, backend, case):
+    """Tracker.registration_step (utils/tracker.py:277-452) vs the reference's own step."""
+    from pin_slam_amd.tracker import Tracker
+    z = golden(case)
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
+    nm.local_geo_features = torch.nn.Parameter(torch.as_tensor(z["local_features"], device=dev))
+    dec = H.decoder_from_fixture(z, nm.config)
+    cfg = nm.config
+    cfg.surface_sample_range_m = float(z["surface_sample_range_m"])
+    cfg.max_sdf_std_ratio = float(z["max_sdf_std_ratio"])
+    tr = Tracker(cfg, nm, dec)
+    src = torch.as_tensor(z["source"], device=dev)
+    T, cov, eig, _, valid_points, resid_cm, _ = tr.registration_step(
+        src, None, torch.zeros(src.shape[0], device=dev), None, 9, float(z["reg_min_grad_norm"]),
+        float(z["reg_max_grad_norm"]), float(z["reg_GM_dist_m"]), float(z["reg_GM_grad"]), float(z["reg_lm_lambda"]))
+    assert abs(valid_points.shape[0] - int(z["valid_count"])) <= 2
+    assert resid_cm == pytest.approx(float(z["resid_cm"]), rel=1e-3)
+    np.testing.assert_allclose(_np(T), z["delta_T"], atol=5e-6)
+
+
+@pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
+def test_tracking_loop_fixture(golden, dev, case):
+    """The whole Tracker.tracking loop (utils/tracker.py:39-174: iterations, convergence,
+    validity checks, fall-back) from the identity guess vs the reference's own run."""
+    from pin_slam_amd.tracker import Tracker
+    z = golden(case)
+    nm = H.neural_points_from_fixture(z, dev)
+    nm.local_geo_features = torch.nn.Parameter(torch.as_tensor(z["local_features"], device=dev))
+    dec = H.decoder_from_fixture(z, nm.config)
+    cfg = nm.config
+    cfg.surface_sample_range_m = float(z["surface_sample_range_m"])
+    cfg.max_sdf_std_ratio = float(z["max_sdf_std_ratio"])
+    cfg.reg_iter_n = int(z["reg_iter_n"])
+    tr = Tracker(cfg, nm, dec)
+    src = torch.as_tensor(z["source"], device=dev)
+    T, cov, _, valid = tr.tracking(src, torch.eye(4, dtype=torch.float64, device=dev), cur_ts=9)
+    assert bool(valid) == bool(z["tracking_valid"])
+    np.testing.assert_allclose(_np(T), z["tracking_T"], atol=2e-5)
