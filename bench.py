@@ -10,6 +10,10 @@ in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
 batch against its replica of the map ("weak" scaling, no data-path collective);
 the barrier + max-over-ranks timing is the only collective.
 
+Second leg (key "mapper", configs[3]): mapper iterations/s of Mapper.mapping on a 4M-point
+map with 1M sampled queries per iteration per GPU, feature gradients SUM all-reduced over
+RCCL when N > 1 (see mapper_leg).
+
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
 mean kernel time from HIP events on the launch stream.  cpu_baseline: the numpy oracle
@@ -30,12 +34,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import pin_slam_amd as P  # noqa: E402
-from pin_slam_amd.synthetic import surface_map, surface_queries  # noqa: E402
+from pin_slam_amd.synthetic import surface_map, surface_pool, surface_queries  # noqa: E402
 
 N_SIDE = 1000            # 1,000,000 neural points
 N_QUERY = 262144
 BYTES_PER_QUERY = 944    # SURVEY.md 8(d), Kc=33, k=8, F=8
 HBM_PEAK = 8.0e12        # MI355X_MICROARCH.md (spec)
+MAPPER_SIDE = 2000       # 4,000,000 neural points (configs[3])
+MAPPER_BS = 1 << 20      # 1M sampled queries per iteration per GPU
+MAPPER_POOL = 1 << 22    # training-sample pool
+
+
+def mapper_bytes_per_iter(n, L, dec=10):
+    """SURVEY.md 8(d) mapper bytes: forward 932 B/row over the batch + stencil rows, feature-grad
+    scatter 2*4*F*k = 512 B/row, dense Adam (read p,g,m,v; write p,m,v,g=0) 32 B per feature."""
+    rows = n + 6 * ((n + dec - 1) // dec)
+    return rows * (932 + 512) + 32 * 8 * (L + 1)
 
 
 def parse():
@@ -46,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--nwf", action="store_true", help="weighted_first=False variant (per-neighbour decoding)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hash", "grid"])
+    ap.add_argument("--no-mapper", action="store_true", help="skip the mapper leg (configs[3])")
+    ap.add_argument("--mapper-steps", type=int, default=10)
+    ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per launch (from profiles/), reported as roofline.traffic")
     return ap.parse_args()
@@ -70,6 +87,85 @@ def cpu_baseline(nm, dec, q, wf):
     return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"one full {qh.shape[0]}-query batch over the same 1M-point map, numpy oracle "
                       f"single-threaded, median of 3 ({t:.2f} s each)"}
+
+
+def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
+    """Oracle (numpy, 1 thread) mapper forward/backward on `sample` rows of one batch plus the
+    dense Adam over the whole map, extrapolated to a full batch (the map query work is linear
+    in the rows)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import pin_oracle as O
+    from tests.helpers import oracle_mlp, oracle_state
+    st = oracle_state(nm)
+    mlp = oracle_mlp(dec)
+    c = nm.config
+    dx = O.neighbor_offsets(2, 0.2)
+    ch, lh, th = coord[:sample].cpu().numpy(), label[:sample].cpu().numpy(), ts[:sample].cpu().numpy()
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        out = O.mapper_forward_backward(st, mlp, ch, lh, th, 8, dx, nm.max_valid_dist2, bool(c.weighted_first),
+                                        float(np.float32(0.055)), 0.5, 10, 0.3 * 0.2)
+        t_fb = time.perf_counter() - t0
+        m = np.zeros_like(st.local_features)
+        v = np.zeros_like(st.local_features)
+        t0 = time.perf_counter()
+        O.adam_step(st.local_features, out["feat_grad"], m, v, 1, 0.01)
+        t_adam = time.perf_counter() - t0
+    n = coord.shape[0]
+    t_iter = t_fb * (n / sample) + t_adam
+    return {"value": 1.0 / t_iter, "unit": "iters/s", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle single-threaded: forward+backward of {sample} of the {n} batch rows "
+                      f"({t_fb:.2f} s, scaled x{n / sample:.0f}) + dense Adam over the map ({t_adam:.2f} s)"}
+
+
+def mapper_leg(args, dev, world, rank):
+    """configs[3]: Mapper.mapping on a 4M-point map, 1M sampled queries per iteration per GPU
+    (+ 6 x 100K numerical-gradient stencil rows), BCE + 0.5 eikonal, Adam on the features
+    (decoder frozen, the steady state after freeze_after_frame).  W > 1: per-rank batches,
+    feature gradients SUM all-reduced over RCCL every iteration (weak scaling)."""
+    wf = not args.nwf
+    nm, dec, pts = surface_map(MAPPER_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf,
+                               query_backend=args.backend, bs=MAPPER_BS)
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    coord, label, ts = surface_pool(pts, MAPPER_POOL, seed=11 + rank, device=dev)
+    mapper = P.Mapper(nm.config, None, nm, dec, group=dist.group.WORLD if world > 1 else None)
+    mapper.set_pool(coord, label, ts)
+    torch.manual_seed(1234 + rank)
+    backend = nm.backend()
+    mapper.mapping(max(args.mapper_warmup, 1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    mapper.mapping(args.mapper_steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    L = int(nm.local_neural_points.shape[0])
+    bpi = mapper_bytes_per_iter(MAPPER_BS, L)
+    ms = elapsed / args.mapper_steps * 1e3
+    res = {"metric": "mapper iters/sec", "value": args.mapper_steps / elapsed, "unit": "iters/s",
+           "queries_per_sec": MAPPER_BS * world * args.mapper_steps / elapsed, "ms_per_iter": ms,
+           "steps": args.mapper_steps, "warmup": args.mapper_warmup, "scaling": "weak",
+           "config": {"workload": "Mapper.mapping, 4M-point map, 1M queries/iter/GPU + numerical-gradient "
+                                  "stencil (configs[3])", "map_points": int(pts.shape[0]),
+                      "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",
+                      "grad_allreduce": "RCCL SUM, 128 MB/iter" if world > 1 else None,
+                      "candidate_backend": backend, "timed": "mapping(K): K iterations + Adam state init + "
+                                                             "assign_local_to_global"},
+           "roofline": {"bound": "hbm", "achieved": bpi / (ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
+                        "unit": "GB/s", "frac": bpi / (ms * 1e-3) / HBM_PEAK, "traffic": None,
+                        "scope": "whole iteration", "algorithmic_bytes_per_iter": bpi}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        idx = torch.randint(0, MAPPER_POOL, (MAPPER_BS,), device=dev)
+        res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx], ts[idx], 16384)
+    return res
 
 
 def main():
@@ -153,6 +249,9 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
+    del nm, dec, pts, q
+    if not args.no_mapper:
+        out["mapper"] = mapper_leg(args, dev, world, rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -238,6 +238,81 @@ int pin_query_feature_fwd_grid(const PinGrid* grid, const PinPoints* pts, const 
                                int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts,
                                float* certainty, int32_t* ids, int32_t* gids, void* stream);
 
+/* One mapping iteration (utils/mapper.py:443-572): the main batch of n_main rows and the
+ * numerical-gradient stencil of 6*n_stencil rows generated from coord[::decimation]
+ * (mapper.py:683-711; row n_main + b*n_stencil + k is coord[k*decimation] +- eps along axis
+ * b/2, + for even b). */
+typedef struct PinTrainCfg {
+    int64_t n_main;              /* N, rows of the batch */
+    int64_t n_stencil;           /* ceil(N / decimation), 0 disables the eikonal term */
+    int32_t decimation;          /* gradient_decimation */
+    int32_t nn_k;                /* query_nn_k */
+    int32_t weighted_first;
+    float eps;                   /* float32(voxel_size_m * num_grad_step_ratio) */
+    float sigma;                 /* BCE scale, Mapper.sdf_scale (mapper.py:521, loss.py:40-47) */
+    float weight_e;              /* eikonal weight (mapper.py:547) */
+    float grad_scale;            /* multiplies loss and gradients: 1, or 1/world_size so that a SUM
+                                    all-reduce of per-rank gradients is the gradient of the mean loss */
+    int32_t reserved;
+} PinTrainCfg;
+
+/* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
+typedef struct PinTrainState {
+    int32_t* ids;                /* [rows, nn_k] local feature rows, -1 invalid */
+    float* weights;              /* [rows, nn_k] IDW weights */
+    float* x;                    /* weighted_first: [rows, 11] decoder input; else [rows, nn_k, 3] vectors */
+    float* sdf;                  /* [rows] predicted sdf */
+    float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL */
+    int64_t* ts_update;          /* [L] amax with the main rows' ts (neural_points.py:644), may be NULL */
+} PinTrainState;
+
+/* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */
+typedef struct PinAdamStep {
+    float neg_step_size;         /* float32(-lr / (1 - beta1^t)) */
+    float one_minus_beta1;       /* lerp weight */
+    float beta2;
+    float one_minus_beta2;
+    float bias_correction2_sqrt; /* float32(sqrt(1 - beta2^t)) */
+    float eps;                   /* adam_eps */
+    int32_t zero_grad;           /* 1: grad := 0 after the step (opt.zero_grad of the next iteration) */
+    int32_t reserved;
+} PinAdamStep;
+
+/* decoder-parameter gradient layout of pin_train_backward's mlp_grad */
+#define PIN_MLP_GRAD_SIZE (PIN_HIDDEN_DIM * (PIN_FEATURE_DIM + 3) + 2 * PIN_HIDDEN_DIM + 1) /* W1,b1,W2,b2 */
+
+/*
+ * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping
+ * iteration (mapper.py:461-468, :683-711; neural_points.py:528-674 with training_mode): fills
+ * st->ids/weights/x/sdf and applies the certainty / ts_update side effects with atomics.
+ * Exactly one of hash / grid is non-NULL (grid: non-fat, features read live).
+ */
+int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp,
+                      const float* coord, const int64_t* ts, const PinTrainCfg* cfg, const PinTrainState* st,
+                      void* stream);
+
+/* Workspace bytes of pin_train_backward for rows = n_main + 6 n_stencil. */
+static inline int64_t pin_train_workspace_bytes(int64_t rows) {
+    const int64_t nblk = (rows + 255) / 256;
+    return nblk * 4 * 8 + nblk * PIN_MLP_GRAD_SIZE * 4;
+}
+
+/*
+ * pin_train_backward -- gradient of  BCEWithLogits(sdf/sigma, sigmoid(label/sigma)) (mean)
+ *   + weight_e * mean_k (|g_k| - 1)^2,  g_k = central differences of the stencil rows
+ * (mapper.py:515-547) w.r.t. the local features (grad_features [L+1,8] += , may be NULL) and,
+ * if mlp_grad != NULL, the decoder parameters (mlp_grad [PIN_MLP_GRAD_SIZE] += , summed in a
+ * fixed order).  loss_out (1 double on the device, may be NULL) receives the loss.  workspace:
+ * pin_train_workspace_bytes(rows) bytes, needed when loss_out or mlp_grad is non-NULL.
+ */
+int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* label, const PinTrainCfg* cfg,
+                       const PinTrainState* st, float* grad_features, float* mlp_grad, void* workspace,
+                       double* loss_out, void* stream);
+
+/* pin_adam_step -- dense Adam over n floats in place (torch.optim.Adam, weight_decay 0). */
+int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,12 +4,16 @@ hot path of PIN-SLAM (kelly7707/PIN_SLAM).
 Drop-in classes mirror the reference's Python API:
     pin_slam_amd.NeuralPoints   <- model/neural_points.py:NeuralPoints
     pin_slam_amd.Decoder        <- model/decoder.py:Decoder
+    pin_slam_amd.Mapper         <- utils/mapper.py:Mapper (training path)
+    pin_slam_amd.Tracker        <- utils/tracker.py:Tracker (registration path)
 The compute runs in hand-written HIP kernels for gfx950 (libpin_slam_amd.so,
 C ABI in include/pin_slam_amd.h).
 """
 from .config import Config
 from .decoder import Decoder
+from .mapper import Mapper
 from .neural_points import NeuralPoints
 from .query import query_sdf
+from .tracker import Tracker
 
-__all__ = ["Config", "Decoder", "NeuralPoints", "query_sdf"]
+__all__ = ["Config", "Decoder", "Mapper", "NeuralPoints", "Tracker", "query_sdf"]

@@ -60,6 +60,23 @@ class PinMlp(ctypes.Structure):
                 ("reserved", i32)]
 
 
+class PinTrainCfg(ctypes.Structure):
+    _fields_ = [("n_main", i64), ("n_stencil", i64), ("decimation", i32), ("nn_k", i32), ("weighted_first", i32),
+                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("reserved", i32)]
+
+
+class PinTrainState(ctypes.Structure):
+    _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
+                ("certainties", c_void_p), ("ts_update", c_void_p)]
+
+
+class PinAdamStep(ctypes.Structure):
+    _fields_ = [("neg_step_size", f32), ("one_minus_beta1", f32), ("beta2", f32), ("one_minus_beta2", f32),
+                ("bias_correction2_sqrt", f32), ("eps", f32), ("zero_grad", i32), ("reserved", i32)]
+
+
+MLP_GRAD_SIZE = HIDDEN_DIM * (FEATURE_DIM + 3) + 2 * HIDDEN_DIM + 1
+
 _P = ctypes.POINTER
 # name -> (argtypes) ; every function returns int
 _SIGS = {
@@ -85,6 +102,11 @@ _SIGS = {
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
+                          _P(PinTrainState), c_void_p],
+    "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
 }
 
 _lib = None

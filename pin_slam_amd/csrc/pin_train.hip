@@ -1,0 +1,412 @@
+// pin_train.hip -- one mapping iteration of utils/mapper.py:443-575 as three launches.
+//
+//  k_train_forward   main batch (N rows) + the numerical-gradient stencil (6 * N/dec rows,
+//                    generated in-kernel from coord[::dec] +- eps e_a, mapper.py:683-711):
+//                    training-mode query_feature (certainty scatter_add, ts amax on the main
+//                    rows, neural_points.py:637-648) + Decoder.sdf.  Saves per row the k ids,
+//                    IDW weights and the decoder input x for the backward.
+//  k_train_backward  dL/dsdf of  BCEWithLogits(sdf/s, sigmoid(label/s))  (loss.py:40-47) and of
+//                    weight_e * mean((|g| - 1)^2) through the stencil (mapper.py:546-547);
+//                    decoder backward; dL/dfeatures scattered with float atomics shaped as
+//                    8 lanes x 32 B per row; optional decoder-parameter gradients.
+//  k_adam            dense torch.optim.Adam step (tools.py:111-112) that also zeroes the grad.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "pin_device.h"
+
+using namespace pin;
+
+namespace {
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int launch_status() { return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP; }
+
+// row r of the iteration: a main query or a stencil query (x+,x-,y+,y-,z+,z- blocks)
+__device__ __forceinline__ void row_coord(const float* __restrict__ coord, const PinTrainCfg& c, int64_t r, float& qx,
+                                          float& qy, float& qz) {
+    if (r < c.n_main) {
+        qx = coord[3 * r];
+        qy = coord[3 * r + 1];
+        qz = coord[3 * r + 2];
+        return;
+    }
+    const int64_t s = r - c.n_main;
+    const int blk = (int)(s / c.n_stencil);
+    const int64_t b = (s % c.n_stencil) * c.decimation;
+    qx = coord[3 * b];
+    qy = coord[3 * b + 1];
+    qz = coord[3 * b + 2];
+    // x + eps e_a (even blk) or x - eps e_a (odd blk), mapper.py:697-702
+    if ((blk >> 1) == 0) qx = (blk & 1) ? qx - c.eps : qx + c.eps;
+    else if ((blk >> 1) == 1) qy = (blk & 1) ? qy - c.eps : qy + c.eps;
+    else qz = (blk & 1) ? qz - c.eps : qz + c.eps;
+}
+
+template <bool WF, class Src>
+__device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const PinMlp& m,
+                                                   const float* __restrict__ coord, const int64_t* __restrict__ ts,
+                                                   PinTrainCfg c, int64_t r, PinTrainState st) {
+    float qx, qy, qz;
+    row_coord(coord, c, r, qx, qy, qz);
+    TopK tk;
+    tk.init();
+    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    const int nn_k = c.nn_k;
+    float u[kK];
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        u[j] = (j < nn_k && tk.g[j] >= 0) ? 1.0f / (tk.d[j] + kIdwEps) : 0.f;
+        S = S + u[j];
+    }
+    float x[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) x[d] = 0.f;
+    float sdf = 0.f;
+    const int64_t qts = (ts && r < c.n_main) ? ts[r] : -1;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
+        const bool valid = u[j] > 0.f;
+        const float4 rc = src.record(tk.g[j]);
+        const int raw = __float_as_int(rc.w);
+        const int id = valid ? (raw & kIdMask) : -1;
+        float4 f0, f1;
+        src.features(tk.g[j], id > 0 ? id : 0, f0, f1);
+        float v0 = qx - rc.x, v1 = qy - rc.y, v2 = qz - rc.z;
+        if (valid && (raw & PIN_RECORD_UNFAITHFUL)) {
+            v0 = qx - p.positions[3 * (int64_t)id];
+            v1 = qy - p.positions[3 * (int64_t)id + 1];
+            v2 = qz - p.positions[3 * (int64_t)id + 2];
+        }
+        if (p.after_pgo && valid) quat_rotate_passive(((const float4*)p.orientations)[id], v0, v1, v2);
+        const float w = valid && nn > 0 ? u[j] / S : 0.f;
+        const float xj[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
+        if (j < nn_k) {
+            st.ids[r * nn_k + j] = id;
+            st.weights[r * nn_k + j] = w;
+        }
+        if (valid) {
+            // training side effects (neural_points.py:640, :644)
+            if (st.certainties) atomicAdd(st.certainties + id, w);
+            if (qts >= 0 && st.ts_update) atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
+        }
+        if (WF) {
+#pragma unroll
+            for (int d = 0; d < kD; ++d) x[d] = x[d] + (valid ? xj[d] : 0.f) * w;
+        } else {
+            float g3[3];
+            float sk = 0.f;
+            if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3);
+            sdf = sdf + sk * w;  // sum_j sdf_j w_j (mapper.py:467-468)
+            if (j < nn_k) {
+                float* xo = st.x + (r * nn_k + j) * 3;  // neighbour vectors for the backward
+                xo[0] = v0;
+                xo[1] = v1;
+                xo[2] = v2;
+            }
+        }
+    }
+    if (WF) {
+        float gx[kD];
+        sdf = mlp_sdf<false, 0, kD>(m, x, gx);
+#pragma unroll
+        for (int d = 0; d < kD; ++d) st.x[r * kD + d] = x[d];
+    }
+    st.sdf[r] = sdf;
+}
+
+template <bool WF>
+__global__ void __launch_bounds__(kBlock)
+k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
+                     const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= c.n_main + 6 * c.n_stencil) return;
+    const HashSource src(h, p);
+    train_forward_body<WF>(src, p, m, coord, ts, c, r, st);
+}
+
+template <bool WF>
+__global__ void __launch_bounds__(kBlock)
+k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
+                     const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= c.n_main + 6 * c.n_stencil) return;
+    const GridSource<false> src(g, p);
+    train_forward_body<WF>(src, p, m, coord, ts, c, r, st);
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
+
+// dL/dsdf of row r and its loss term (BCE rows: mean over N; stencil groups: weight_e * mean over N/dec)
+__device__ __forceinline__ float row_dsdf(const PinTrainCfg& c, const float* __restrict__ sdf,
+                                          const float* __restrict__ label, int64_t r, double& loss) {
+    loss = 0.0;
+    if (r < c.n_main) {
+        const float pz = sdf[r] / c.sigma;
+        const float y = sigmoidf_(label[r] / c.sigma);
+        loss = (double)fmaxf(pz, 0.f) - (double)pz * y + log1p(exp(-fabs((double)pz)));
+        loss /= (double)c.n_main;
+        return (sigmoidf_(pz) - y) / ((float)c.n_main * c.sigma);
+    }
+    const int64_t s = r - c.n_main;
+    const int blk = (int)(s / c.n_stencil);
+    const int64_t k = s % c.n_stencil;
+    const float* g6 = sdf + c.n_main + k;
+    const float two_eps = 2.f * c.eps;
+    const float gv[3] = {(g6[0] - g6[c.n_stencil]) / two_eps, (g6[2 * c.n_stencil] - g6[3 * c.n_stencil]) / two_eps,
+                         (g6[4 * c.n_stencil] - g6[5 * c.n_stencil]) / two_eps};
+    const float gn = sqrtf((gv[0] * gv[0] + gv[1] * gv[1]) + gv[2] * gv[2]);
+    if (blk == 0) loss = c.weight_e * (double)(gn - 1.f) * (gn - 1.f) / (double)c.n_stencil;
+    const float dg = c.weight_e * 2.f * (gn - 1.f) / (gn > 0.f ? gn : 1.f) / (float)c.n_stencil;
+    const float d_axis = dg * gv[blk >> 1] / two_eps;
+    return (blk & 1) ? -d_axis : d_axis;
+}
+
+// backward: one row per lane for the decoder; the row's k x 8 feature-gradient terms are staged
+// in LDS and scattered with 64 lanes covering 8 rows x 32 contiguous bytes per instruction.
+// Decoder-parameter gradients: wave shuffle sums -> per-block partials (fixed order, no
+// same-address atomics) -> k_mlp_grad_final.
+constexpr int kMlpGrad = PIN_MLP_GRAD_SIZE;
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// decoder backward of one input row x with upstream dL/d(out) = so (already times sdf_scale):
+// gf += sum_c delta_c W1[c][0:8]; decoder-parameter terms summed over the wave into mw (lane 0)
+template <bool MLP_GRAD>
+__device__ __forceinline__ void decoder_backward(const PinMlp& m, const float (&x)[kD], float so, float (&gf)[kF],
+                                                 float* __restrict__ mw, bool accumulate) {
+#pragma unroll 2
+    for (int cc = 0; cc < kH; ++cc) {
+        const float* wr = m.W1 + cc * kD;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kD; ++i) acc = fmaf(wr[i], x[i], acc);
+        const float pre = acc + m.b1[cc];
+        const bool on = pre > 0.f;
+        const float delta = on ? so * m.W2[cc] : 0.f;
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
+        if (MLP_GRAD) {
+            float dw[kD + 2];
+#pragma unroll
+            for (int i = 0; i < kD; ++i) dw[i] = wave_sum_f(delta * x[i]);
+            dw[kD] = wave_sum_f(delta);                       // b1
+            dw[kD + 1] = wave_sum_f(on ? so * pre : 0.f);     // W2
+            if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+                for (int i = 0; i < kD; ++i) mw[cc * kD + i] = (accumulate ? mw[cc * kD + i] : 0.f) + dw[i];
+                mw[kH * kD + cc] = (accumulate ? mw[kH * kD + cc] : 0.f) + dw[kD];
+                mw[kH * kD + kH + cc] = (accumulate ? mw[kH * kD + kH + cc] : 0.f) + dw[kD + 1];
+            }
+        }
+    }
+    if (MLP_GRAD) {
+        const float v = wave_sum_f(so);
+        if ((threadIdx.x & 63) == 0) mw[kMlpGrad - 1] = (accumulate ? mw[kMlpGrad - 1] : 0.f) + v;  // b2
+    }
+}
+
+template <bool WF, bool MLP_GRAD>
+__global__ void __launch_bounds__(kBlock)
+k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
+                 PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
+                 double* __restrict__ loss_part) {
+    constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
+    __shared__ float gst[kBlock * kJ * kF];
+    __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
+    const int64_t nrows = c.n_main + 6 * c.n_stencil;
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool live = r < nrows;
+    const int nn_k = c.nn_k;
+    const int wave = threadIdx.x >> 6;
+    double loss = 0.0;
+    const float dsdf = live ? row_dsdf(c, st.sdf, label, r, loss) * c.grad_scale : 0.f;
+    loss *= (double)c.grad_scale;
+    const float so = dsdf * m.sdf_scale;              // dL/d(lout output)
+    float* mw = MLP_GRAD ? mlds[wave] : nullptr;
+    if (WF) {
+        float x[kD];
+#pragma unroll
+        for (int d = 0; d < kD; ++d) x[d] = live ? st.x[r * kD + d] : 0.f;
+        float gf[kF];
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gf[d] = 0.f;
+        decoder_backward<MLP_GRAD>(m, x, so, gf, mw, false);
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = gf[d];
+    } else {
+        // per-neighbour decoder backward: dL/dsdf_j = dsdf * w_j (mapper.py:467-468)
+        for (int j = 0; j < kK; ++j) {
+            const int id = (live && j < nn_k) ? st.ids[r * nn_k + j] : -1;
+            const bool ok = id >= 0;
+            const float w = ok ? st.weights[r * nn_k + j] : 0.f;
+            float x[kD];
+            if (ok) {
+                const float4* fr = (const float4*)(p.features + (int64_t)id * kF);
+                const float4 f0 = fr[0], f1 = fr[1];
+                const float* v = st.x + (r * nn_k + j) * 3;
+                x[0] = f0.x; x[1] = f0.y; x[2] = f0.z; x[3] = f0.w;
+                x[4] = f1.x; x[5] = f1.y; x[6] = f1.z; x[7] = f1.w;
+                x[8] = v[0]; x[9] = v[1]; x[10] = v[2];
+            } else {
+#pragma unroll
+                for (int d = 0; d < kD; ++d) x[d] = 0.f;
+            }
+            float gf[kF];
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gf[d] = 0.f;
+            if (__any(ok) || MLP_GRAD) decoder_backward<MLP_GRAD>(m, x, so * w, gf, mw, j > 0);
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
+        }
+    }
+    {
+        const double v = [&] {
+            double t = loss;
+            for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+            return t;
+        }();
+        if ((threadIdx.x & 63) == 0 && loss_part) loss_part[(int64_t)blockIdx.x * kWaves + wave] = v;
+    }
+    __syncthreads();
+    if (MLP_GRAD) {
+        for (int e = threadIdx.x; e < kMlpGrad; e += kBlock) {
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) v += mlds[w][e];
+            mlp_part[(int64_t)blockIdx.x * kMlpGrad + e] = v;
+        }
+    }
+    if (!grad_features) return;
+    // scatter: element e = (row, j, d), d fastest
+    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
+    const int total = kBlock * nn_k * kF;
+    for (int e = threadIdx.x; e < total; e += kBlock) {
+        const int d = e & (kF - 1);
+        const int rj = e >> 3;
+        const int lr = rj / nn_k, j = rj - lr * nn_k;
+        const int64_t rr = row0 + lr;
+        if (rr >= nrows) break;
+        const int id = st.ids[rr * nn_k + j];
+        if (id < 0) continue;
+        const float g = WF ? st.weights[rr * nn_k + j] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        atomicAdd(grad_features + (int64_t)id * kF + d, g);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_loss_final(const double* __restrict__ part, int64_t n,
+                                                   double* __restrict__ out) {
+    double v = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += 64) v += part[i];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (threadIdx.x == 0) out[0] = v;
+}
+
+// mlp_grad[e] += sum_b part[b][e], fixed order
+__global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk,
+                                                           float* __restrict__ out) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= kMlpGrad) return;
+    float v = 0.f;
+    for (int64_t b = 0; b < nblk; ++b) v += part[b * kMlpGrad + e];
+    out[e] += v;
+}
+
+// torch.optim.Adam (single-tensor form, weight_decay 0):
+//   m = m + (1-b1)(g - m);  v = v b2 + ((1-b2) g) g;  p += (-lr/bc1 * m) / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void __launch_bounds__(kBlock)
+k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
+       PinAdamStep a) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float g = grad[i];
+    float m = m_[i], v = v_[i];
+    m = m + a.one_minus_beta1 * (g - m);
+    v = v * a.beta2;
+    v = v + (a.one_minus_beta2 * g) * g;
+    const float denom = sqrtf(v) / a.bias_correction2_sqrt + a.eps;
+    prm[i] = prm[i] + (a.neg_step_size * m) / denom;
+    m_[i] = m;
+    v_[i] = v;
+    if (a.zero_grad) grad[i] = 0.f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp,
+                      const float* coord, const int64_t* ts, const PinTrainCfg* cfg, const PinTrainState* st,
+                      void* stream) {
+    if (!pts || !mlp || !cfg || !st || !coord || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
+    if ((!hash && !grid) || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
+    if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    if (rows == 0) return PIN_OK;
+    auto s = as_stream(stream);
+    if (grid) {
+        if (cfg->weighted_first)
+            hipLaunchKernelGGL(k_train_forward_grid<true>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts, *mlp,
+                               coord, ts, *cfg, *st);
+        else
+            hipLaunchKernelGGL(k_train_forward_grid<false>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts, *mlp,
+                               coord, ts, *cfg, *st);
+    } else {
+        if (cfg->weighted_first)
+            hipLaunchKernelGGL(k_train_forward_hash<true>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts, *mlp,
+                               coord, ts, *cfg, *st);
+        else
+            hipLaunchKernelGGL(k_train_forward_hash<false>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts, *mlp,
+                               coord, ts, *cfg, *st);
+    }
+    return launch_status();
+}
+
+int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* label, const PinTrainCfg* cfg,
+                       const PinTrainState* st, float* grad_features, float* mlp_grad, void* workspace,
+                       double* loss_out, void* stream) {
+    if (!pts || !mlp || !cfg || !st || !label || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
+    if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    if (rows == 0) return PIN_OK;
+    if ((loss_out || mlp_grad) && !workspace) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    const dim3 g = grid_for(rows);
+    const int64_t nblk = g.x;
+    double* lpart = loss_out ? (double*)workspace : nullptr;
+    float* mpart = mlp_grad ? (float*)((char*)workspace + nblk * kWaves * sizeof(double)) : nullptr;
+#define PIN_LAUNCH_BWD(WF, MG)                                                                               \
+    hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
+                       grad_features, mpart, lpart)
+    if (cfg->weighted_first) {
+        if (mlp_grad) PIN_LAUNCH_BWD(true, true); else PIN_LAUNCH_BWD(true, false);
+    } else {
+        if (mlp_grad) PIN_LAUNCH_BWD(false, true); else PIN_LAUNCH_BWD(false, false);
+    }
+#undef PIN_LAUNCH_BWD
+    if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, s, lpart, nblk * kWaves, loss_out);
+    if (mlp_grad)
+        hipLaunchKernelGGL(k_mlp_grad_final, dim3((kMlpGrad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, mpart, nblk,
+                           mlp_grad);
+    return launch_status();
+}
+
+int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
+                  void* stream) {
+    if (!a || n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_adam, grid_for(n), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg, exp_avg_sq, n,
+                       *a);
+    return launch_status();
+}
+
+}  // extern "C"

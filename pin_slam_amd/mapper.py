@@ -1,0 +1,316 @@
+"""Drop-in for the training path of utils/mapper.py:Mapper.
+
+``mapping(iter_count)`` (utils/mapper.py:425-593) runs each iteration as three HIP launches
+(+ the Adam launches) instead of the reference's autograd graph:
+
+  pin_train_forward   batch rows + numerical-gradient stencil rows, training-mode
+                      query_feature (certainty / ts side effects) + Decoder.sdf
+  pin_train_backward  BCE + eikonal gradients, decoder backward, feature-gradient scatter,
+                      decoder-parameter gradients (only while the decoder is trainable)
+  pin_adam_step       torch.optim.Adam (fresh state per mapping() call, tools.py:89-116)
+
+and finishes with ``assign_local_to_global`` (neural_points.py:315-324) like the reference.
+
+Data parallel: with a process group of W > 1 ranks, every rank draws
+its own batch, the per-rank gradients are scaled by 1/W inside the backward and SUM
+all-reduced (RCCL over xGMI on ROCm), so every rank applies the same Adam step to its replica
+of the map.  Certainty deltas (SUM) and ts_update (MAX) are reconciled once at the end of
+mapping(): nothing inside an iteration reads them.
+
+``sdf`` and ``get_numerical_gradient`` mirror utils/mapper.py:670-733 on the autograd-capable
+drop-in query_feature for callers outside the fused loop.
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .query import mlp_view
+
+
+def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
+    """utils/tools.py:401-407."""
+    points = torch.matmul(transformation[:, :3, :3].to(points), points.unsqueeze(-1)) + \
+        transformation[:, :3, 3:].to(points)
+    return points.squeeze(-1)
+
+
+class _TrainBuffers:
+    """Per-row buffers of one iteration, reused across iterations and mapping() calls."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, rows, nn_k, wf, device):
+        key = (rows, nn_k, wf, str(device))
+        if key != self.key:
+            D = _lib.FEATURE_DIM + 3
+            self.ids = torch.empty((rows, nn_k), dtype=torch.int32, device=device)
+            self.weights = torch.empty((rows, nn_k), dtype=torch.float32, device=device)
+            self.x = torch.empty((rows, D) if wf else (rows, nn_k, 3), dtype=torch.float32, device=device)
+            self.sdf = torch.empty((rows,), dtype=torch.float32, device=device)
+            nblk = (rows + 255) // 256
+            self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_GRAD_SIZE * 4,), dtype=torch.uint8,
+                                         device=device)
+            self.loss = torch.zeros((1,), dtype=torch.float64, device=device)
+            self.key = key
+        return self
+
+
+class Mapper:
+    """utils/mapper.py:Mapper -- constructor signature, pools and training entry points."""
+
+    def __init__(self, config, dataset, neural_points, geo_mlp, sem_mlp=None, color_mlp=None, group=None):
+        self.config = config
+        self.silence = config.silence
+        self.dataset = dataset
+        self.neural_points = neural_points
+        self.geo_mlp = geo_mlp
+        self.sem_mlp = sem_mlp
+        self.color_mlp = color_mlp
+        self.device = config.device
+        self.dtype = config.dtype
+        self.used_poses = None
+        self.lose_track = False
+        # utils/mapper.py:50-54
+        self.require_gradient = False
+        if config.ekional_loss_on or getattr(config, "proj_correction_on", False) or \
+                getattr(config, "consistency_loss_on", False):
+            self.require_gradient = True
+        if config.numerical_grad and not getattr(config, "proj_correction_on", False) and \
+                not getattr(config, "consistency_loss_on", False):
+            self.require_gradient = False
+        self.total_iter = 0
+        self.sdf_scale = config.logistic_gaussian_ratio * config.sigma_sigmoid_m
+        self.new_idx = None
+        self.ba_done_flag = False
+        self.train_less = False
+        dev, dt = self.device, self.dtype
+        self.coord_pool = torch.empty((0, 3), device=dev, dtype=dt)
+        self.global_coord_pool = torch.empty((0, 3), device=dev, dtype=dt)
+        self.sdf_label_pool = torch.empty((0,), device=dev, dtype=dt)
+        self.color_pool = None
+        self.sem_label_pool = None
+        self.normal_label_pool = None
+        self.weight_pool = torch.empty((0,), device=dev, dtype=dt)
+        self.time_pool = torch.empty((0,), device=dev, dtype=torch.long)
+        self.pool_sample_count = 0
+        self.group = group
+        self.last_loss = None        # device f64 tensor: loss of the last iteration
+        self._buf = _TrainBuffers()
+        self._adam_t = 0
+
+    # ---------------------------------------------------------------- data pool
+    def set_pool(self, coord, sdf_label, ts, weight=None, global_coord=None):
+        """Install a training-sample pool (the output of Mapper.process_frame, utils/mapper.py:110-321)."""
+        self.coord_pool = coord
+        self.global_coord_pool = coord if global_coord is None else global_coord
+        self.sdf_label_pool = sdf_label
+        self.time_pool = ts
+        self.weight_pool = torch.ones_like(sdf_label) if weight is None else weight
+        self.pool_sample_count = int(sdf_label.shape[0])
+
+    def get_batch(self, global_coord=False):
+        """utils/mapper.py:323-361."""
+        stop = getattr(self.dataset, "stop_status", False) if self.dataset is not None else False
+        bs = int(self.config.bs)
+        bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
+        if bs_new_sample > 0 and self.new_idx is not None and not self.lose_track and not stop:
+            new_idx_count = self.new_idx.shape[0]
+            if new_idx_count > 0:
+                bs_new = min(new_idx_count, bs_new_sample)
+                bs_history = bs - bs_new
+                index_history = torch.randint(0, self.pool_sample_count, (bs_history,), device=self.device)
+                index_new_batch = torch.randint(0, new_idx_count, (bs_new,), device=self.device)
+                index = torch.cat((index_history, self.new_idx[index_new_batch]), dim=0)
+            else:
+                index = torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+        else:
+            index = torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+        coord = self.global_coord_pool[index, :] if global_coord else self.coord_pool[index, :]
+        sdf_label = self.sdf_label_pool[index]
+        ts = self.time_pool[index]
+        weight = self.weight_pool[index]
+        sem_label = self.sem_label_pool[index] if self.sem_label_pool is not None else None
+        color_label = self.color_pool[index] if self.color_pool is not None else None
+        normal_label = self.normal_label_pool[index, :] if self.normal_label_pool is not None else None
+        return coord, sdf_label, ts, normal_label, sem_label, color_label, weight
+
+    # ---------------------------------------------------------------- training
+    def _check_supported(self):
+        c = self.config
+        if c.main_loss_type != "bce":
+            raise NotImplementedError("fused mapping implements main_loss_type 'bce' (utils/loss.py:40-47)")
+        if getattr(c, "semantic_on", False) or getattr(c, "color_on", False):
+            raise NotImplementedError("fused mapping implements the geometric decoder only")
+        if getattr(c, "proj_correction_on", False) or getattr(c, "consistency_loss_on", False):
+            raise NotImplementedError("proj_correction / consistency losses are not on the fused path")
+        if c.ekional_loss_on and c.weight_e > 0:
+            if not c.numerical_grad:
+                raise NotImplementedError("analytic-gradient eikonal (double backward) is not on the fused path")
+            if getattr(c, "ekional_add_to", "all") != "all":
+                raise NotImplementedError("fused mapping implements ekional_add_to 'all'")
+        if getattr(c, "loss_weight_on", False):
+            raise NotImplementedError("fused mapping implements the unweighted BCE (loss_weight_on False)")
+
+    def _world(self):
+        if self.group is False or not dist.is_available() or not dist.is_initialized():
+            return 1
+        return dist.get_world_size(self.group)
+
+    def mapping(self, iter_count):
+        """utils/mapper.py:425-593 (iteration body :443-575)."""
+        if self.train_less:
+            iter_count = max(1, iter_count - 5)
+        self._check_supported()
+        c = self.config
+        nm = self.neural_points
+        feats = nm.local_geo_features
+        _lib.require_device(feats.data)
+        mlp_params = [p for p in self.geo_mlp.parameters() if p.requires_grad]
+        train_mlp = len(mlp_params) > 0
+        if train_mlp and len(mlp_params) != 4:
+            raise NotImplementedError("fused mapping trains the whole 11->64->1 decoder or none of it")
+        world = self._world()
+        dev = feats.device
+        # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441)
+        fdata = feats.data
+        f_grad = torch.zeros_like(fdata)
+        f_m = torch.zeros_like(fdata)
+        f_v = torch.zeros_like(fdata)
+        if train_mlp:
+            m_grad = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+            m_m = torch.zeros_like(m_grad)
+            m_v = torch.zeros_like(m_grad)
+        cert_before = nm.local_point_certainties.clone() if world > 1 else None
+        self._adam_t = 0
+        for _ in range(iter_count):
+            coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
+            if self.ba_done_flag:
+                coord = transform_batch_torch(coord, self.used_poses[ts])
+            self.train_step(coord, sdf_label, ts, f_grad, m_grad if train_mlp else None, world)
+            self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad if train_mlp else None,
+                       m_m if train_mlp else None, m_v if train_mlp else None)
+            self.total_iter += 1
+        if world > 1:
+            self._sync_side_effects(cert_before)
+        nm.assign_local_to_global()
+
+    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1):
+        """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
+        SUM all-reduced over the group when world > 1.  Returns the device loss tensor."""
+        c = self.config
+        nm = self.neural_points
+        q = coord.detach().to(torch.float32).contiguous()
+        _lib.require_device(q)
+        label = sdf_label.detach().to(torch.float32).contiguous()
+        ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
+        n = q.shape[0]
+        dec = int(c.gradient_decimation)
+        eik = bool(c.ekional_loss_on and c.weight_e > 0)
+        nd = (n + dec - 1) // dec if eik else 0
+        nn_k = int(c.query_nn_k)
+        wf = bool(c.weighted_first)
+        rows = n + 6 * nd
+        b = self._buf.get(rows, nn_k, wf, q.device)
+        cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
+                               eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
+                               sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
+                               grad_scale=float(np.float32(1.0 / world)), reserved=0)
+        hv, pv = nm._views("local", True)
+        st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
+                                sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
+                                ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None)
+        mv = mlp_view(self.geo_mlp)
+        if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
+            raise RuntimeError("local_geo_features must be a contiguous float32 tensor")
+        s = _lib.stream()
+        if nm.backend() == "grid":
+            gv = nm.grid_view("local", False)
+            _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), _lib.ptr(ts64),
+                      ctypes.byref(cfg), ctypes.byref(st), s)
+        else:
+            _lib.call("pin_train_forward", hv.ref(), None, pv.ref(), mv.ref(), _lib.ptr(q), _lib.ptr(ts64),
+                      ctypes.byref(cfg), ctypes.byref(st), s)
+        _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
+                  _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
+        if world > 1:
+            dist.all_reduce(grad_features, group=self.group)
+            if mlp_grad is not None:
+                dist.all_reduce(mlp_grad, group=self.group)
+        self.last_loss = b.loss
+        self.last_sdf = b.sdf[:n]
+        return b.loss
+
+    def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None):
+        """torch.optim.Adam(betas=(0.9, 0.99), eps=adam_eps) step (utils/tools.py:111-112)."""
+        c = self.config
+        self._adam_t = (self._adam_t + 1) if step is None else step
+        st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
+        s = _lib.stream()
+        _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
+                  ctypes.byref(st), s)
+        if m_grad is not None:
+            off = 0
+            for p in mlp_params:
+                k = p.numel()
+                pd = p.data
+                if not (pd.is_contiguous() and pd.dtype == torch.float32):
+                    raise RuntimeError("decoder parameters must be contiguous float32")
+                _lib.call("pin_adam_step", _lib.ptr(pd), _lib.ptr(m_grad[off:off + k]), _lib.ptr(m_m[off:off + k]),
+                          _lib.ptr(m_v[off:off + k]), k, ctypes.byref(st), s)
+                off += k
+
+    def _sync_side_effects(self, cert_before):
+        nm = self.neural_points
+        delta = nm.local_point_certainties - cert_before
+        dist.all_reduce(delta, group=self.group)
+        nm.local_point_certainties.copy_(cert_before + delta)
+        dist.all_reduce(nm.local_point_ts_update, op=dist.ReduceOp.MAX, group=self.group)
+
+    # ---------------------------------------------------------------- autograd helpers
+    def sdf(self, x, get_std=False):
+        """utils/mapper.py:670-681 on the drop-in query_feature (training mode, autograd-capable)."""
+        geo_feature, _, weight_knn, _, _ = self.neural_points.query_feature(x)
+        sdf_pred = self.geo_mlp.sdf(geo_feature)
+        sdf_std = None
+        if not self.config.weighted_first:
+            sdf_pred_mean = torch.sum(sdf_pred * weight_knn, dim=1)
+            if get_std:
+                sdf_var = torch.sum((weight_knn * (sdf_pred - sdf_pred_mean.unsqueeze(-1)) ** 2), dim=1)
+                sdf_std = torch.sqrt(sdf_var).squeeze(1)
+            sdf_pred = sdf_pred_mean.squeeze(1)
+        return sdf_pred, sdf_std
+
+    def get_numerical_gradient(self, x, sdf_x=None, eps=0.02, two_side=True):
+        """utils/mapper.py:683-733."""
+        N = x.shape[0]
+        ex = torch.tensor([eps, 0.0, 0.0], dtype=x.dtype, device=x.device)
+        ey = torch.tensor([0.0, eps, 0.0], dtype=x.dtype, device=x.device)
+        ez = torch.tensor([0.0, 0.0, eps], dtype=x.dtype, device=x.device)
+        if two_side:
+            pts = torch.cat((x + ex, x - ex, x + ey, x - ey, x + ez, x - ez), dim=0)
+            s = self.sdf(pts)[0].unsqueeze(-1)
+            gx = (s[:N] - s[N:2 * N]) / (2 * eps)
+            gy = (s[2 * N:3 * N] - s[3 * N:4 * N]) / (2 * eps)
+            gz = (s[4 * N:5 * N] - s[5 * N:]) / (2 * eps)
+        else:
+            pts = torch.cat((x + ex, x + ey, x + ez), dim=0)
+            s = self.sdf(pts)[0].unsqueeze(-1)
+            sx = sdf_x.unsqueeze(-1)
+            gx = (s[:N] - sx) / eps
+            gy = (s[N:2 * N] - sx) / eps
+            gz = (s[2 * N:] - sx) / eps
+        return torch.cat([gx, gy, gz], dim=1)
+
+
+def adam_scalars(lr, step, eps, beta1=0.9, beta2=0.99, zero_grad=True) -> "_lib.PinAdamStep":
+    """Scalars torch.optim.Adam (single-tensor) derives per step, cast to float32 as its kernels do."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    return _lib.PinAdamStep(neg_step_size=float(np.float32(-(lr / bc1))), one_minus_beta1=float(np.float32(1 - beta1)),
+                            beta2=float(np.float32(beta2)), one_minus_beta2=float(np.float32(1 - beta2)),
+                            bias_correction2_sqrt=float(np.float32(bc2 ** 0.5)), eps=float(np.float32(eps)),
+                            zero_grad=int(zero_grad), reserved=0)

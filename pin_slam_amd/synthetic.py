@@ -53,3 +53,14 @@ def surface_queries(pts, n, seed=7, sigma=0.25, device="cuda"):
     idx = torch.randint(0, pts.shape[0], (n,), generator=g)
     q = pts[idx] + torch.randn(n, 3, generator=g) * sigma
     return q.to(device)
+
+
+def surface_pool(pts, n, seed=11, sigma=0.25, device="cuda"):
+    """Mapper training pool: map points offset along z by
+    N(0, sigma^2), label = -offset, frame ts 0.  Returns (coord [n,3], label [n], ts [n])."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    idx = torch.randint(0, pts.shape[0], (n,), generator=g)
+    off = torch.randn(n, generator=g) * sigma
+    coord = pts[idx].clone()
+    coord[:, 2] += off
+    return coord.to(device), (-off).to(device), torch.zeros(n, dtype=torch.int64, device=device)

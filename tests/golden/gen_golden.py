@@ -119,6 +119,53 @@ def build_map(cfg, n_side, seed):
     return npm, pts
 
 
+def room_surface(res, rng):
+    """Well-conditioned scene for the registration fixtures: floor, four walls and a box,
+    sampled at the voxel spacing, with inward-facing unit normals."""
+    a = np.arange(-6.0, 6.0, res) + res / 2
+    h = np.arange(0.0, 3.0, res) + res / 2
+    A, Hh = np.meshgrid(a, h, indexing="ij")
+    X, Y = np.meshgrid(a, a, indexing="ij")
+    parts = [(np.stack([X.ravel(), Y.ravel(), np.zeros(X.size)], 1), (0, 0, 1))]
+    for sgn in (-1.0, 1.0):
+        parts.append((np.stack([np.full(A.size, 6.0 * sgn), A.ravel(), Hh.ravel()], 1), (-sgn, 0, 0)))
+        parts.append((np.stack([A.ravel(), np.full(A.size, 6.0 * sgn), Hh.ravel()], 1), (0, -sgn, 0)))
+    b = np.arange(-1.0, 1.0, res) + res / 2
+    bh = np.arange(0.0, 1.5, res) + res / 2
+    B1, B2 = np.meshgrid(b, b, indexing="ij")
+    parts.append((np.stack([B1.ravel(), B2.ravel(), np.full(B1.size, 1.5)], 1), (0, 0, 1)))
+    Bb, Bz = np.meshgrid(b, bh, indexing="ij")
+    for sgn in (-1.0, 1.0):
+        parts.append((np.stack([np.full(Bb.size, sgn), Bb.ravel(), Bz.ravel()], 1), (sgn, 0, 0)))
+        parts.append((np.stack([Bb.ravel(), np.full(Bb.size, sgn), Bz.ravel()], 1), (0, sgn, 0)))
+    pts = np.concatenate([q for q, _ in parts]).astype(np.float32)
+    nrm = np.concatenate([np.tile(np.asarray(n, np.float32), (q.shape[0], 1)) for q, n in parts])
+    pts += rng.normal(0, res * 0.05, pts.shape).astype(np.float32)
+    return pts, nrm
+
+
+def build_room_map(cfg, seed):
+    """Room map through the reference's insert path; returns (npm, map points, their normals)."""
+    rng = np.random.default_rng(seed)
+    pts, nrm = room_surface(cfg.voxel_size_m, rng)
+    npm = NeuralPoints(cfg)
+    T = 10
+    npm.travel_dist = torch.arange(T, dtype=torch.float32) * 10.0
+    npm.update(torch.from_numpy(pts), torch.zeros(3), torch.eye(3), 0)
+    M = npm.count()
+    g = torch.Generator().manual_seed(seed)
+    npm.point_ts_create = torch.full((M,), 9, dtype=torch.int64)
+    npm.point_ts_update = npm.point_ts_create.clone()
+    npm.geo_features = torch.randn(M + 1, cfg.feature_dim, generator=g) * 0.05
+    npm.geo_features[-1] = 0.0
+    npm.point_certainties = torch.rand(M, generator=g) * 10.0
+    # normal of each kept map point = normal of its nearest input sample
+    P = npm.neural_points.numpy()
+    d = ((P[:, None, :] - pts[None, :, :]) ** 2).sum(-1)
+    kept_n = nrm[d.argmin(1)]
+    return npm, P, kept_n
+
+
 def random_quats(m, g):
     q = torch.randn(m, 4, generator=g)
     q = q / q.norm(dim=1, keepdim=True)
@@ -332,25 +379,22 @@ def gen_mapper_case(name, cfg_kwargs, n_side, n_batch, seed, iters=2):
     print(name, "L=", npm.local_count(), "loss", [rec[f"it{i}_loss"] for i in range(iters)])
 
 
-def gen_tracker_case(name, cfg_kwargs, n_side, n_src, seed):
+def gen_tracker_case(name, cfg_kwargs, n_src, seed, n_train=150):
     """One registration_step (utils/tracker.py:277-452) on a shifted scan."""
     cfg = make_config(**cfg_kwargs)
     cfg.local_map_radius = 1e4  # whole map local
-    npm, _ = build_map(cfg, n_side, seed)
-    npm.point_ts_create[:] = 9
-    npm.point_ts_update[:] = 9
+    npm, P, N = build_room_map(cfg, seed)
     npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
     dec = decoder(cfg)
-    # train the decoder+features a little so the SDF is meaningful near the surface
+    # train the decoder+features a little so the SDF is meaningful near the surface:
+    # samples along the surface normal, label = -offset (the convention of the mapper cases)
     fm = _FakeMapper(cfg, npm, dec)
     opt = setup_optimizer(cfg, list(npm.parameters()), list(dec.parameters()))
     rng = np.random.default_rng(seed + 5)
-    P = npm.local_neural_points.numpy()
-    for _ in range(60):
-        base = P[rng.integers(0, P.shape[0], 4096)]
+    for _ in range(n_train):
+        pick = rng.integers(0, P.shape[0], 4096)
         off = rng.normal(0, 0.25, 4096).astype(np.float32)
-        coord = base.copy()
-        coord[:, 2] += off
+        coord = (P[pick] + off[:, None] * N[pick]).astype(np.float32)
         ct = torch.from_numpy(coord)
         feat, _, wk, _, _ = npm.query_feature(ct)
         sdf = dec.sdf(feat)
@@ -379,14 +423,29 @@ def gen_tracker_case(name, cfg_kwargs, n_side, n_src, seed):
                                     cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
                                     cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, False)
     delta_T, _, _, _, valid_points, resid_cm, _ = res
-    # the whole registration loop (utils/tracker.py:39-174) from the identity guess
+    # the whole registration loop (utils/tracker.py:39-174) from the identity guess, with the
+    # per-iteration increments and residuals recorded
+    hist_dT, hist_res, hist_cnt = [], [], []
+    step = tracker.registration_step
+
+    def recording_step(*a, **kw):
+        out = step(*a, **kw)
+        hist_dT.append(out[0].numpy().copy())
+        hist_res.append(float(out[5]))
+        hist_cnt.append(int(out[4].shape[0]))
+        return out
+
+    tracker.registration_step = recording_step
     T_track, _, _, valid_track = tracker.tracking(pts, torch.eye(4, dtype=torch.float64), cur_ts=9)
+    tracker.registration_step = step
     rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
                num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
                source=src, sdf=sdf_pred.numpy(), grad=sdf_grad.numpy(), mask=mask.numpy(),
                certainty=certainty.numpy(), sdf_std=sdf_std.numpy(),
                delta_T=delta_T.numpy(), valid_count=np.int64(valid_points.shape[0]),
                tracking_T=T_track.numpy(), tracking_valid=np.bool_(valid_track),
+               tracking_delta_T=np.stack(hist_dT), tracking_resid_cm=np.asarray(hist_res),
+               tracking_valid_count=np.asarray(hist_cnt, dtype=np.int64),
                reg_iter_n=np.int64(cfg.reg_iter_n), reg_term_thre_deg=np.float64(cfg.reg_term_thre_deg),
                reg_term_thre_m=np.float64(cfg.reg_term_thre_m),
                resid_cm=np.float64(resid_cm),
@@ -446,7 +505,13 @@ def gen_neighborhoods():
     np.savez_compressed(os.path.join(OUT, "neighborhoods.npz"), **rec)
 
 
-def main():
+def main(only=None):
+    if only:   # regenerate selected cases only, e.g.  gen_golden.py tracker_wf tracker_nwf
+        cases = {"tracker_wf": lambda: gen_tracker_case("tracker_wf", dict(weighted_first=True), 3000, seed=6),
+                 "tracker_nwf": lambda: gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7)}
+        for name in only:
+            cases[name]()
+        return
     meta = {"torch": torch.__version__, "numpy": np.__version__, "generated": time.strftime("%Y-%m-%d")}
     gen_neighborhoods()
     gen_query_case("query_wf", dict(weighted_first=True), 120, 1600, seed=1)
@@ -454,8 +519,8 @@ def main():
     gen_query_case("query_kitti", dict(voxel=0.4, alpha=0.5, nn_k=6, weighted_first=False), 90, 1200, seed=3)
     gen_mapper_case("mapper_wf", dict(weighted_first=True), 100, 2000, seed=4)
     gen_mapper_case("mapper_nwf", dict(weighted_first=False), 100, 2000, seed=5)
-    gen_tracker_case("tracker_wf", dict(weighted_first=True), 100, 3000, seed=6)
-    gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 100, 3000, seed=7)
+    gen_tracker_case("tracker_wf", dict(weighted_first=True), 3000, seed=6)
+    gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7)
     gen_mesher_case("mesher_wf", dict(weighted_first=True), 60, seed=8)
     with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
         for k, v in meta.items():
@@ -463,4 +528,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

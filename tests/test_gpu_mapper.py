@@ -1,0 +1,165 @@
+"""Fused mapping iteration (pin_train_forward / pin_train_backward / pin_adam_step) against
+the reference's mapper fixtures (utils/mapper.py:443-575 run by tests/golden/gen_golden.py).
+
+Tolerances (fp32; the reference's CPU autograd and our float atomics sum in different
+orders): loss rel 1e-5, sdf abs 1e-5, feature grads rel 1e-4 / abs 1e-8, decoder grads
+rel 1e-3 / abs 1e-7, certainties rel 1e-5 / abs 1e-4, ts_update exact; Adam fed the
+reference's own gradients matches its post-step parameters to rel 1e-6 / abs 1e-7.
+"""
+import numpy as np
+import pytest
+import torch
+
+import pin_slam_amd as P
+from pin_slam_amd import _lib
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+BACKENDS = ["hash", "grid"]
+CASES = ["mapper_wf", "mapper_nwf"]
+MLP_KEYS = ["W1", "b1", "W2", "b2"]
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return "cuda"
+
+
+def _setup(z, dev, backend):
+    nm = H.neural_points_from_fixture(z, dev, backend=backend)
+    assert nm.backend() == backend
+    dec = H.decoder_from_fixture(z, nm.config)
+    dec.to(dev)
+    cfg = nm.config
+    assert abs(cfg.voxel_size_m * cfg.num_grad_step_ratio - float(z["num_grad_eps"])) < 1e-12
+    assert cfg.gradient_decimation == int(z["gradient_decimation"]) and cfg.weight_e == float(z["weight_e"])
+    assert cfg.lr == float(z["lr"]) and cfg.adam_eps == float(z["adam_eps"])
+    mapper = P.Mapper(cfg, None, nm, dec)
+    assert abs(mapper.sdf_scale - float(z["sigma"])) < 1e-12
+    np.testing.assert_array_equal(_np(nm.local_geo_features), z["local_features_before"])
+    np.testing.assert_array_equal(_np(nm.local_point_certainties), z["local_cert_before"])
+    return nm, dec, mapper
+
+
+def _split(flat):
+    out, off = {}, 0
+    for key, n in zip(MLP_KEYS, (64 * 11, 64, 64, 1)):
+        out[key] = flat[off:off + n]
+        off += n
+    return out
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_train_step_fixture(golden, dev, backend, case):
+    """Each iteration: loss, sdf, feature and decoder gradients and the side effects of the
+    fused forward/backward; then Adam on the reference's gradients (isolates the optimiser)."""
+    z = golden(case)
+    nm, dec, mapper = _setup(z, dev, backend)
+    feats = nm.local_geo_features.data
+    f_grad = torch.zeros_like(feats)
+    f_m, f_v = torch.zeros_like(feats), torch.zeros_like(feats)
+    m_grad = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+    m_m, m_v = torch.zeros_like(m_grad), torch.zeros_like(m_grad)
+    params = list(dec.parameters())
+    for it in range(int(z["iters"])):
+        coord = torch.as_tensor(z[f"it{it}_coord"], device=dev)
+        label = torch.as_tensor(z[f"it{it}_label"], device=dev)
+        ts = torch.as_tensor(z[f"it{it}_ts"], device=dev)
+        loss = mapper.train_step(coord, label, ts, f_grad, m_grad)
+        assert float(loss) == pytest.approx(float(z[f"it{it}_loss"]), rel=1e-5)
+        np.testing.assert_allclose(_np(mapper.last_sdf), z[f"it{it}_sdf"], atol=1e-5)
+        np.testing.assert_allclose(_np(f_grad), z[f"it{it}_feat_grad"], rtol=1e-4, atol=1e-8)
+        got = _split(_np(m_grad))
+        for key in MLP_KEYS:
+            want = z[f"it{it}_grad_{key}"].reshape(-1)
+            np.testing.assert_allclose(got[key], want, rtol=1e-3, atol=1e-7, err_msg=key)
+        np.testing.assert_allclose(_np(nm.local_point_certainties), z[f"it{it}_cert_after"], rtol=1e-5, atol=1e-4)
+        np.testing.assert_array_equal(_np(nm.local_point_ts_update), z[f"it{it}_ts_after"])
+        # Adam on the reference's own gradients; zero_grad clears our buffers for the next step
+        f_grad.copy_(torch.as_tensor(z[f"it{it}_feat_grad"], device=dev))
+        m_grad.copy_(torch.as_tensor(np.concatenate([z[f"it{it}_grad_{k}"].reshape(-1) for k in MLP_KEYS]),
+                                     device=dev))
+        mapper._adam(feats, f_grad, f_m, f_v, params, m_grad, m_m, m_v, step=it + 1)
+        assert float(f_grad.abs().max()) == 0.0 and float(m_grad.abs().max()) == 0.0
+        np.testing.assert_allclose(_np(feats), z[f"it{it}_features_after"], rtol=1e-6, atol=1e-7)
+        for key, p in zip(MLP_KEYS, params):
+            np.testing.assert_allclose(_np(p), z[f"it{it}_{key}_after"], rtol=1e-6, atol=1e-7, err_msg=key)
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_mapping_call_fixture(golden, dev, backend, case, monkeypatch):
+    """Mapper.mapping(iters) end to end on the fixture's batches: global features, certainty
+    and ts after assign_local_to_global.  Adam's first step moves every touched feature by
+    +-lr whatever the gradient's size, so elements whose reference gradient is within float
+    noise of 0 may legitimately take the other sign: at most 0.1% of elements may differ."""
+    z = golden(case)
+    nm, dec, mapper = _setup(z, dev, backend)
+    batches = iter(range(int(z["iters"])))
+
+    def get_batch(global_coord=False):
+        it = next(batches)
+        coord = torch.as_tensor(z[f"it{it}_coord"], device=dev)
+        label = torch.as_tensor(z[f"it{it}_label"], device=dev)
+        ts = torch.as_tensor(z[f"it{it}_ts"], device=dev)
+        return coord, label, ts, None, None, None, torch.ones_like(label)
+
+    monkeypatch.setattr(mapper, "get_batch", get_batch)
+    mapper.mapping(int(z["iters"]))
+    got = _np(nm.geo_features)
+    want = z["global_features_after"]
+    off = ~np.isclose(got, want, rtol=1e-5, atol=1e-6)
+    assert off.mean() <= 1e-3, f"{off.sum()} of {off.size} feature elements off"
+    np.testing.assert_allclose(_np(nm.point_certainties), z["global_cert_after"], rtol=1e-5, atol=1e-4)
+    np.testing.assert_array_equal(_np(nm.point_ts_update), z["global_ts_update_after"])
+    for key, p in zip(MLP_KEYS, dec.parameters()):
+        np.testing.assert_allclose(_np(p), z[f"it{int(z['iters']) - 1}_{key}_after"], rtol=1e-4, atol=1e-5,
+                                   err_msg=key)
+
+
+def test_frozen_decoder_trains_features_only(golden, dev):
+    """Decoder frozen (freeze_model, utils/tools.py:186-191, after freeze_after_frame): the
+    decoder parameters stay bit-identical and the features still move."""
+    z = golden("mapper_wf")
+    nm, dec, mapper = _setup(z, dev, "grid")
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    before = [p.detach().clone() for p in dec.parameters()]
+    f0 = nm.local_geo_features.detach().clone()
+    coord = torch.as_tensor(z["it0_coord"], device=dev)
+    label = torch.as_tensor(z["it0_label"], device=dev)
+    ts = torch.as_tensor(z["it0_ts"], device=dev)
+    mapper.get_batch = lambda global_coord=False: (coord, label, ts, None, None, None, torch.ones_like(label))
+    mapper.mapping(1)
+    for b, p in zip(before, dec.parameters()):
+        assert torch.equal(b, p.detach())
+    moved = (nm.geo_features[nm.local_mask] != f0).any(-1)
+    assert int(moved.sum()) > 100
+
+
+def test_adam_matches_torch(dev):
+    """pin_adam_step against torch.optim.Adam on the same device, three steps."""
+    g = torch.Generator(device="cpu").manual_seed(0)
+    p0 = torch.randn(10007, generator=g)
+    grads = [torch.randn(10007, generator=g) * 10 ** (-k) for k in range(3)]
+    ref = torch.nn.Parameter(p0.clone().to(dev))
+    opt = torch.optim.Adam([ref], lr=0.01, betas=(0.9, 0.99), eps=1e-15, foreach=False)
+    mine = p0.clone().to(dev)
+    m, v = torch.zeros_like(mine), torch.zeros_like(mine)
+    from pin_slam_amd.mapper import adam_scalars
+    import ctypes
+    for t, gr in enumerate(grads, 1):
+        ref.grad = gr.to(dev)
+        opt.step()
+        gbuf = gr.to(dev).contiguous()
+        _lib.call("pin_adam_step", _lib.ptr(mine), _lib.ptr(gbuf), _lib.ptr(m), _lib.ptr(v), mine.numel(),
+                  ctypes.byref(adam_scalars(0.01, t, 1e-15)), _lib.stream())
+        np.testing.assert_allclose(_np(mine), _np(ref), rtol=1e-6, atol=1e-7)

@@ -259,7 +259,11 @@ def test_registration_step_fixture(golden, dev, backend, case):
 @pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
 def test_tracking_loop_fixture(golden, dev, case):
     """The whole Tracker.tracking loop (utils/tracker.py:39-174: iterations, convergence,
-    validity checks, fall-back) from the identity guess vs the reference's own run."""
+    validity checks, fall-back) from the identity guess vs the reference's own run on a
+    well-conditioned room scene: same number of iterations, per-iteration increments within
+    5e-5 (f32 reductions in a different order feed the next iteration), residuals within
+    1e-3 relative, valid-point counts within 3 (points at the gradient-norm thresholds), the
+    final pose within 1e-4 and the same validity verdict."""
     from pin_slam_amd.tracker import Tracker
     z = golden(case)
     nm = H.neural_points_from_fixture(z, dev)
@@ -270,7 +274,21 @@ def test_tracking_loop_fixture(golden, dev, case):
     cfg.max_sdf_std_ratio = float(z["max_sdf_std_ratio"])
     cfg.reg_iter_n = int(z["reg_iter_n"])
     tr = Tracker(cfg, nm, dec)
+    hist = []
+    step = tr.registration_step
+
+    def recording_step(*a, **kw):
+        out = step(*a, **kw)
+        hist.append((_np(out[0]), float(out[5]), int(out[4].shape[0])))
+        return out
+
+    tr.registration_step = recording_step
     src = torch.as_tensor(z["source"], device=dev)
     T, cov, _, valid = tr.tracking(src, torch.eye(4, dtype=torch.float64, device=dev), cur_ts=9)
+    assert len(hist) == z["tracking_delta_T"].shape[0]
+    for i, (dT, res, cnt) in enumerate(hist):
+        np.testing.assert_allclose(dT, z["tracking_delta_T"][i], atol=5e-5, err_msg=f"iteration {i}")
+        assert res == pytest.approx(float(z["tracking_resid_cm"][i]), rel=1e-3)
+        assert abs(cnt - int(z["tracking_valid_count"][i])) <= 3
     assert bool(valid) == bool(z["tracking_valid"])
-    np.testing.assert_allclose(_np(T), z["tracking_T"], atol=2e-5)
+    np.testing.assert_allclose(_np(T), z["tracking_T"], atol=1e-4)
