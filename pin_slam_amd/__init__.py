@@ -6,14 +6,16 @@ Drop-in classes mirror the reference's Python API:
     pin_slam_amd.Decoder        <- model/decoder.py:Decoder
     pin_slam_amd.Mapper         <- utils/mapper.py:Mapper (training path)
     pin_slam_amd.Tracker        <- utils/tracker.py:Tracker (registration path)
+    pin_slam_amd.Mesher         <- utils/mesher.py:Mesher.query_points
 The compute runs in hand-written HIP kernels for gfx950 (libpin_slam_amd.so,
 C ABI in include/pin_slam_amd.h).
 """
 from .config import Config
 from .decoder import Decoder
 from .mapper import Mapper
+from .mesher import Mesher
 from .neural_points import NeuralPoints
 from .query import query_sdf
 from .tracker import Tracker
 
-__all__ = ["Config", "Decoder", "Mapper", "NeuralPoints", "Tracker", "query_sdf"]
+__all__ = ["Config", "Decoder", "Mapper", "Mesher", "NeuralPoints", "Tracker", "query_sdf"]

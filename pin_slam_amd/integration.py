@@ -1,0 +1,54 @@
+"""Route an unmodified PIN-SLAM checkout's hot path through pin_slam_amd.
+
+    import pin_slam_amd.integration
+    pin_slam_amd.integration.install()      # first lines of pin_slam.py / pin_slam_ros.py / vis_pin_map.py
+
+``install()`` imports the reference modules (so it must run where they import) and
+
+* replaces ``model.neural_points.NeuralPoints`` and ``model.decoder.Decoder`` by the drop-in
+  classes, so every later ``from model.neural_points import NeuralPoints`` binds ours;
+* transplants the hot-path methods onto the reference's ``utils.mapper.Mapper``,
+  ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, keeping everything else
+  of those classes (data sampling, bundle adjustment, marching cubes, ...) as it is.
+
+It returns the list of (module, attribute) pairs it patched.  Nothing in the package calls it.
+"""
+import importlib
+
+from .decoder import Decoder
+from .mapper import Mapper
+from .mesher import Mesher
+from .neural_points import NeuralPoints
+from .tracker import Tracker
+
+MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "_sync_side_effects", "sdf",
+                  "get_numerical_gradient")
+TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
+MESHER_METHODS = ("query_points",)
+
+
+def install(neural_points=True, decoder=True, mapper=True, tracker=True, mesher=True):
+    patched = []
+
+    def setcls(modname, name, obj):
+        mod = importlib.import_module(modname)
+        setattr(mod, name, obj)
+        patched.append((modname, name))
+
+    def methods(modname, clsname, src, names):
+        cls = getattr(importlib.import_module(modname), clsname)
+        for n in names:
+            setattr(cls, n, src.__dict__[n])
+            patched.append((modname, f"{clsname}.{n}"))
+
+    if neural_points:
+        setcls("model.neural_points", "NeuralPoints", NeuralPoints)
+    if decoder:
+        setcls("model.decoder", "Decoder", Decoder)
+    if mapper:
+        methods("utils.mapper", "Mapper", Mapper, MAPPER_METHODS)
+    if tracker:
+        methods("utils.tracker", "Tracker", Tracker, TRACKER_METHODS)
+    if mesher:
+        methods("utils.mesher", "Mesher", Mesher, MESHER_METHODS)
+    return patched

@@ -156,9 +156,10 @@ class Mapper:
             raise NotImplementedError("fused mapping implements the unweighted BCE (loss_weight_on False)")
 
     def _world(self):
-        if self.group is False or not dist.is_available() or not dist.is_initialized():
+        group = getattr(self, "group", None)
+        if group is False or not dist.is_available() or not dist.is_initialized():
             return 1
-        return dist.get_world_size(self.group)
+        return dist.get_world_size(group)
 
     def mapping(self, iter_count):
         """utils/mapper.py:425-593 (iteration body :443-575)."""
@@ -214,6 +215,8 @@ class Mapper:
         nn_k = int(c.query_nn_k)
         wf = bool(c.weighted_first)
         rows = n + 6 * nd
+        if not hasattr(self, "_buf"):    # methods transplanted onto the reference class
+            self._buf = _TrainBuffers()
         b = self._buf.get(rows, nn_k, wf, q.device)
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
@@ -237,9 +240,7 @@ class Mapper:
         _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
                   _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
         if world > 1:
-            dist.all_reduce(grad_features, group=self.group)
-            if mlp_grad is not None:
-                dist.all_reduce(mlp_grad, group=self.group)
+            allreduce_gradients([grad_features, mlp_grad], getattr(self, "group", None))
         self.last_loss = b.loss
         self.last_sdf = b.sdf[:n]
         return b.loss
@@ -247,7 +248,7 @@ class Mapper:
     def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None):
         """torch.optim.Adam(betas=(0.9, 0.99), eps=adam_eps) step (utils/tools.py:111-112)."""
         c = self.config
-        self._adam_t = (self._adam_t + 1) if step is None else step
+        self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
         _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
@@ -265,10 +266,8 @@ class Mapper:
 
     def _sync_side_effects(self, cert_before):
         nm = self.neural_points
-        delta = nm.local_point_certainties - cert_before
-        dist.all_reduce(delta, group=self.group)
-        nm.local_point_certainties.copy_(cert_before + delta)
-        dist.all_reduce(nm.local_point_ts_update, op=dist.ReduceOp.MAX, group=self.group)
+        sync_side_effects(nm.local_point_certainties, cert_before, nm.local_point_ts_update,
+                          getattr(self, "group", None))
 
     # ---------------------------------------------------------------- autograd helpers
     def sdf(self, x, get_std=False):
@@ -304,6 +303,23 @@ class Mapper:
             gy = (s[N:2 * N] - sx) / eps
             gz = (s[2 * N:] - sx) / eps
         return torch.cat([gx, gy, gz], dim=1)
+
+
+def allreduce_gradients(grads, group=None):
+    """SUM all-reduce of the per-rank gradients (already scaled by 1/world in the backward, so
+    the sum is the gradient of the mean loss over the union of the ranks' batches)."""
+    for g in grads:
+        if g is not None:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+
+
+def sync_side_effects(cert, cert_before, ts_update, group=None):
+    """Training-mode side effects of a data-parallel mapping() call: certainty deltas add up
+    across ranks (scatter_add_, neural_points.py:640), ts_update takes the max (:644)."""
+    delta = cert - cert_before
+    dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=group)
+    cert.copy_(cert_before + delta)
+    dist.all_reduce(ts_update, op=dist.ReduceOp.MAX, group=group)
 
 
 def adam_scalars(lr, step, eps, beta1=0.9, beta2=0.99, zero_grad=True) -> "_lib.PinAdamStep":

@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 
 from oracle import pin_oracle as O
@@ -26,12 +27,38 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_lib.exported_symbols()) == decl, "ctypes signature table out of sync with the header"
 
 
-def test_struct_layouts_match_header():
+STRUCTS = ["PinHash", "PinPoints", "PinGridDims", "PinGrid", "PinMlp", "PinRegParams", "PinTrainCfg",
+           "PinTrainState", "PinAdamStep"]
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """sizeof / offsetof of every ABI struct, compiled from include/pin_slam_amd.h with gcc,
+    against the ctypes mirrors in pin_slam_amd/_lib.py."""
+    import shutil
+    import subprocess
     from pin_slam_amd import _lib
-    # field order/size as declared in include/pin_slam_amd.h (x86-64 SysV layout)
-    assert ctypes.sizeof(_lib.PinHash) == 8 + 8 + 4 + 4 + 8 + 4 + 4
-    assert ctypes.sizeof(_lib.PinPoints) == 8 * 7 + 4 + 4
-    assert ctypes.sizeof(_lib.PinMlp) == 8 * 4 + 4 + 4
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pin_slam_amd.h"', "int main(void) {"]
+    for name in STRUCTS:
+        lines.append(f'printf("{name} sizeof %zu\\n", sizeof({name}));')
+        for field, _ in getattr(_lib, name)._fields_:
+            lines.append(f'printf("{name} {field} %zu\\n", offsetof({name}, {field}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {(a, b): int(c) for a, b, c in (line.split() for line in out if line)}
+    for name in STRUCTS:
+        cls = getattr(_lib, name)
+        assert got[(name, "sizeof")] == ctypes.sizeof(cls), name
+        for field, _ in cls._fields_:
+            assert got[(name, field)] == getattr(cls, field).offset, (name, field)
+    # every struct the header declares is mirrored
+    hdr = open(os.path.join(ROOT, "include", "pin_slam_amd.h")).read()
+    assert sorted(re.findall(r"^} (Pin\w+);", hdr, re.M)) == sorted(STRUCTS)
 
 
 def test_neighbor_offsets_host(golden):

@@ -145,6 +145,31 @@ def test_mesher_fixture(golden, dev, backend):
     np.testing.assert_allclose(_np(sdf), z["sdf"], rtol=0, atol=SDF_ATOL)
 
 
+@pytest.mark.parametrize("host", [True, False])
+@pytest.mark.parametrize("out_torch", [False, True])
+def test_mesher_query_points_dropin(golden, dev, host, out_torch):
+    """Mesher.query_points (utils/mesher.py:41-136): batched, host or device coordinates,
+    reference output types (float64 numpy / CPU float32 tensors, mask as 0/1)."""
+    z = golden("mesher_wf")
+    nm = H.neural_points_from_fixture(z, dev)
+    dec = H.decoder_from_fixture(z, nm.config)
+    import pin_slam_amd as P
+    mesher = P.Mesher(nm.config, nm, dec)
+    coord = torch.as_tensor(z["coord"])
+    if not host:
+        coord = coord.to(dev)
+    sdf, sem, color, mask = mesher.query_points(coord, 7777, True, False, False, True, query_locally=False,
+                                                mask_min_nn_count=int(z["mesh_min_nn"]), out_torch=out_torch)
+    assert sem is None and color is None
+    if out_torch:
+        assert sdf.dtype == torch.float32 and mask.dtype == torch.float32 and not sdf.is_cuda
+        sdf, mask = sdf.numpy(), mask.numpy()
+    else:
+        assert sdf.dtype == np.float64 and mask.dtype == np.float64
+    np.testing.assert_array_equal(mask, z["mc_mask"].astype(np.float64))
+    np.testing.assert_allclose(sdf, z["sdf"], rtol=0, atol=SDF_ATOL)
+
+
 @pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_tracker_fixture_queries(golden, dev, backend, case):

@@ -1,0 +1,51 @@
+"""pin_slam_amd.integration.install() against stand-in reference modules (CPU): the class
+swap and the method transplant land where pin_slam.py / utils/*.py look them up."""
+import sys
+import types
+
+import pin_slam_amd as P
+from pin_slam_amd import integration
+
+
+def _fake(name, **attrs):
+    m = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    return m
+
+
+def test_install_patches_reference_modules(monkeypatch):
+    class RefMapper:
+        def process_frame(self):
+            return "kept"
+
+        def mapping(self, n):
+            return "reference"
+
+    class RefTracker:
+        def tracking(self):
+            return "reference"
+
+    class RefMesher:
+        def query_points(self):
+            return "reference"
+
+        def mc_mesh(self):
+            return "kept"
+
+    mods = {"model": _fake("model"), "model.neural_points": _fake("model.neural_points", NeuralPoints=object),
+            "model.decoder": _fake("model.decoder", Decoder=object), "utils": _fake("utils"),
+            "utils.mapper": _fake("utils.mapper", Mapper=RefMapper),
+            "utils.tracker": _fake("utils.tracker", Tracker=RefTracker),
+            "utils.mesher": _fake("utils.mesher", Mesher=RefMesher)}
+    for k, v in mods.items():
+        monkeypatch.setitem(sys.modules, k, v)
+    patched = integration.install()
+    from model.neural_points import NeuralPoints
+    from model.decoder import Decoder
+    assert NeuralPoints is P.NeuralPoints and Decoder is P.Decoder
+    assert RefMapper.mapping is P.Mapper.mapping and RefMapper.train_step is P.Mapper.train_step
+    assert RefMapper().process_frame() == "kept"
+    assert RefTracker.tracking is P.Tracker.tracking and RefTracker.registration_step is P.Tracker.registration_step
+    assert RefMesher.query_points is P.Mesher.query_points and RefMesher().mc_mesh() == "kept"
+    assert ("utils.mapper", "Mapper.mapping") in patched
