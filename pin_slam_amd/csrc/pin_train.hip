@@ -303,12 +303,20 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     }
 }
 
-__global__ void __launch_bounds__(64) k_loss_final(const double* __restrict__ part, int64_t n,
-                                                   double* __restrict__ out) {
+// sum of the per-wave loss partials, fixed order (1024 threads, strided, then a tree)
+__global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ part, int64_t n,
+                                                     double* __restrict__ out) {
+    __shared__ double red[16];
     double v = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += 64) v += part[i];
+    for (int64_t i = threadIdx.x; i < n; i += 1024) v += part[i];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (threadIdx.x == 0) out[0] = v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < 16; ++w) t += red[w];
+        out[0] = t;
+    }
 }
 
 // mlp_grad[e] += sum_b part[b][e], fixed order
@@ -393,7 +401,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         if (mlp_grad) PIN_LAUNCH_BWD(false, true); else PIN_LAUNCH_BWD(false, false);
     }
 #undef PIN_LAUNCH_BWD
-    if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, s, lpart, nblk * kWaves, loss_out);
+    if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
     if (mlp_grad)
         hipLaunchKernelGGL(k_mlp_grad_final, dim3((kMlpGrad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, mpart, nblk,
                            mlp_grad);
