@@ -64,18 +64,23 @@ typedef struct PinGridDims {
     int32_t reserved;
 } PinGridDims;
 
-/* Occupancy grid + compact 64-byte records (see pin_grid_mark / pin_grid_fill). */
+/* Occupancy grid + compact per-cell arrays in brick order (see pin_grid_mark / pin_grid_fill). */
 typedef struct PinGrid {
     const uint32_t* bricks;      /* [nb,4]: bits lo, bits hi, exclusive prefix, 0 */
     PinGridDims dims;
-    const float* crec;           /* [n_occ,16]: {x,y,z,bits(id)} {f0..f3} {f4..f7} {certainty,0,0,0} */
+    const float* crec;           /* [n_occ,4]: x, y, z, bits(id) of the cell's point (its record) */
     const int32_t* cgid;         /* [n_occ] global point index of each compact record */
     int64_t n_occ;
     const int32_t* offsets;      /* [pin_cells_padded(Kc)] packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 */
     float resolution;
     int32_t num_cells;           /* Kc, reference cell order (model/neural_points.py:430-439) */
     float max_valid_dist2;
-    int32_t fat;                 /* 1: features/certainty read from crec; 0: from PinPoints */
+    const float* cfeat;          /* [n_occ,8] features in brick order (fat), else NULL */
+    const float* ccert;          /* [n_occ] certainties in brick order (fat), else NULL */
+    int32_t fat;                 /* 1: features/certainty read from cfeat/ccert; 0: from PinPoints by id */
+    int32_t window;              /* max |offset| component (num_nei_cells); <= 2 enables the
+                                    brick-window scan (<= 8 bricks cover the neighbourhood) */
+    int32_t reserved;
 } PinGrid;
 
 /* Geo decoder, hidden_level = 1 (model/decoder.py:16-88). */
@@ -201,6 +206,13 @@ int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, 
                       const float* sdf_std, const float* sdf_label, const float* weight, int64_t n,
                       const PinRegParams* prm, double* workspace, double* out, uint8_t* valid_out, void* stream);
 
+/*
+ * pin_cell_bounds -- out[0..2] = min, out[3..5] = max over the points of floor(p / resolution)
+ * (f32 division, the reference's voxel rule, neural_points.py:214); the occupancy-grid box.
+ * Empty input leaves out = {INT64_MAX x3, INT64_MIN x3}.
+ */
+int pin_cell_bounds(const float* positions, int64_t num_points, float resolution, int64_t* out, void* stream);
+
 /* Workspace bytes pin_grid_mark needs for a grid of nb bricks. */
 static inline int64_t pin_grid_workspace_bytes(int64_t num_bricks) {
     return ((num_bricks + 4095) / 4096) * 4 + 16;
@@ -220,17 +232,33 @@ int pin_grid_mark(const float* positions, int64_t num_points, float resolution, 
                   void* workspace, void* stream);
 
 /*
- * pin_grid_fill -- compact records in brick order for one query mode: crec[rank(cell_g)] =
- * {record_g, features[id_g], certainty[id_g]} and cgid[rank] = g, for every own-cell point.
+ * pin_grid_fill -- compact arrays in brick order for one query mode, for every own-cell point g
+ * at rank r = rank(cell_g): crec[r] = record_g, cgid[r] = g and, when cfeat / ccert are
+ * non-NULL, cfeat[r] = features[id_g], ccert[r] = certainty[id_g] (zeros for rejected records).
  */
 int pin_grid_fill(const float* positions, int64_t num_points, float resolution, const int32_t* table,
                   int64_t buffer_size, const PinGridDims* dims, const uint32_t* bricks, const float* records,
-                  const float* features, const float* certainties, float* crec, int32_t* cgid, void* stream);
+                  const float* features, const float* certainties, float* crec, float* cfeat, float* ccert,
+                  int32_t* cgid, void* stream);
 
-/* pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid. */
+/* Query bins of a grid box: 8x8x8 cells (2x2x2 bricks) each. */
+static inline int64_t pin_query_bins(const PinGridDims* d) {
+    return (int64_t)((d->nbx + 1) / 2) * ((d->nby + 1) / 2) * ((d->nbz + 1) / 2);
+}
+/* Workspace bytes of pin_query_sdf_grid's binned form for n queries. */
+static inline int64_t pin_query_workspace_bytes(int64_t n, const PinGridDims* d) {
+    return 4 * (pin_query_bins(d) + 2 * n);
+}
+
+/*
+ * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  workspace NULL:
+ * queries are processed in input order.  Otherwise (pin_query_workspace_bytes(n, &grid->dims)
+ * bytes) they are first counting-sorted into 8x8x8-cell bins and processed bin by bin (better
+ * line sharing for random batches); outputs are identical and stay at each query's index.
+ */
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
                        int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
-                       int32_t* nn_count, float* certainty, float* sdf_std, void* stream);
+                       int32_t* nn_count, float* certainty, float* sdf_std, void* workspace, void* stream);
 
 /* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
  * (features always read live from pts->features; gids from grid->cgid). */

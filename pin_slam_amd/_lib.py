@@ -43,7 +43,7 @@ class PinGridDims(ctypes.Structure):
 class PinGrid(ctypes.Structure):
     _fields_ = [("bricks", c_void_p), ("dims", PinGridDims), ("crec", c_void_p), ("cgid", c_void_p), ("n_occ", i64),
                 ("offsets", c_void_p), ("resolution", f32), ("num_cells", i32), ("max_valid_dist2", f32),
-                ("fat", i32)]
+                ("cfeat", c_void_p), ("ccert", c_void_p), ("fat", i32), ("window", i32), ("reserved", i32)]
 
 
 class PinRegParams(ctypes.Structure):
@@ -95,11 +95,12 @@ _SIGS = {
     "pin_query_certainty": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p],
     "pin_reg_normal_eq": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64,
                           _P(PinRegParams), c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_cell_bounds": [c_void_p, i64, f32, c_void_p, c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_fill": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p,
-                      c_void_p, c_void_p, c_void_p],
+                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_void_p],
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),

@@ -22,6 +22,15 @@ constexpr int64_t kP0 = 73856093LL, kP1 = 19349669LL, kP2 = 83492791LL;  // neur
 constexpr float kInvalidDist2 = 9e3f;    // neural_points.py:561
 constexpr float kIdwEps = 1e-15f;        // neural_points.py:618
 
+// XCD-aware block order: the hardware places block b on XCD (b mod 8); this bijection hands
+// each XCD one contiguous eighth of the logical blocks, so spatially ordered inputs keep their
+// neighbourhoods within one XCD's L2.
+__device__ __forceinline__ int64_t xcd_block() {
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // floor_mod(floor(q/res) . primes, B): the reference's fmod + negative-index wrap
 // (neural_points.py:465-476).  Division is IEEE f32 (no reciprocal), as on the CPU path.
 __device__ __forceinline__ uint32_t base_slot(float qx, float qy, float qz, float res, int64_t B) {
@@ -132,26 +141,118 @@ struct HashSource {
 // The occupancy grid (pin_grid.hip): cell -> brick bit -> rank -> 64-byte compact record.
 // Payload = compact record index.  FAT: features / certainty come from the compact record
 // (one line per candidate); otherwise from the live PinPoints arrays.
+// one of 8 registers by a per-lane 3-bit index, as a select tree (no scratch)
+__device__ __forceinline__ uint32_t sel8(const uint32_t (&w)[8], int k) {
+    const uint32_t a0 = (k & 1) ? w[1] : w[0], a1 = (k & 1) ? w[3] : w[2];
+    const uint32_t a2 = (k & 1) ? w[5] : w[4], a3 = (k & 1) ? w[7] : w[6];
+    const uint32_t b0 = (k & 2) ? a1 : a0, b1 = (k & 2) ? a3 : a2;
+    return (k & 4) ? b1 : b0;
+}
+
 template <bool FAT>
 struct GridSource {
     static constexpr int kChunk = 8;
+    static constexpr int kSeg = 32;   // offsets per list segment: 32 KB of LDS per block
     const PinGrid& gr;
     const PinPoints& p;
     __device__ GridSource(const PinGrid& g_, const PinPoints& p_) : gr(g_), p(p_) {}
 
+    // query cell relative to the box, clamped so that every offset stays representable in
+    // int32 and a far-away query still lands outside the box for every offset
+    __device__ __forceinline__ static int rel(float v, float r, int64_t o, int e) {
+        const int64_t l = (int64_t)floorf(v / r) - o;
+        return (int)(l < -256 ? -256 : (l > (int64_t)e + 256 ? (int64_t)e + 256 : l));
+    }
+
     template <int CH>
     __device__ __forceinline__ int scan(float qx, float qy, float qz, TopK& tk) const {
+        if (gr.window <= 2) return scan_window<CH>(qx, qy, qz, tk);
+        return scan_cells<CH>(qx, qy, qz, tk);
+    }
+
+    // Brick-window scan (window <= 2): the 5x5x5-cell neighbourhood lies in <= 2 bricks per
+    // axis, so the <= 8 bricks are loaded in ONE round trip; the occupied offsets (reference
+    // cell order) are then found with register selects and their compact-record indices listed
+    // in LDS (one column per lane: conflict-free, no barrier); records are fetched for listed
+    // cells only, CH per round trip.
+    template <int CH>
+    __device__ __forceinline__ int scan_window(float qx, float qy, float qz, TopK& tk) const {
+        __shared__ int s_list[kSeg][kBlock];
+        const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
+        const float4* __restrict__ crec = (const float4*)gr.crec;
+        const int32_t* __restrict__ offs = gr.offsets;
+        const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
+        const int nbx = gr.dims.nbx, nby = gr.dims.nby, nbz = gr.dims.nbz;
+        const int lx = rel(qx, res, gr.dims.ox, 4 * nbx);
+        const int ly = rel(qy, res, gr.dims.oy, 4 * nby);
+        const int lz = rel(qz, res, gr.dims.oz, 4 * nbz);
+        const int bx0 = (lx - 2) >> 2, by0 = (ly - 2) >> 2, bz0 = (lz - 2) >> 2;
+        uint32_t wl[8], wh[8], wp[8];
+        {
+            uint4 w[8];
+            bool in[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int bx = bx0 + (k & 1), by = by0 + ((k >> 1) & 1), bz = bz0 + (k >> 2);
+                in[k] = (unsigned)bx < (unsigned)nbx && (unsigned)by < (unsigned)nby && (unsigned)bz < (unsigned)nbz;
+                w[k] = bricks[in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                wl[k] = in[k] ? w[k].x : 0u;
+                wh[k] = in[k] ? w[k].y : 0u;
+                wp[k] = w[k].z;
+            }
+        }
+        const int tid = threadIdx.x;
+        const int Kc = gr.num_cells;
+        int nn = 0;
+        for (int s0 = 0; s0 < Kc; s0 += kSeg) {
+            const int s1 = Kc < s0 + kSeg ? Kc : s0 + kSeg;
+            int cnt = 0;
+            for (int t = s0; t < s1; ++t) {
+                const int of = offs[t];
+                const int cx = lx + ((of & 255) - 128);
+                const int cy = ly + (((of >> 8) & 255) - 128);
+                const int cz = lz + (((of >> 16) & 255) - 128);
+                const int k = ((cx >> 2) - bx0) | (((cy >> 2) - by0) << 1) | (((cz >> 2) - bz0) << 2);
+                const uint64_t bits = ((uint64_t)sel8(wh, k) << 32) | sel8(wl, k);
+                const int bit = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
+                if ((bits >> bit) & 1ull) {
+                    s_list[cnt][tid] = (int)(sel8(wp, k) + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
+                    ++cnt;
+                }
+            }
+            // trip count = the longest list among the ACTIVE lanes (__any ignores lanes that
+            // returned early in a partial last wave)
+            for (int j0 = 0; __any(j0 < cnt); j0 += CH) {
+                int ci[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) ci[u] = (j0 + u < cnt) ? s_list[j0 + u][tid] : -1;
+                float4 r[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int id = __float_as_int(r[u].w);
+                    const float d2 = dist2(r[u].x, r[u].y, r[u].z, qx, qy, qz);
+                    const bool ok = ci[u] >= 0 && id != -1 && d2 <= maxd2;
+                    nn += ok ? 1 : 0;
+                    tk.insert(ok ? d2 : INFINITY, ci[u]);
+                }
+            }
+        }
+        return nn;
+    }
+
+    // Per-cell scan (any window): CH cell lookups back to back, then CH record gathers.
+    template <int CH>
+    __device__ __forceinline__ int scan_cells(float qx, float qy, float qz, TopK& tk) const {
         const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
         const float4* __restrict__ crec = (const float4*)gr.crec;
         const int32_t* __restrict__ offs = gr.offsets;  // padded to a multiple of 16 entries
         const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
         const int ex = 4 * gr.dims.nbx, ey = 4 * gr.dims.nby, ez = 4 * gr.dims.nbz;
-        // query cell relative to the box, clamped so that every offset stays representable in
-        // int32 and a far-away query still lands outside the box for every offset
-        auto rel = [](float v, float r, int64_t o, int e) -> int {
-            const int64_t l = (int64_t)floorf(v / r) - o;
-            return (int)(l < -256 ? -256 : (l > (int64_t)e + 256 ? (int64_t)e + 256 : l));
-        };
         const int lx = rel(qx, res, gr.dims.ox, ex);
         const int ly = rel(qy, res, gr.dims.oy, ey);
         const int lz = rel(qz, res, gr.dims.oz, ez);
@@ -184,7 +285,7 @@ struct GridSource {
             }
             float4 r[CH];
 #pragma unroll
-            for (int t = 0; t < CH; ++t) r[t] = crec[4 * (ci[t] > 0 ? ci[t] : 0)];
+            for (int t = 0; t < CH; ++t) r[t] = crec[ci[t] > 0 ? ci[t] : 0];
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int id = __float_as_int(r[t].w);
@@ -197,13 +298,13 @@ struct GridSource {
         return nn;
     }
     __device__ __forceinline__ float4 record(int pay) const {
-        return ((const float4*)gr.crec)[4 * (int64_t)(pay > 0 ? pay : 0)];
+        return ((const float4*)gr.crec)[pay > 0 ? pay : 0];
     }
     __device__ __forceinline__ void features(int pay, int64_t id, float4& f0, float4& f1) const {
         if (FAT) {
-            const float4* r = (const float4*)gr.crec + 4 * (int64_t)(pay > 0 ? pay : 0);
-            f0 = r[1];
-            f1 = r[2];
+            const float4* r = (const float4*)gr.cfeat + 2 * (int64_t)(pay > 0 ? pay : 0);
+            f0 = r[0];
+            f1 = r[1];
         } else {
             const float4* __restrict__ feat = (const float4*)p.features;
             f0 = feat[2 * id];
@@ -211,7 +312,7 @@ struct GridSource {
         }
     }
     __device__ __forceinline__ float certainty(int pay, int64_t id) const {
-        if (FAT) return ((const float4*)gr.crec)[4 * (int64_t)(pay > 0 ? pay : 0) + 3].x;
+        if (FAT) return gr.ccert[pay > 0 ? pay : 0];
         return p.certainties[id];
     }
     __device__ __forceinline__ int gid(int pay) const { return pay >= 0 ? gr.cgid[pay] : -1; }
@@ -345,25 +446,67 @@ __device__ __forceinline__ float gather_certainty(const Src& src, const Neighbou
     return cert;
 }
 
-// Decoder forward fused with its input gradient (model/decoder.py:66-88):
-//   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
-// One pass over the hidden units; weights are wave-uniform (scalar loads).
+// Decoder weights staged in LDS once per block (stage_mlp): W1 rows padded to 12 floats
+// (three 16-B broadcast reads per row), then b1, W2, b2.  Broadcast LDS reads return in order,
+// so the compiler keeps several in flight; the scalar-load form paid a dependent K$ round trip
+// per hidden-unit pair.
+constexpr int kWRow = 12;
+constexpr int kWB1 = kH * kWRow;
+constexpr int kWW2 = kWB1 + kH;
+constexpr int kWB2 = kWW2 + kH;
+constexpr int kWSize = kWB2 + 4;
+
+struct MlpW {
+    const float* w;   // LDS
+    float sdf_scale;
+};
+
+// all threads of the block must call this (it ends with a barrier)
+__device__ __forceinline__ MlpW stage_mlp(const PinMlp& m, float* s_w) {
+    for (int e = threadIdx.x; e < kWSize; e += blockDim.x) {
+        float v = 0.f;
+        if (e < kWB1) {
+            const int c = e / kWRow, i = e - c * kWRow;
+            v = i < kD ? m.W1[c * kD + i] : 0.f;
+        } else if (e < kWW2) {
+            v = m.b1[e - kWB1];
+        } else if (e < kWB2) {
+            v = m.W2[e - kWW2];
+        } else if (e == kWB2) {
+            v = m.b2[0];
+        }
+        s_w[e] = v;
+    }
+    __syncthreads();
+    return MlpW{s_w, m.sdf_scale};
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void load_row(const float* __restrict__ w, int c, float (&r)[kWRow]) {
+    const float4* p = (const float4*)(w + c * kWRow);
+    const float4 a = p[0], b = p[1], d = p[2];
+    r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+    r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+    r[8] = d.x; r[9] = d.y; r[10] = d.z; r[11] = d.w;
+}
 
 // Decoder forward fused with its input gradient (model/decoder.py:66-88):
 //   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
-// One pass over the hidden units, two at a time with packed FMAs (v_pk_fma_f32); weights
-// are wave-uniform (scalar loads).
+// One pass over the hidden units, two at a time with packed FMAs (v_pk_fma_f32).
 template <bool GRAD, int OFF, int NOUT>
-__device__ __forceinline__ float mlp_sdf(const PinMlp& m, const float (&x)[kD], float (&gx)[NOUT]) {
+__device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
     f32x2 out2 = {0.f, 0.f};
     f32x2 g2[NOUT];
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) g2[i] = (f32x2){0.f, 0.f};
-#pragma unroll 2
+#pragma unroll 1
     for (int c = 0; c < kH; c += 2) {
-        const float* w0 = m.W1 + c * kD;
-        const float* w1 = w0 + kD;
+        float w0[kWRow], w1[kWRow];
+        load_row(m.w, c, w0);
+        load_row(m.w, c + 1, w1);
+        const f32x2 b = *(const f32x2*)(m.w + kWB1 + c);
+        const f32x2 v2 = *(const f32x2*)(m.w + kWW2 + c);
         f32x2 acc = {0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < kD; ++i) {
@@ -371,8 +514,8 @@ __device__ __forceinline__ float mlp_sdf(const PinMlp& m, const float (&x)[kD], 
             const f32x2 xv = {x[i], x[i]};
             acc = __builtin_elementwise_fma(wv, xv, acc);
         }
-        const f32x2 pre = acc + (f32x2){m.b1[c], m.b1[c + 1]};
-        const f32x2 a = {pre.x > 0.f ? m.W2[c] : 0.f, pre.y > 0.f ? m.W2[c + 1] : 0.f};
+        const f32x2 pre = acc + b;
+        const f32x2 a = {pre.x > 0.f ? v2.x : 0.f, pre.y > 0.f ? v2.y : 0.f};
         out2 = __builtin_elementwise_fma(a, pre, out2);
         if (GRAD) {
 #pragma unroll
@@ -386,7 +529,7 @@ __device__ __forceinline__ float mlp_sdf(const PinMlp& m, const float (&x)[kD], 
 #pragma unroll
         for (int i = 0; i < NOUT; ++i) gx[i] = (g2[i].x + g2[i].y) * m.sdf_scale;
     }
-    return ((out2.x + out2.y) + m.b2[0]) * m.sdf_scale;
+    return ((out2.x + out2.y) + m.w[kWB2]) * m.sdf_scale;
 }
 
 }  // namespace pin

@@ -157,16 +157,14 @@ __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints
     if (!valid) o.cert = 0.f;
 }
 
+// Everything after the candidate scan: IDW weights, streamed neighbour inputs, decoder,
+// closed-form gradient, outputs.  Used by the fused kernels and by the split epilogue.
 template <bool WF, bool PGO, bool GRAD, class Src>
-__device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const PinMlp& m,
-                                               const float* __restrict__ q, int64_t i, int nn_k, int zero_empty,
-                                               float* __restrict__ sdf_out, float* __restrict__ grad_out,
-                                               int* __restrict__ nn_out, float* __restrict__ cert_out,
-                                               float* __restrict__ std_out) {
-    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
-    TopK tk;
-    tk.init();
-    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+__device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoints& p, const MlpW& m, float qx,
+                                                   float qy, float qz, const TopK& tk, int nn, int64_t i, int nn_k,
+                                                   int zero_empty, float* __restrict__ sdf_out,
+                                                   float* __restrict__ grad_out, int* __restrict__ nn_out,
+                                                   float* __restrict__ cert_out, float* __restrict__ std_out) {
     // IDW weights from the top-k distances alone (neural_points.py:618-632)
     float u[kK];
     float S = 0.f;
@@ -312,26 +310,100 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
     if (std_out) std_out[i] = std_v;
 }
 
+template <bool WF, bool PGO, bool GRAD, class Src>
+__device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const MlpW& m,
+                                               const float* __restrict__ q, int64_t i, int nn_k, int zero_empty,
+                                               float* __restrict__ sdf_out, float* __restrict__ grad_out,
+                                               int* __restrict__ nn_out, float* __restrict__ cert_out,
+                                               float* __restrict__ std_out) {
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    TopK tk;
+    tk.init();
+    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    query_sdf_epilogue<WF, PGO, GRAD>(src, p, m, qx, qy, qz, tk, nn, i, nn_k, zero_empty, sdf_out, grad_out, nn_out,
+                                      cert_out, std_out);
+}
+
 template <bool WF, bool PGO, bool GRAD>
 __global__ void __launch_bounds__(kBlock)
 k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n, int nn_k,
             int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out, int* __restrict__ nn_out,
             float* __restrict__ cert_out, float* __restrict__ std_out) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const HashSource src(h, p);
-    query_sdf_body<WF, PGO, GRAD>(src, p, m, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+    query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
 }
 
 template <bool WF, bool PGO, bool GRAD, bool FAT>
 __global__ void __launch_bounds__(kBlock)
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n,
                  int nn_k, int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out,
-                 int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out) {
+                 int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out,
+                 const int* __restrict__ order) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
+    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    if (t >= n) return;
+    const int64_t i = order ? order[t] : t;
+    const GridSource<FAT> src(g, p);
+    query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+}
+
+// Query binning (counting sort by 8x8x8-cell bins of the grid box): random batches are
+// processed bin by bin so that a block's gathers share lines and, with xcd_block(), each XCD's
+// L2 sees one region of the map.  Outputs still go to each query's own index.
+__device__ __forceinline__ int query_bin(const float* __restrict__ q, int64_t i, const PinGrid& g) {
+    const float res = g.resolution;
+    const int bx = (g.dims.nbx + 1) >> 1, by = (g.dims.nby + 1) >> 1, bz = (g.dims.nbz + 1) >> 1;
+    auto axis = [&](float v, int64_t o, int nb) -> int {
+        int64_t c = ((int64_t)floorf(v / res) - o) >> 3;
+        return (int)(c < 0 ? 0 : (c >= nb ? nb - 1 : c));
+    };
+    const int cx = axis(q[3 * i], g.dims.ox, bx);
+    const int cy = axis(q[3 * i + 1], g.dims.oy, by);
+    const int cz = axis(q[3 * i + 2], g.dims.oz, bz);
+    return (cz * by + cy) * bx + cx;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_bin_count(const float* __restrict__ q, int64_t n, const PinGrid g, int* __restrict__ hist, int* __restrict__ rank) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const GridSource<FAT> src(g, p);
-    query_sdf_body<WF, PGO, GRAD>(src, p, m, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+    rank[i] = atomicAdd(hist + query_bin(q, i, g), 1);
+}
+
+// in-place exclusive scan of nb counts, one block of 1024 threads (bins per thread contiguous)
+__global__ void __launch_bounds__(1024) k_bin_scan(int* __restrict__ hist, int nb) {
+    __shared__ int part[1024];
+    const int per = (nb + 1023) / 1024;
+    const int lo = threadIdx.x * per, hi = min(nb, lo + per);
+    int s = 0;
+    for (int k = lo; k < hi; ++k) s += hist[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = part[threadIdx.x] - s;
+    for (int k = lo; k < hi; ++k) {
+        const int c = hist[k];
+        hist[k] = run;
+        run += c;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_bin_scatter(const float* __restrict__ q, int64_t n, const PinGrid g, const int* __restrict__ off,
+              const int* __restrict__ rank, int* __restrict__ order) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    order[off[query_bin(q, i, g)] + rank[i]] = (int)i;
 }
 
 // ------------------------------------------------------------------ drop-in query_feature
@@ -670,12 +742,12 @@ int pin_train_scatter(const int32_t* ids, const float* weights, int64_t n, int32
 
 static bool grid_ok(const PinGrid* g) {
     return g && g->bricks && g->crec && g->cgid && g->offsets && g->num_cells > 0 && g->resolution > 0.f &&
-           g->dims.nbx > 0 && g->dims.nby > 0 && g->dims.nbz > 0;
+           g->dims.nbx > 0 && g->dims.nby > 0 && g->dims.nbz > 0 && (!g->fat || (g->cfeat && g->ccert));
 }
 
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
                        int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
-                       int32_t* nn_count, float* certainty, float* sdf_std, void* stream) {
+                       int32_t* nn_count, float* certainty, float* sdf_std, void* workspace, void* stream) {
     if (!grid_ok(grid) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
         return PIN_ERR_ARG;
     const bool fat = grid->fat != 0;
@@ -683,13 +755,24 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
         return PIN_ERR_ARG;
     if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
     if (n == 0) return PIN_OK;
-    if (!q) return PIN_ERR_ARG;
+    if (!q || n > INT32_MAX) return PIN_ERR_ARG;
     const bool g = grad != nullptr;
     const bool pgo = pts->after_pgo != 0;
     auto s = as_stream(stream);
+    int* order = nullptr;
+    if (workspace) {
+        const int nbins = (int)pin_query_bins(&grid->dims);
+        int* hist = (int*)workspace;
+        int* rank = hist + nbins;
+        order = rank + n;
+        if (hipMemsetAsync(hist, 0, (size_t)nbins * sizeof(int), s) != hipSuccess) return PIN_ERR_HIP;
+        hipLaunchKernelGGL(k_bin_count, grid_for(n), dim3(kBlock), 0, s, q, n, *grid, hist, rank);
+        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, hist, nbins);
+        hipLaunchKernelGGL(k_bin_scatter, grid_for(n), dim3(kBlock), 0, s, q, n, *grid, hist, rank, order);
+    }
 #define PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT)                                                                     \
     hipLaunchKernelGGL((k_query_sdf_grid<WF, PGO, GRAD, FAT>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, *mlp, \
-                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std)
+                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std, order)
 #define PIN_SDFG_FAT(WF, PGO, GRAD) \
     do { if (fat) PIN_LAUNCH_SDFG(WF, PGO, GRAD, true); else PIN_LAUNCH_SDFG(WF, PGO, GRAD, false); } while (0)
     if (weighted_first) {

@@ -47,7 +47,7 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 }
 
 template <bool WF, class Src>
-__device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const PinMlp& m,
+__device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t r, PinTrainState st) {
     float qx, qy, qz;
@@ -124,20 +124,24 @@ template <bool WF>
 __global__ void __launch_bounds__(kBlock)
 k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main + 6 * c.n_stencil) return;
     const HashSource src(h, p);
-    train_forward_body<WF>(src, p, m, coord, ts, c, r, st);
+    train_forward_body<WF>(src, p, mw, coord, ts, c, r, st);
 }
 
 template <bool WF>
 __global__ void __launch_bounds__(kBlock)
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main + 6 * c.n_stencil) return;
     const GridSource<false> src(g, p);
-    train_forward_body<WF>(src, p, m, coord, ts, c, r, st);
+    train_forward_body<WF>(src, p, mw, coord, ts, c, r, st);
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
@@ -182,17 +186,18 @@ __device__ __forceinline__ float wave_sum_f(float v) {
 // decoder backward of one input row x with upstream dL/d(out) = so (already times sdf_scale):
 // gf += sum_c delta_c W1[c][0:8]; decoder-parameter terms summed over the wave into mw (lane 0)
 template <bool MLP_GRAD>
-__device__ __forceinline__ void decoder_backward(const PinMlp& m, const float (&x)[kD], float so, float (&gf)[kF],
+__device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)[kD], float so, float (&gf)[kF],
                                                  float* __restrict__ mw, bool accumulate) {
 #pragma unroll 2
     for (int cc = 0; cc < kH; ++cc) {
-        const float* wr = m.W1 + cc * kD;
+        float wr[kWRow];
+        load_row(m.w, cc, wr);
         float acc = 0.f;
 #pragma unroll
         for (int i = 0; i < kD; ++i) acc = fmaf(wr[i], x[i], acc);
-        const float pre = acc + m.b1[cc];
+        const float pre = acc + m.w[kWB1 + cc];
         const bool on = pre > 0.f;
-        const float delta = on ? so * m.W2[cc] : 0.f;
+        const float delta = on ? so * m.w[kWW2 + cc] : 0.f;
 #pragma unroll
         for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
         if (MLP_GRAD) {
@@ -223,6 +228,8 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
     __shared__ float gst[kBlock * kJ * kF];
     __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
+    __shared__ float s_mlp[kWSize];
+    const MlpW mlpw = stage_mlp(m, s_mlp);
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool live = r < nrows;
@@ -231,7 +238,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     double loss = 0.0;
     const float dsdf = live ? row_dsdf(c, st.sdf, label, r, loss) * c.grad_scale : 0.f;
     loss *= (double)c.grad_scale;
-    const float so = dsdf * m.sdf_scale;              // dL/d(lout output)
+    const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
     float* mw = MLP_GRAD ? mlds[wave] : nullptr;
     if (WF) {
         float x[kD];
@@ -240,7 +247,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         float gf[kF];
 #pragma unroll
         for (int d = 0; d < kF; ++d) gf[d] = 0.f;
-        decoder_backward<MLP_GRAD>(m, x, so, gf, mw, false);
+        decoder_backward<MLP_GRAD>(mlpw, x, so, gf, mw, false);
 #pragma unroll
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = gf[d];
     } else {
@@ -264,7 +271,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             float gf[kF];
 #pragma unroll
             for (int d = 0; d < kF; ++d) gf[d] = 0.f;
-            if (__any(ok) || MLP_GRAD) decoder_backward<MLP_GRAD>(m, x, so * w, gf, mw, j > 0);
+            if (__any(ok) || MLP_GRAD) decoder_backward<MLP_GRAD>(mlpw, x, so * w, gf, mw, j > 0);
 #pragma unroll
             for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
         }

@@ -22,6 +22,7 @@ instead (not the reference's behaviour).
 """
 import ctypes
 import math
+import os
 import weakref
 
 import numpy as np
@@ -213,6 +214,7 @@ class NeuralPoints(nn.Module):
         self.neighbor_K = self.neighbor_dx.shape[0]
         self.max_valid_dist2 = 3 * ((num_nei_cells + 1) * self.resolution) ** 2
         dx_host = np.ascontiguousarray(self.neighbor_dx.cpu().numpy().astype(np.int32))
+        self.neighbor_window = int(np.abs(dx_host).max()) if dx_host.size else 0
         self._cells_host = dx_host
         self._cells = None  # device tables built lazily (need the HIP runtime)
         self._offsets = None
@@ -314,11 +316,11 @@ class NeuralPoints(nn.Module):
         pts = self.neural_points.contiguous()
         _lib.require_device(pts)
         res = float(np.float32(self.resolution))
-        cells = torch.floor(pts / res).to(torch.int64)
-        lo = cells.min(0)[0]
-        hi = cells.max(0)[0]
-        ext = ((hi - lo + 1 + 3) // 4).cpu().tolist()
-        lo = lo.cpu().tolist()
+        bounds = torch.empty(6, dtype=torch.int64, device=pts.device)
+        _lib.call("pin_cell_bounds", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(bounds), _lib.stream())
+        b = bounds.cpu().tolist()
+        lo, hi = b[:3], b[3:]
+        ext = [(h - l + 1 + 3) // 4 for l, h in zip(lo, hi)]
         nb = ext[0] * ext[1] * ext[2]
         if nb > self.MAX_GRID_BRICKS:
             return None
@@ -334,7 +336,8 @@ class NeuralPoints(nn.Module):
         return bricks, dims, int(marked)
 
     def compact_records(self, mode: str, fat: bool):
-        """(crec [n_occ,16] f32, cgid [n_occ] i32) in brick order for a query mode."""
+        """(crec [n_occ,4] f32, cfeat [n_occ,8] or None, ccert [n_occ] or None, cgid [n_occ] i32) in
+        brick order for a query mode (features / certainties copied only when ``fat``)."""
         occ = self.occupancy()
         local = mode == "local"
         feats = (self.local_geo_features if local else self.geo_features) if fat else None
@@ -347,25 +350,31 @@ class NeuralPoints(nn.Module):
     def _build_compact(self, occ, rec, feats, cert):
         bricks, dims, n_occ = occ
         pts = self.neural_points.contiguous()
-        crec = torch.zeros((max(n_occ, 1), 16), dtype=torch.float32, device=pts.device)
-        cgid = torch.full((max(n_occ, 1),), -1, dtype=torch.int32, device=pts.device)
+        n = max(n_occ, 1)
+        crec = torch.zeros((n, 4), dtype=torch.float32, device=pts.device)
+        cfeat = torch.zeros((n, 8), dtype=torch.float32, device=pts.device) if feats is not None else None
+        ccert = torch.zeros((n,), dtype=torch.float32, device=pts.device) if feats is not None else None
+        cgid = torch.full((n,), -1, dtype=torch.int32, device=pts.device)
         f = feats.detach().contiguous() if feats is not None else None
         c = cert.detach().contiguous() if cert is not None else None
         _lib.call("pin_grid_fill", _lib.ptr(pts), pts.shape[0], float(np.float32(self.resolution)),
                   _lib.ptr(self.buffer_pt_index), self.buffer_size, ctypes.byref(dims), _lib.ptr(bricks),
-                  _lib.ptr(rec), _lib.ptr(f), _lib.ptr(c), _lib.ptr(crec), _lib.ptr(cgid), _lib.stream())
-        return crec, cgid
+                  _lib.ptr(rec), _lib.ptr(f), _lib.ptr(c), _lib.ptr(crec), _lib.ptr(cfeat), _lib.ptr(ccert),
+                  _lib.ptr(cgid), _lib.stream())
+        return crec, cfeat, ccert, cgid
 
     def grid_view(self, mode: str, fat: bool):
         from .query import _View
         bricks, dims, n_occ = self.occupancy()
-        crec, cgid = self.compact_records(mode, fat)
+        crec, cfeat, ccert, cgid = self.compact_records(mode, fat)
         offs = self._offset_table()
         g = _lib.PinGrid(bricks=bricks.data_ptr(), dims=dims, crec=crec.data_ptr(), cgid=cgid.data_ptr(),
                          n_occ=n_occ, offsets=offs.data_ptr(), resolution=float(np.float32(self.resolution)),
                          num_cells=int(self.neighbor_K), max_valid_dist2=float(np.float32(self.max_valid_dist2)),
-                         fat=int(fat))
-        return _View(g, (bricks, crec, cgid, offs))
+                         cfeat=cfeat.data_ptr() if cfeat is not None else None,
+                         ccert=ccert.data_ptr() if ccert is not None else None, fat=int(fat), window=99 if os.environ.get("PIN_GRID_SCAN") == "cells" else self.neighbor_window,
+                         reserved=0)
+        return _View(g, (bricks, crec, cfeat, ccert, cgid, offs))
 
     # ------------------------------------------------------------------ map update
     def update(self, points: torch.Tensor, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor, cur_ts):
@@ -431,12 +440,31 @@ class NeuralPoints(nn.Module):
         self.global2local = g2l
         self.local_geo_features = nn.Parameter(self.geo_features[mask])
         self.local_orientation = sensor_orientation
+        self._local_snapshot = self._snapshot()
+
+    def _snapshot(self):
+        """Identity + version of the position / orientation tensors right after reset_local_map:
+        while both the global and the local copies are untouched, writing the local copy back
+        (assign_local_to_global) is an exact no-op and is skipped, so derived indexes built over
+        ``neural_points`` (records, occupancy grid) stay valid across mapping() calls."""
+        ts = (self.neural_points, self.local_neural_points, self.point_orientations, self.local_point_orientations)
+        return tuple((weakref.ref(t), t._version) for t in ts)
+
+    def _unchanged_since_reset(self, idx):
+        snap = getattr(self, "_local_snapshot", None)
+        if snap is None:
+            return False
+        ts = (self.neural_points, self.local_neural_points, self.point_orientations, self.local_point_orientations)
+        return all(snap[i][0]() is ts[i] and ts[i]._version == snap[i][1] for i in idx)
 
     def assign_local_to_global(self):
         """model/neural_points.py:315-324."""
         m = self.local_mask
-        self.neural_points[m[:-1]] = self.local_neural_points
-        self.point_orientations[m[:-1]] = self.local_point_orientations
+        if not self._unchanged_since_reset((0, 1)):
+            self.neural_points[m[:-1]] = self.local_neural_points
+        if not self._unchanged_since_reset((2, 3)):
+            self.point_orientations[m[:-1]] = self.local_point_orientations
+        self._local_snapshot = self._snapshot()
         self.geo_features[m] = self.local_geo_features.data
         self.point_certainties[m[:-1]] = self.local_point_certainties
         self.point_ts_update[m[:-1]] = self.local_point_ts_update

@@ -2,12 +2,19 @@
 Function behind ``NeuralPoints.query_feature`` and the fused SDF(+gradient) call
 used by the tracker and mesher paths."""
 import ctypes
+import os
 
 import numpy as np
 import torch
 from torch.autograd.function import once_differentiable
 
 from . import _lib
+
+# counting-sort queries into spatial bins before the grid SDF query (PIN_QUERY_BIN=1 enables):
+# the binned kernel is ~20% faster on random batches, but the three extra launches cost more
+# than that at 262K queries (tools/prof_bin.sh), so it is off by default
+_BIN_QUERIES = os.environ.get("PIN_QUERY_BIN", "0") == "1"
+_BIN_MIN = 65536   # below this the sort's launches cost more than the locality returns
 
 
 class _View:
@@ -139,8 +146,14 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
     if nm.backend() == "grid":
         gv = nm.grid_view(mode, True)
+        ws = None
+        if _BIN_QUERIES and n >= _BIN_MIN:
+            d = gv.struct.dims
+            nbins = ((d.nbx + 1) // 2) * ((d.nby + 1) // 2) * ((d.nbz + 1) // 2)
+            ws = torch.empty((nbins + 2 * n,), dtype=torch.int32, device=dev)
         _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
-                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
+                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.ptr(ws),
+                  _lib.stream())
     else:
         _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
                   _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())

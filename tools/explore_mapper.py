@@ -38,6 +38,7 @@ def main():
             p.requires_grad_(False)
         coord, label, ts = surface_pool(pts, bs, device="cuda")
         mapper = P.Mapper(nm.config, None, nm, dec)
+        mapper.set_pool(coord, label, ts)
         fg = torch.zeros_like(nm.local_geo_features.data)
         c = nm.config
         n = bs

@@ -2,7 +2,7 @@
 # PMC passes (one counter group per run, kernel-trace only), for the roofline traffic figure.
 # PMC_GROUPS: groups separated by ';', counters inside a group by spaces.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
 rm -rf $OUT
 mkdir -p $OUT
 export TMPDIR=/tmp
