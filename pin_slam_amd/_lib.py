@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpin_slam_amd.so")
+# PIN_LIB overrides the library path (experiment variants built by tools/variants.py)
+LIB_PATH = os.environ.get("PIN_LIB") or os.path.join(_HERE, "libpin_slam_amd.so")
 
 PIN_OK = 0
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}

@@ -33,16 +33,19 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, extra=(), out: str = None) -> str:
+    """Compile every csrc/*.hip into one shared library (``out`` defaults to the in-tree LIB;
+    ``extra`` adds compiler flags, e.g. -D switches for experiment variants)."""
+    out = out or LIB
+    if out == LIB and not force and not _stale():
         return LIB
     cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"),
-           *sources(), "-o", LIB + ".tmp"]
+           *sources(), "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

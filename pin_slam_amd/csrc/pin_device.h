@@ -228,7 +228,10 @@ struct GridSource {
             for (int j0 = 0; __any(j0 < cnt); j0 += CH) {
                 int ci[CH];
 #pragma unroll
-                for (int u = 0; u < CH; ++u) ci[u] = (j0 + u < cnt) ? s_list[j0 + u][tid] : -1;
+                for (int u = 0; u < CH; ++u) {
+                    const int v = s_list[j0 + u][tid];   // j0 + u < kSeg: stale slots are masked
+                    ci[u] = (j0 + u < cnt) ? v : -1;
+                }
                 float4 r[CH];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
@@ -446,11 +449,13 @@ __device__ __forceinline__ float gather_certainty(const Src& src, const Neighbou
     return cert;
 }
 
-// Decoder weights staged in LDS once per block (stage_mlp): W1 rows padded to 12 floats
-// (three 16-B broadcast reads per row), then b1, W2, b2.  Broadcast LDS reads return in order,
-// so the compiler keeps several in flight; the scalar-load form paid a dependent K$ round trip
-// per hidden-unit pair.
-constexpr int kWRow = 12;
+// Decoder weights staged in LDS once per block (stage_mlp), laid out for the packed loop:
+// hidden units in pairs (c, c+1), W1 interleaved per input i as {W1[c][i], W1[c+1][i]}
+// (12 inputs incl. one pad -> 24 floats per pair), then b1, W2, b2.  A pair's operand for
+// v_pk_fma_f32 is one 8-B broadcast LDS read; broadcast reads return in order, so several
+// stay in flight (the scalar-load form paid a dependent K$ round trip per pair).
+constexpr int kWRow = 12;                    // padded inputs per hidden unit
+constexpr int kWPair = 2 * kWRow;            // floats per hidden-unit pair
 constexpr int kWB1 = kH * kWRow;
 constexpr int kWW2 = kWB1 + kH;
 constexpr int kWB2 = kWW2 + kH;
@@ -461,12 +466,15 @@ struct MlpW {
     float sdf_scale;
 };
 
+// W1[c][i] in the staged layout
+__device__ __forceinline__ int w1_at(int c, int i) { return (c >> 1) * kWPair + 2 * i + (c & 1); }
+
 // all threads of the block must call this (it ends with a barrier)
 __device__ __forceinline__ MlpW stage_mlp(const PinMlp& m, float* s_w) {
     for (int e = threadIdx.x; e < kWSize; e += blockDim.x) {
         float v = 0.f;
         if (e < kWB1) {
-            const int c = e / kWRow, i = e - c * kWRow;
+            const int pr = e / kWPair, r = e - pr * kWPair, i = r >> 1, c = 2 * pr + (r & 1);
             v = i < kD ? m.W1[c * kD + i] : 0.f;
         } else if (e < kWW2) {
             v = m.b1[e - kWB1];
@@ -483,12 +491,10 @@ __device__ __forceinline__ MlpW stage_mlp(const PinMlp& m, float* s_w) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// row c of W1 from the staged layout (stride-2 reads)
 __device__ __forceinline__ void load_row(const float* __restrict__ w, int c, float (&r)[kWRow]) {
-    const float4* p = (const float4*)(w + c * kWRow);
-    const float4 a = p[0], b = p[1], d = p[2];
-    r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
-    r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
-    r[8] = d.x; r[9] = d.y; r[10] = d.z; r[11] = d.w;
+#pragma unroll
+    for (int i = 0; i < kWRow; ++i) r[i] = w[w1_at(c, i)];
 }
 
 // Decoder forward fused with its input gradient (model/decoder.py:66-88):
@@ -500,29 +506,23 @@ __device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], fl
     f32x2 g2[NOUT];
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) g2[i] = (f32x2){0.f, 0.f};
-#pragma unroll 1
+#pragma unroll 2
     for (int c = 0; c < kH; c += 2) {
-        float w0[kWRow], w1[kWRow];
-        load_row(m.w, c, w0);
-        load_row(m.w, c + 1, w1);
+        const f32x2* __restrict__ wp = (const f32x2*)(m.w + (c >> 1) * kWPair);
+        f32x2 wv[kD];
+#pragma unroll
+        for (int i = 0; i < kD; ++i) wv[i] = wp[i];
         const f32x2 b = *(const f32x2*)(m.w + kWB1 + c);
         const f32x2 v2 = *(const f32x2*)(m.w + kWW2 + c);
         f32x2 acc = {0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < kD; ++i) {
-            const f32x2 wv = {w0[i], w1[i]};
-            const f32x2 xv = {x[i], x[i]};
-            acc = __builtin_elementwise_fma(wv, xv, acc);
-        }
+        for (int i = 0; i < kD; ++i) acc = __builtin_elementwise_fma(wv[i], (f32x2){x[i], x[i]}, acc);
         const f32x2 pre = acc + b;
         const f32x2 a = {pre.x > 0.f ? v2.x : 0.f, pre.y > 0.f ? v2.y : 0.f};
         out2 = __builtin_elementwise_fma(a, pre, out2);
         if (GRAD) {
 #pragma unroll
-            for (int i = 0; i < NOUT; ++i) {
-                const f32x2 wv = {w0[OFF + i], w1[OFF + i]};
-                g2[i] = __builtin_elementwise_fma(a, wv, g2[i]);
-            }
+            for (int i = 0; i < NOUT; ++i) g2[i] = __builtin_elementwise_fma(a, wv[OFF + i], g2[i]);
         }
     }
     if (GRAD) {
