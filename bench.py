@@ -52,6 +52,23 @@ def mapper_bytes_per_iter(n, L, dec=10):
     return rows * (932 + 512) + 32 * 8 * (L + 1)
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def measured_traffic(kernel_prefix):
+    """HBM-side bytes per launch of the headline kernel from the committed PMC pass
+    (tools/traffic.sh -> profiles/traffic.json), or None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k in t.get("kernels", []):
+        if k["name"].startswith(kernel_prefix):
+            return k["bytes_per_launch"]
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,8 +260,12 @@ def main():
                    "candidate_backend": backend, "map_index_build_ms": round(build_ms, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": args.traffic_bytes,
-                     "kernel": "k_query_sdf", "kernel_ms": kern_ms,
+                     "traffic": (args.traffic_bytes if args.traffic_bytes is not None
+                                 else measured_traffic(f"k_query_sdf_grid<{str(wf).lower()}, false, true, true>"
+                                                       if backend == "grid" else "k_query_sdf<")),
+                     "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
+                                       "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
+                     "kernel": "k_query_sdf_grid" if backend == "grid" else "k_query_sdf", "kernel_ms": kern_ms,
                      "algorithmic_bytes_per_query": BYTES_PER_QUERY},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -10,6 +10,17 @@
 
 #include "pin_slam_amd.h"
 
+// Tuning switches (compile-time; tools/variants.py sweeps them)
+#ifndef PIN_MLP_UNROLL
+#define PIN_MLP_UNROLL 2     // hidden-unit pairs per decoder-loop iteration
+#endif
+#ifndef PIN_NB_GROUP
+#define PIN_NB_GROUP 4       // neighbours gathered per streaming group
+#endif
+#ifndef PIN_GRID_CHUNK
+#define PIN_GRID_CHUNK 8     // candidate records fetched per round trip (grid source)
+#endif
+
 namespace pin {
 
 constexpr int kF = PIN_FEATURE_DIM;      // feature_dim
@@ -151,7 +162,7 @@ __device__ __forceinline__ uint32_t sel8(const uint32_t (&w)[8], int k) {
 
 template <bool FAT>
 struct GridSource {
-    static constexpr int kChunk = 8;
+    static constexpr int kChunk = PIN_GRID_CHUNK;
     static constexpr int kSeg = 32;   // offsets per list segment: 32 KB of LDS per block
     const PinGrid& gr;
     const PinPoints& p;
@@ -506,7 +517,7 @@ __device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], fl
     f32x2 g2[NOUT];
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) g2[i] = (f32x2){0.f, 0.f};
-#pragma unroll 2
+#pragma unroll PIN_MLP_UNROLL
     for (int c = 0; c < kH; c += 2) {
         const f32x2* __restrict__ wp = (const f32x2*)(m.w + (c >> 1) * kWPair);
         f32x2 wv[kD];

@@ -195,7 +195,7 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
         for (int j = 0; j < kK; ++j) {
             // neighbours stream in two groups of four: bounds the registers held by gathers
             // in flight while keeping four lines outstanding per lane
-            if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
+            if (j && j % PIN_NB_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
             const bool valid = u[j] > 0.f;
             NbInput in;
             if (want_cert) stream_neighbour<PGO, true>(src, p, tk.g[j], valid, qx, qy, qz, in);
