@@ -281,7 +281,11 @@ typedef struct PinTrainCfg {
     float weight_e;              /* eikonal weight (mapper.py:547) */
     float grad_scale;            /* multiplies loss and gradients: 1, or 1/world_size so that a SUM
                                     all-reduce of per-rank gradients is the gradient of the mean loss */
-    int32_t reserved;
+    int32_t grad_stride;         /* floats per row of grad_features: 8 = plain [L+1,8] gradient (the
+                                    forward applies the certainty side effect with atomics); 16 = 64-B
+                                    rows {g0..g7, certainty delta, 0 x7}: the backward adds each
+                                    neighbour's weight to lane 8 in the same memory-side request as
+                                    its gradient and the forward leaves certainties alone */
 } PinTrainCfg;
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
@@ -303,7 +307,7 @@ typedef struct PinAdamStep {
     float bias_correction2_sqrt; /* float32(sqrt(1 - beta2^t)) */
     float eps;                   /* adam_eps */
     int32_t zero_grad;           /* 1: grad := 0 after the step (opt.zero_grad of the next iteration) */
-    int32_t reserved;
+    int32_t grad_stride;         /* element i's gradient is grad[(i/8)*grad_stride + i%8] (8: contiguous) */
 } PinAdamStep;
 
 /* decoder-parameter gradient layout of pin_train_backward's mlp_grad */
@@ -328,7 +332,7 @@ static inline int64_t pin_train_workspace_bytes(int64_t rows) {
 /*
  * pin_train_backward -- gradient of  BCEWithLogits(sdf/sigma, sigmoid(label/sigma)) (mean)
  *   + weight_e * mean_k (|g_k| - 1)^2,  g_k = central differences of the stencil rows
- * (mapper.py:515-547) w.r.t. the local features (grad_features [L+1,8] += , may be NULL) and,
+ * (mapper.py:515-547) w.r.t. the local features (grad_features [L+1,grad_stride] += , may be NULL) and,
  * if mlp_grad != NULL, the decoder parameters (mlp_grad [PIN_MLP_GRAD_SIZE] += , summed in a
  * fixed order).  loss_out (1 double on the device, may be NULL) receives the loss.  workspace:
  * pin_train_workspace_bytes(rows) bytes, needed when loss_out or mlp_grad is non-NULL.

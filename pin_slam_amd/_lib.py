@@ -63,7 +63,7 @@ class PinMlp(ctypes.Structure):
 
 class PinTrainCfg(ctypes.Structure):
     _fields_ = [("n_main", i64), ("n_stencil", i64), ("decimation", i32), ("nn_k", i32), ("weighted_first", i32),
-                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("reserved", i32)]
+                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("grad_stride", i32)]
 
 
 class PinTrainState(ctypes.Structure):
@@ -73,7 +73,7 @@ class PinTrainState(ctypes.Structure):
 
 class PinAdamStep(ctypes.Structure):
     _fields_ = [("neg_step_size", f32), ("one_minus_beta1", f32), ("beta2", f32), ("one_minus_beta2", f32),
-                ("bias_correction2_sqrt", f32), ("eps", f32), ("zero_grad", i32), ("reserved", i32)]
+                ("bias_correction2_sqrt", f32), ("eps", f32), ("zero_grad", i32), ("grad_stride", i32)]
 
 
 MLP_GRAD_SIZE = HIDDEN_DIM * (FEATURE_DIM + 3) + 2 * HIDDEN_DIM + 1

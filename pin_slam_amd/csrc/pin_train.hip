@@ -91,9 +91,11 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             st.weights[r * nn_k + j] = w;
         }
         if (valid) {
-            // training side effects (neural_points.py:640, :644)
-            if (st.certainties) atomicAdd(st.certainties + id, w);
-            if (qts >= 0 && st.ts_update) atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
+            // training side effects (neural_points.py:640, :644); with 16-float gradient rows the
+            // certainty is added by the backward; ts: read first, the max is usually a no-op
+            if (st.certainties && c.grad_stride != 16) atomicAdd(st.certainties + id, w);
+            if (qts >= 0 && st.ts_update && st.ts_update[id] < qts)
+                atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
         }
         if (WF) {
 #pragma unroll
@@ -294,23 +296,28 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         }
     }
     if (!grad_features) return;
-    // scatter: element e = (row, j, d), d fastest
+    // scatter: element e = (row, j, lane), lane fastest, L lanes per (row, neighbour): L = 8 for
+    // plain rows (a wave instruction covers 8 rows x 32 B), L = 9 for 64-B rows (lane 8 = the
+    // certainty; 7 rows per instruction).  One memory-side request per (row, neighbour).
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int total = kBlock * nn_k * kF;
+    const int L = c.grad_stride == 16 ? kF + 1 : kF;
+    const int total = kBlock * nn_k * L;
     for (int e = threadIdx.x; e < total; e += kBlock) {
-        const int d = e & (kF - 1);
-        const int rj = e >> 3;
+        const int rj = e / L;
+        const int d = e - rj * L;
         const int lr = rj / nn_k, j = rj - lr * nn_k;
         const int64_t rr = row0 + lr;
         if (rr >= nrows) break;
         const int id = st.ids[rr * nn_k + j];
         if (id < 0) continue;
-        const float g = WF ? st.weights[rr * nn_k + j] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
-        atomicAdd(grad_features + (int64_t)id * kF + d, g);
+        const float w = st.weights[rr * nn_k + j];
+        float g;
+        if (d == kF) g = w;   // certainty lane (64-B rows only)
+        else g = WF ? w * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        atomicAdd(grad_features + (int64_t)id * c.grad_stride + d, g);
     }
 }
 
-// sum of the per-wave loss partials, fixed order (1024 threads, strided, then a tree)
 __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ part, int64_t n,
                                                      double* __restrict__ out) {
     __shared__ double red[16];
@@ -336,23 +343,45 @@ __global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restri
     out[e] += v;
 }
 
-// torch.optim.Adam (single-tensor form, weight_decay 0):
-//   m = m + (1-b1)(g - m);  v = v b2 + ((1-b2) g) g;  p += (-lr/bc1 * m) / (sqrt(v)/sqrt(bc2) + eps)
-__global__ void __launch_bounds__(kBlock)
-k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
-       PinAdamStep a) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const float g = grad[i];
-    float m = m_[i], v = v_[i];
+// torch.optim.Adam (single-tensor form, weight_decay 0), four elements per thread:
+//   m = m + (1-b1)(g - m);  v = v b2 + ((1-b1') g) g;  p += (-lr/bc1 * m) / (sqrt(v)/sqrt(bc2) + eps)
+// Element i's gradient sits at (i/8)*grad_stride + i%8 (64-B accumulator rows: lanes 0..7).
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, const PinAdamStep& a) {
     m = m + a.one_minus_beta1 * (g - m);
     v = v * a.beta2;
     v = v + (a.one_minus_beta2 * g) * g;
     const float denom = sqrtf(v) / a.bias_correction2_sqrt + a.eps;
-    prm[i] = prm[i] + (a.neg_step_size * m) / denom;
-    m_[i] = m;
-    v_[i] = v;
-    if (a.zero_grad) grad[i] = 0.f;
+    p = p + (a.neg_step_size * m) / denom;
+    return p;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
+       PinAdamStep a) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i0 = 4 * t;
+    if (i0 >= n) return;
+    if (i0 + 4 <= n) {
+        const int64_t gi = a.grad_stride == 8 ? i0 : (i0 >> 3) * a.grad_stride + (i0 & 7);
+        float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + gi), m = *(float4*)(m_ + i0), v = *(float4*)(v_ + i0);
+        adam_one(p.x, g.x, m.x, v.x, a);
+        adam_one(p.y, g.y, m.y, v.y, a);
+        adam_one(p.z, g.z, m.z, v.z, a);
+        adam_one(p.w, g.w, m.w, v.w, a);
+        *(float4*)(prm + i0) = p;
+        *(float4*)(m_ + i0) = m;
+        *(float4*)(v_ + i0) = v;
+        if (a.zero_grad) *(float4*)(grad + gi) = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    for (int64_t i = i0; i < n; ++i) {   // tail (contiguous layout only: strided needs n % 8 == 0)
+        float p = prm[i], m = m_[i], v = v_[i];
+        adam_one(p, grad[i], m, v, a);
+        prm[i] = p;
+        m_[i] = m;
+        v_[i] = v;
+        if (a.zero_grad) grad[i] = 0.f;
+    }
 }
 
 }  // namespace
@@ -365,6 +394,7 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     if (!pts || !mlp || !cfg || !st || !coord || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
     if ((!hash && !grid) || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (cfg->grad_stride != 8 && cfg->grad_stride != 16) return PIN_ERR_ARG;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     auto s = as_stream(stream);
@@ -391,6 +421,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
                        double* loss_out, void* stream) {
     if (!pts || !mlp || !cfg || !st || !label || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (cfg->grad_stride != 8 && cfg->grad_stride != 16) return PIN_ERR_ARG;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     if ((loss_out || mlp_grad) && !workspace) return PIN_ERR_ARG;
@@ -418,9 +449,11 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
                   void* stream) {
     if (!a || n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq))) return PIN_ERR_ARG;
+    if (a->grad_stride != 8 && (a->grad_stride < 8 || n % 8)) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
-    hipLaunchKernelGGL(k_adam, grid_for(n), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg, exp_avg_sq, n,
-                       *a);
+    if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_adam, grid_for((n + 3) / 4), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg,
+                       exp_avg_sq, n, *a);
     return launch_status();
 }
 

@@ -21,8 +21,7 @@ from .mesher import Mesher
 from .neural_points import NeuralPoints
 from .tracker import Tracker
 
-MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "_sync_side_effects", "sdf",
-                  "get_numerical_gradient")
+MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient")
 TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
 MESHER_METHODS = ("query_points",)
 

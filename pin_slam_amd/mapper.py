@@ -15,7 +15,9 @@ Data parallel: with a process group of W > 1 ranks, every
 its own batch, the per-rank gradients are scaled by 1/W inside the backward and SUM
 all-reduced (RCCL over xGMI on ROCm), so every rank applies the same Adam step to its replica
 of the map.  Certainty deltas (SUM) and ts_update (MAX) are reconciled once at the end of
-mapping(): nothing inside an iteration reads them.
+mapping(): nothing inside an iteration reads them.  (train_step also accepts [L+1,16]
+gradient rows that carry the certainty delta in lane 8 -- measured slower than 32-B rows plus
+certainty atomics, so mapping() uses the latter.)
 
 ``sdf`` and ``get_numerical_gradient`` mirror utils/mapper.py:670-733 on the autograd-capable
 drop-in query_feature for callers outside the fused loop.
@@ -166,7 +168,6 @@ class Mapper:
         if self.train_less:
             iter_count = max(1, iter_count - 5)
         self._check_supported()
-        c = self.config
         nm = self.neural_points
         feats = nm.local_geo_features
         _lib.require_device(feats.data)
@@ -176,11 +177,14 @@ class Mapper:
             raise NotImplementedError("fused mapping trains the whole 11->64->1 decoder or none of it")
         world = self._world()
         dev = feats.device
-        # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441)
+        # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441).  The gradient
+        # is a plain [L+1,8] buffer (32-B rows: the cheapest atomic shape measured); the forward
+        # applies the certainty side effect itself.
         fdata = feats.data
         f_grad = torch.zeros_like(fdata)
         f_m = torch.zeros_like(fdata)
         f_v = torch.zeros_like(fdata)
+        m_grad = m_m = m_v = None
         if train_mlp:
             m_grad = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
             m_m = torch.zeros_like(m_grad)
@@ -191,12 +195,14 @@ class Mapper:
             coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
             if self.ba_done_flag:
                 coord = transform_batch_torch(coord, self.used_poses[ts])
-            self.train_step(coord, sdf_label, ts, f_grad, m_grad if train_mlp else None, world)
-            self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad if train_mlp else None,
-                       m_m if train_mlp else None, m_v if train_mlp else None)
+            self.train_step(coord, sdf_label, ts, f_grad, m_grad, world)
+            self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
             self.total_iter += 1
         if world > 1:
-            self._sync_side_effects(cert_before)
+            cert = nm.local_point_certainties
+            cert_delta = cert - cert_before
+            sync_side_effects(cert_delta, nm.local_point_ts_update, getattr(self, "group", None))
+            cert.copy_(cert_before + cert_delta)
         nm.assign_local_to_global()
 
     def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1):
@@ -209,6 +215,9 @@ class Mapper:
         label = sdf_label.detach().to(torch.float32).contiguous()
         ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
         n = q.shape[0]
+        stride = int(grad_features.shape[1]) if grad_features is not None else 8
+        if stride not in (8, 16) or (grad_features is not None and not grad_features.is_contiguous()):
+            raise ValueError("grad_features must be a contiguous [L+1, 8] or [L+1, 16] float32 tensor")
         dec = int(c.gradient_decimation)
         eik = bool(c.ekional_loss_on and c.weight_e > 0)
         nd = (n + dec - 1) // dec if eik else 0
@@ -221,7 +230,7 @@ class Mapper:
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
                                sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
-                               grad_scale=float(np.float32(1.0 / world)), reserved=0)
+                               grad_scale=float(np.float32(1.0 / world)), grad_stride=stride)
         hv, pv = nm._views("local", True)
         st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
@@ -251,8 +260,9 @@ class Mapper:
         self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
+        sf = adam_scalars(c.lr, self._adam_t, c.adam_eps, grad_stride=int(f_grad.shape[1]))
         _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
-                  ctypes.byref(st), s)
+                  ctypes.byref(sf), s)
         if m_grad is not None:
             off = 0
             for p in mlp_params:
@@ -264,10 +274,6 @@ class Mapper:
                           _lib.ptr(m_v[off:off + k]), k, ctypes.byref(st), s)
                 off += k
 
-    def _sync_side_effects(self, cert_before):
-        nm = self.neural_points
-        sync_side_effects(nm.local_point_certainties, cert_before, nm.local_point_ts_update,
-                          getattr(self, "group", None))
 
     # ---------------------------------------------------------------- autograd helpers
     def sdf(self, x, get_std=False):
@@ -307,26 +313,31 @@ class Mapper:
 
 def allreduce_gradients(grads, group=None):
     """SUM all-reduce of the per-rank gradients (already scaled by 1/world in the backward, so
-    the sum is the gradient of the mean loss over the union of the ranks' batches)."""
+    the sum is the gradient of the mean loss over the union of the ranks' batches).  A [L+1,16]
+    accumulator exchanges only its gradient lanes 0..7 (packed, 128 MB at 4M points)."""
     for g in grads:
-        if g is not None:
+        if g is None:
+            continue
+        if g.dim() == 2 and g.shape[1] == 16:
+            packed = g[:, :8].contiguous()
+            dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+            g[:, :8].copy_(packed)
+        else:
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
 
 
-def sync_side_effects(cert, cert_before, ts_update, group=None):
-    """Training-mode side effects of a data-parallel mapping() call: certainty deltas add up
-    across ranks (scatter_add_, neural_points.py:640), ts_update takes the max (:644)."""
-    delta = cert - cert_before
-    dist.all_reduce(delta, op=dist.ReduceOp.SUM, group=group)
-    cert.copy_(cert_before + delta)
+def sync_side_effects(cert_delta, ts_update, group=None):
+    """Training-mode side effects of a data-parallel mapping() call: the ranks' certainty deltas
+    add up (scatter_add_, neural_points.py:640) and ts_update takes the max (:644)."""
+    dist.all_reduce(cert_delta, op=dist.ReduceOp.SUM, group=group)
     dist.all_reduce(ts_update, op=dist.ReduceOp.MAX, group=group)
 
 
-def adam_scalars(lr, step, eps, beta1=0.9, beta2=0.99, zero_grad=True) -> "_lib.PinAdamStep":
+def adam_scalars(lr, step, eps, beta1=0.9, beta2=0.99, zero_grad=True, grad_stride=8) -> "_lib.PinAdamStep":
     """Scalars torch.optim.Adam (single-tensor) derives per step, cast to float32 as its kernels do."""
     bc1 = 1 - beta1 ** step
     bc2 = 1 - beta2 ** step
     return _lib.PinAdamStep(neg_step_size=float(np.float32(-(lr / bc1))), one_minus_beta1=float(np.float32(1 - beta1)),
                             beta2=float(np.float32(beta2)), one_minus_beta2=float(np.float32(1 - beta2)),
                             bias_correction2_sqrt=float(np.float32(bc2 ** 0.5)), eps=float(np.float32(eps)),
-                            zero_grad=int(zero_grad), reserved=0)
+                            zero_grad=int(zero_grad), grad_stride=int(grad_stride))

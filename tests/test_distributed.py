@@ -55,9 +55,16 @@ def _worker(rank, world, port, case, q):
         fg_t = torch.from_numpy(fg / world)
         mg_t = torch.from_numpy(mg / world)
         allreduce_gradients([fg_t, mg_t, None])
-        cert_t = torch.from_numpy(cert.astype(np.float32))
+        # gradients in the mapper's 64-B accumulator rows (lanes 0..7; lane 8 = certainty delta)
+        acc = torch.zeros((fg.shape[0], 16), dtype=torch.float64)
+        acc[:, :8] = torch.from_numpy(fg / world)
+        acc[:-1, 8] = torch.from_numpy((cert - cert0).astype(np.float64))
+        allreduce_gradients([acc])
+        assert torch.equal(acc[:, :8], fg_t), "packed lanes must reduce like the plain gradient"
+        cert_delta = acc[:-1, 8].contiguous()
         ts_t = torch.from_numpy(ts.astype(np.int64))
-        sync_side_effects(cert_t, torch.from_numpy(cert0.astype(np.float32)), ts_t)
+        sync_side_effects(cert_delta, ts_t)
+        cert_t = torch.from_numpy(cert0.astype(np.float64)) + cert_delta
         lt = torch.tensor([loss / world], dtype=torch.float64)
         dist.all_reduce(lt)
         tm = torch.tensor([1.0 + rank], dtype=torch.float64)

@@ -125,6 +125,25 @@ def test_mapping_call_fixture(golden, dev, backend, case, monkeypatch):
                                    err_msg=key)
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_train_step_folded_certainty(golden, dev, case):
+    """64-B gradient rows (grad_stride 16, what mapping() uses): lanes 0..7 hold the feature
+    gradient and lane 8 the certainty side effect; certainties themselves stay untouched."""
+    z = golden(case)
+    nm, dec, mapper = _setup(z, dev, "grid")
+    cert0 = nm.local_point_certainties.clone()
+    acc = torch.zeros((nm.local_geo_features.shape[0], 16), dtype=torch.float32, device=dev)
+    coord = torch.as_tensor(z["it0_coord"], device=dev)
+    label = torch.as_tensor(z["it0_label"], device=dev)
+    ts = torch.as_tensor(z["it0_ts"], device=dev)
+    mapper.train_step(coord, label, ts, acc)
+    assert torch.equal(nm.local_point_certainties, cert0)
+    np.testing.assert_allclose(_np(acc[:, :8]), z["it0_feat_grad"], rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(_np(cert0 + acc[:-1, 8]), z["it0_cert_after"], rtol=1e-5, atol=1e-4)
+    assert float(acc[:, 9:].abs().max()) == 0.0
+    np.testing.assert_array_equal(_np(nm.local_point_ts_update), z["it0_ts_after"])
+
+
 def test_frozen_decoder_trains_features_only(golden, dev):
     """Decoder frozen (freeze_model, utils/tools.py:186-191, after freeze_after_frame): the
     decoder parameters stay bit-identical and the features still move."""
