@@ -5,8 +5,8 @@ Workload (BASELINE.json configs[1]): synthetic 1M-point
 surface map (1000 x 1000 voxels of 0.3 m, hash table B = 5e7), 262,144 queries
 per step = map points + N(0, 0.25^2), Kc = 33 cells (num_nei_cells 2, alpha 0.2),
 k = 8, F = 8, decoder 11 -> 64 -> 1, weighted_first, fp32, query_locally=False.
-One step = one fused HIP launch (pin_query_sdf) over the batch, inputs resident
-in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
+One step = Tracker/Mesher's fused query over the batch (pin_query_order: a tile-grouped
+processing order, then one pin_query_sdf_grid launch), inputs resident in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
 batch against its replica of the map ("weak" scaling, no data-path collective);
 the barrier + max-over-ranks timing is the only collective.
 
@@ -16,7 +16,8 @@ RCCL when N > 1 (see mapper_leg).
 
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
-mean kernel time from HIP events on the launch stream.  cpu_baseline: the numpy oracle
+mean duration of the SDF+grad kernel alone (HIP events on the launch stream around
+pin_query_sdf_grid with the order precomputed); the ordering pass is reported beside it.  cpu_baseline: the numpy oracle
 (oracle/pin_oracle.py, single thread) on one full batch, rank 0 at N=1 only.
 """
 import argparse
@@ -78,6 +79,9 @@ def parse():
     ap.add_argument("--nwf", action="store_true", help="weighted_first=False variant (per-neighbour decoding)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hash", "grid"])
     ap.add_argument("--no-mapper", action="store_true", help="skip the mapper leg (configs[3])")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL on ROCm; gloo only to rehearse N ranks on "
+                         "fewer GPUs -- ranks then share devices round robin)")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -104,6 +108,49 @@ def cpu_baseline(nm, dec, q, wf):
     return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": 1, "kind": "port",
             "sample": f"one full {qh.shape[0]}-query batch over the same 1M-point map, numpy oracle "
                       f"single-threaded, median of 3 ({t:.2f} s each)"}
+
+
+def time_kernel(nm, dec, q, wf, backend, steps):
+    """Mean duration (ms) of the headline kernel alone -- HIP events on the launch stream around
+    each pin_query_sdf(_grid) launch, with the tile order precomputed -- and of the ordering pass
+    (pin_query_order) that each step also runs."""
+    import ctypes  # noqa: F401
+    from pin_slam_amd import _lib
+    from pin_slam_amd.query import mlp_view, query_order
+    n = q.shape[0]
+    hv, pv = nm._views("global", False)
+    mv = mlp_view(dec)
+    sdf = torch.empty(n, device=q.device)
+    grad = torch.empty((n, 3), device=q.device)
+    nn = torch.empty(n, dtype=torch.int32, device=q.device)
+    std = None if wf else torch.empty(n, device=q.device)
+    if backend == "grid":
+        gv = nm.grid_view("global", True)
+        order = query_order(gv, q)
+
+        def launch():
+            _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0,
+                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.ptr(order),
+                      _lib.stream())
+
+        def order_pass():
+            query_order(gv, q)
+    else:
+        def launch():
+            _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0, _lib.ptr(sdf),
+                      _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
+        order_pass = None
+
+    def mean_ms(fn):
+        fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in ev:
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        return statistics.mean(a.elapsed_time(b) for a, b in ev)
+    return mean_ms(launch), (mean_ms(order_pass) if order_pass else 0.0)
 
 
 def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
@@ -147,6 +194,7 @@ def mapper_leg(args, dev, world, rank):
         p.requires_grad_(False)
     coord, label, ts = surface_pool(pts, MAPPER_POOL, seed=11 + rank, device=dev)
     mapper = P.Mapper(nm.config, None, nm, dec, group=dist.group.WORLD if world > 1 else None)
+    L = int(nm.local_neural_points.shape[0])
     mapper.set_pool(coord, label, ts)
     torch.manual_seed(1234 + rank)
     backend = nm.backend()
@@ -164,7 +212,6 @@ def mapper_leg(args, dev, world, rank):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
-    L = int(nm.local_neural_points.shape[0])
     bpi = mapper_bytes_per_iter(MAPPER_BS, L)
     ms = elapsed / args.mapper_steps * 1e3
     res = {"metric": "mapper iters/sec", "value": args.mapper_steps / elapsed, "unit": "iters/s",
@@ -173,7 +220,8 @@ def mapper_leg(args, dev, world, rank):
            "config": {"workload": "Mapper.mapping, 4M-point map, 1M queries/iter/GPU + numerical-gradient "
                                   "stencil (configs[3])", "map_points": int(pts.shape[0]),
                       "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",
-                      "grad_allreduce": "RCCL SUM, 128 MB/iter" if world > 1 else None,
+                      "grad_allreduce": (f"{dist.get_backend()} all_reduce SUM of the [L+1,8] f32 gradient "
+                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter)") if world > 1 else None,
                       "candidate_backend": backend, "timed": "mapping(K): K iterations + Adam state init + "
                                                              "assign_local_to_global"},
            "roofline": {"bound": "hbm", "achieved": bpi / (ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
@@ -192,11 +240,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = f"cuda:{local_rank}"
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local_rank >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local_rank} but only {ndev} visible GPU(s)")
+    dev_index = local_rank % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    dev = f"cuda:{dev_index}"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(dev))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(dev))
+        else:
+            dist.init_process_group("gloo")
     wf = not args.nwf
     nm, dec, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf,
                                query_backend=args.backend)
@@ -220,23 +275,19 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        starts[i].record()
         step()
-        ends[i].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = statistics.mean(s.elapsed_time(e) for s, e in zip(starts, ends))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps)
+    t = torch.tensor([elapsed, kern_ms, order_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms, order_ms = float(t[0]), float(t[1]), float(t[2])
     total_q = N_QUERY * args.steps * world
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
@@ -266,6 +317,7 @@ def main():
                      "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
                                        "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
                      "kernel": "k_query_sdf_grid" if backend == "grid" else "k_query_sdf", "kernel_ms": kern_ms,
+                     "order_pass_ms": order_ms,
                      "algorithmic_bytes_per_query": BYTES_PER_QUERY},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -241,24 +241,27 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
                   const float* features, const float* certainties, float* crec, float* cfeat, float* ccert,
                   int32_t* cgid, void* stream);
 
-/* Query bins of a grid box: 8x8x8 cells (2x2x2 bricks) each. */
-static inline int64_t pin_query_bins(const PinGridDims* d) {
-    return (int64_t)((d->nbx + 1) / 2) * ((d->nby + 1) / 2) * ((d->nbz + 1) / 2);
-}
-/* Workspace bytes of pin_query_sdf_grid's binned form for n queries. */
-static inline int64_t pin_query_workspace_bytes(int64_t n, const PinGridDims* d) {
-    return 4 * (pin_query_bins(d) + 2 * n);
+/* Workspace bytes of pin_query_order for n queries. */
+static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
+    return 4 * 1024 * ((n + 8191) / 8192 + 1);
 }
 
 /*
- * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  workspace NULL:
- * queries are processed in input order.  Otherwise (pin_query_workspace_bytes(n, &grid->dims)
- * bytes) they are first counting-sorted into 8x8x8-cell bins and processed bin by bin (better
- * line sharing for random batches); outputs are identical and stay at each query's index.
+ * pin_query_order -- a processing order for a random query batch: order[0..n) is a permutation
+ * of the query indices grouped into <= 1024 spatial tiles of the grid box (one radix pass, two
+ * launches, no global atomics).  Feeding it to pin_query_sdf_grid gives better line sharing
+ * and per-XCD L2 locality; results do not depend on the order.
+ */
+int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* order, void* workspace, void* stream);
+
+/*
+ * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  order (n ints,
+ * may be NULL = input order): the order in which queries are processed (pin_query_order);
+ * outputs always go to each query's own index.
  */
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
                        int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
-                       int32_t* nn_count, float* certainty, float* sdf_std, void* workspace, void* stream);
+                       int32_t* nn_count, float* certainty, float* sdf_std, const int32_t* order, void* stream);
 
 /* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
  * (features always read live from pts->features; gids from grid->cgid). */

@@ -102,6 +102,7 @@ _SIGS = {
                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "pin_device.h"
@@ -352,58 +353,155 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
     query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
 }
 
-// Query binning (counting sort by 8x8x8-cell bins of the grid box): random batches are
-// processed bin by bin so that a block's gathers share lines and, with xcd_block(), each XCD's
-// L2 sees one region of the map.  Outputs still go to each query's own index.
-__device__ __forceinline__ int query_bin(const float* __restrict__ q, int64_t i, const PinGrid& g) {
-    const float res = g.resolution;
-    const int bx = (g.dims.nbx + 1) >> 1, by = (g.dims.nby + 1) >> 1, bz = (g.dims.nbz + 1) >> 1;
-    auto axis = [&](float v, int64_t o, int nb) -> int {
-        int64_t c = ((int64_t)floorf(v / res) - o) >> 3;
-        return (int)(c < 0 ? 0 : (c >= nb ? nb - 1 : c));
+// Query tiling: one radix-partition pass of the queries into <= 1024 spatial tiles of the grid
+// box (cubes of 2^shift cells; the host picks the smallest shift >= 3 with <= 1024 tiles).
+// Random batches are then processed tile by tile: a block's gathers share lines and, with
+// xcd_block(), each XCD's L2 holds one region of the map (random 262K-query batch on a 1M map:
+// 104 -> 65 us for the SDF+grad kernel).  Order inside a tile is arbitrary; every query's
+// outputs still go to its own index, so results are unchanged.
+constexpr int kMaxTiles = 1024;
+constexpr int kPartThreads = 1024;   // one thread per tile in the scatter's prefix step
+
+struct TileMap {
+    int64_t ox, oy, oz;
+    float inv_res;   // ordering only: a reciprocal is fine here
+    int shift, ntx, nty, ntz, ntiles;
+};
+
+__device__ __forceinline__ int tile_of(float x, float y, float z, const TileMap& t) {
+    auto axis = [&](float v, int64_t o, int nt) -> int {
+        const int64_t c = ((int64_t)floorf(v * t.inv_res) - o) >> t.shift;
+        return (int)(c < 0 ? 0 : (c >= nt ? nt - 1 : c));
     };
-    const int cx = axis(q[3 * i], g.dims.ox, bx);
-    const int cy = axis(q[3 * i + 1], g.dims.oy, by);
-    const int cz = axis(q[3 * i + 2], g.dims.oz, bz);
-    return (cz * by + cy) * bx + cx;
+    return (axis(z, t.oz, t.ntz) * t.nty + axis(y, t.oy, t.nty)) * t.ntx + axis(x, t.ox, t.ntx);
 }
 
-__global__ void __launch_bounds__(kBlock)
-k_bin_count(const float* __restrict__ q, int64_t n, const PinGrid g, int* __restrict__ hist, int* __restrict__ rank) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    rank[i] = atomicAdd(hist + query_bin(q, i, g), 1);
+// the PER queries of one thread: all coordinate loads first, then the tiles
+template <int PER>
+__device__ __forceinline__ void load_tiles(const float* __restrict__ q, int64_t n, const TileMap& t, int (&tile)[PER]) {
+    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + threadIdx.x;
+    float x[PER], y[PER], z[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int64_t i = lo + (int64_t)u * kPartThreads;
+        const int64_t j = i < n ? i : 0;
+        x[u] = q[3 * j];
+        y[u] = q[3 * j + 1];
+        z[u] = q[3 * j + 2];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) tile[u] = lo + (int64_t)u * kPartThreads < n ? tile_of(x[u], y[u], z[u], t) : -1;
 }
 
-// in-place exclusive scan of nb counts, one block of 1024 threads (bins per thread contiguous)
-__global__ void __launch_bounds__(1024) k_bin_scan(int* __restrict__ hist, int nb) {
-    __shared__ int part[1024];
-    const int per = (nb + 1023) / 1024;
-    const int lo = threadIdx.x * per, hi = min(nb, lo + per);
-    int s = 0;
-    for (int k = lo; k < hi; ++k) s += hist[k];
-    part[threadIdx.x] = s;
+// per-block tile histogram (LDS atomics) -> cnt[block][tile] (one coalesced row)
+template <int PER>
+__global__ void __launch_bounds__(kPartThreads)
+k_part_count(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ cnt) {
+    __shared__ int h[kMaxTiles];
+    for (int k = threadIdx.x; k < t.ntiles; k += kPartThreads) h[k] = 0;
+    int tile[PER];
+    load_tiles<PER>(q, n, t, tile);
     __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    int run = part[threadIdx.x] - s;
-    for (int k = lo; k < hi; ++k) {
-        const int c = hist[k];
-        hist[k] = run;
-        run += c;
-    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+        if (tile[u] >= 0) atomicAdd(h + tile[u], 1);
+    __syncthreads();
+    for (int k = threadIdx.x; k < t.ntiles; k += kPartThreads) cnt[(int64_t)blockIdx.x * t.ntiles + k] = h[k];
 }
 
-__global__ void __launch_bounds__(kBlock)
-k_bin_scatter(const float* __restrict__ q, int64_t n, const PinGrid g, const int* __restrict__ off,
-              const int* __restrict__ rank, int* __restrict__ order) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    order[off[query_bin(q, i, g)] + rank[i]] = (int)i;
+// Each block reads the whole count matrix: thread k sums tile k's column (all blocks, and the
+// blocks before this one), a 1024-wide scan of the column totals gives the tile bases, and the
+// block's queries are placed at base + LDS-atomic rank.  No separate scan launch.
+template <int PER>
+__global__ void __launch_bounds__(kPartThreads)
+k_part_scatter(const float* __restrict__ q, int64_t n, TileMap t, const int* __restrict__ cnt, int nblk,
+               int* __restrict__ order) {
+    __shared__ int base[kMaxTiles];
+    __shared__ int wsum[kPartThreads / 64];
+    int tile[PER];
+    load_tiles<PER>(q, n, t, tile);
+    const int k = threadIdx.x;
+    int pre = 0, tot = 0;
+    if (k < t.ntiles) {
+        int b = 0;
+        for (; b + 4 <= nblk; b += 4) {
+            int v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = cnt[(int64_t)(b + u) * t.ntiles + k];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                tot += v[u];
+                pre += b + u < (int)blockIdx.x ? v[u] : 0;
+            }
+        }
+        for (; b < nblk; ++b) {
+            const int v = cnt[(int64_t)b * t.ntiles + k];
+            tot += v;
+            pre += b < (int)blockIdx.x ? v : 0;
+        }
+    }
+    int incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(incl, o);
+        if ((k & 63) >= o) incl += x;
+    }
+    if ((k & 63) == 63) wsum[k >> 6] = incl;
+    __syncthreads();
+    int tb = incl - tot;
+    for (int w = 0; w < (k >> 6); ++w) tb += wsum[w];
+    if (k < t.ntiles) base[k] = tb + pre;
+    __syncthreads();
+    int pos[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) pos[u] = tile[u] >= 0 ? atomicAdd(base + tile[u], 1) : -1;
+    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+        if (pos[u] >= 0) order[pos[u]] = (int)(lo + (int64_t)u * kPartThreads);
+}
+
+// host: tile map of a grid box
+TileMap tile_map(const PinGrid& g) {
+    TileMap t;
+    t.ox = g.dims.ox;
+    t.oy = g.dims.oy;
+    t.oz = g.dims.oz;
+    t.inv_res = 1.0f / g.resolution;
+    const int64_t ex = 4ll * g.dims.nbx, ey = 4ll * g.dims.nby, ez = 4ll * g.dims.nbz;
+    int sh = 3;
+    for (;; ++sh) {
+        const int64_t nx = (ex + (1ll << sh) - 1) >> sh, ny = (ey + (1ll << sh) - 1) >> sh,
+                      nz = (ez + (1ll << sh) - 1) >> sh;
+        if (nx * ny * nz <= kMaxTiles) {
+            t.ntx = (int)nx;
+            t.nty = (int)ny;
+            t.ntz = (int)nz;
+            break;
+        }
+    }
+    t.shift = sh;
+    t.ntiles = t.ntx * t.nty * t.ntz;
+    return t;
+}
+
+// order[0..n) = the queries grouped by tile; workspace = pin_query_order_workspace_bytes(n).  8 queries
+// per thread (32 blocks at 256K queries) up to 512K queries, 16 per thread beyond, so the count
+// matrix each scatter block reads stays small (~100 rows at 1.6M).
+int partition_queries(const PinGrid& g, const float* q, int64_t n, void* workspace, hipStream_t s, int*& order,
+                      int* out) {
+    const TileMap t = tile_map(g);
+    order = out;
+    int* cnt = (int*)workspace;
+    if (n <= (int64_t)64 * 8 * kPartThreads) {
+        const int nblk = (int)((n + 8 * kPartThreads - 1) / (8 * kPartThreads));
+        hipLaunchKernelGGL(k_part_count<8>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
+        hipLaunchKernelGGL(k_part_scatter<8>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
+    } else {
+        const int nblk = (int)((n + 16 * kPartThreads - 1) / (16 * kPartThreads));
+        hipLaunchKernelGGL(k_part_count<16>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
+        hipLaunchKernelGGL(k_part_scatter<16>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
+    }
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 
 // ------------------------------------------------------------------ drop-in query_feature
@@ -745,9 +843,16 @@ static bool grid_ok(const PinGrid* g) {
            g->dims.nbx > 0 && g->dims.nby > 0 && g->dims.nbz > 0 && (!g->fat || (g->cfeat && g->ccert));
 }
 
+int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* order, void* workspace, void* stream) {
+    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !order || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    int* o = nullptr;
+    return partition_queries(*grid, q, n, workspace, as_stream(stream), o, (int*)order);
+}
+
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
                        int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
-                       int32_t* nn_count, float* certainty, float* sdf_std, void* workspace, void* stream) {
+                       int32_t* nn_count, float* certainty, float* sdf_std, const int32_t* order, void* stream) {
     if (!grid_ok(grid) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
         return PIN_ERR_ARG;
     const bool fat = grid->fat != 0;
@@ -759,20 +864,9 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
     const bool g = grad != nullptr;
     const bool pgo = pts->after_pgo != 0;
     auto s = as_stream(stream);
-    int* order = nullptr;
-    if (workspace) {
-        const int nbins = (int)pin_query_bins(&grid->dims);
-        int* hist = (int*)workspace;
-        int* rank = hist + nbins;
-        order = rank + n;
-        if (hipMemsetAsync(hist, 0, (size_t)nbins * sizeof(int), s) != hipSuccess) return PIN_ERR_HIP;
-        hipLaunchKernelGGL(k_bin_count, grid_for(n), dim3(kBlock), 0, s, q, n, *grid, hist, rank);
-        hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, hist, nbins);
-        hipLaunchKernelGGL(k_bin_scatter, grid_for(n), dim3(kBlock), 0, s, q, n, *grid, hist, rank, order);
-    }
 #define PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT)                                                                     \
     hipLaunchKernelGGL((k_query_sdf_grid<WF, PGO, GRAD, FAT>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, *mlp, \
-                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std, order)
+                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std, (const int*)order)
 #define PIN_SDFG_FAT(WF, PGO, GRAD) \
     do { if (fat) PIN_LAUNCH_SDFG(WF, PGO, GRAD, true); else PIN_LAUNCH_SDFG(WF, PGO, GRAD, false); } while (0)
     if (weighted_first) {

@@ -10,11 +10,9 @@ from torch.autograd.function import once_differentiable
 
 from . import _lib
 
-# counting-sort queries into spatial bins before the grid SDF query (PIN_QUERY_BIN=1 enables):
-# the binned kernel is ~20% faster on random batches, but the three extra launches cost more
-# than that at 262K queries (tools/prof_bin.sh), so it is off by default
-_BIN_QUERIES = os.environ.get("PIN_QUERY_BIN", "0") == "1"
-_BIN_MIN = 65536   # below this the sort's launches cost more than the locality returns
+# partition queries into spatial tiles before the grid SDF query (PIN_QUERY_TILES=0 disables)
+_TILE_QUERIES = os.environ.get("PIN_QUERY_TILES", "1") != "0"
+_TILE_MIN = 65536  # below this the partition's two launches cost more than the locality returns
 
 
 class _View:
@@ -123,6 +121,15 @@ class QueryFeatureFn(torch.autograd.Function):
         return grad_q, grad_f, None, None, None, None, None
 
 
+def query_order(gv, q):
+    """pin_query_order: a tile-grouped processing order for the queries q [N,3] (device int32)."""
+    n = q.shape[0]
+    order = torch.empty((n,), dtype=torch.int32, device=q.device)
+    ws = torch.empty((1024 * ((n + 8191) // 8192 + 1),), dtype=torch.int32, device=q.device)
+    _lib.call("pin_query_order", gv.ref(), _lib.ptr(q), n, _lib.ptr(order), _lib.ptr(ws), _lib.stream())
+    return order
+
+
 def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
               want_certainty=True, nn_k=None, weighted_first=None):
     """Fused query_feature + Decoder.sdf (+ analytic dSDF/dq) in one kernel.
@@ -146,13 +153,9 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
     if nm.backend() == "grid":
         gv = nm.grid_view(mode, True)
-        ws = None
-        if _BIN_QUERIES and n >= _BIN_MIN:
-            d = gv.struct.dims
-            nbins = ((d.nbx + 1) // 2) * ((d.nby + 1) // 2) * ((d.nbz + 1) // 2)
-            ws = torch.empty((nbins + 2 * n,), dtype=torch.int32, device=dev)
+        order = query_order(gv, q) if (_TILE_QUERIES and n >= _TILE_MIN) else None
         _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
-                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.ptr(ws),
+                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.ptr(order),
                   _lib.stream())
     else:
         _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),

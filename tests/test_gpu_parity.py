@@ -248,6 +248,32 @@ def test_random_map_vs_oracle(dev, wf, backend):
     np.testing.assert_allclose(_np(w)[..., 0], oq.weights, rtol=2e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("wf", [True, False])
+def test_query_order_is_a_permutation_and_invisible(dev, wf):
+    """pin_query_order groups a random batch by spatial tile; pin_query_sdf_grid's outputs are
+    bitwise identical with and without it (the order only changes which lane runs a query)."""
+    from pin_slam_amd import _lib
+    from pin_slam_amd.query import mlp_view, query_order
+    nm, dec, pts = H.surface_map(300, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend="grid")
+    q = H.surface_queries(pts, 70001, device=dev)
+    gv = nm.grid_view("global", True)
+    order = query_order(gv, q)
+    assert torch.equal(torch.sort(order.long())[0], torch.arange(q.shape[0], device=dev))
+    hv, pv = nm._views("global", False)
+    mv = mlp_view(dec)
+    outs = []
+    for o in (None, order):
+        sdf = torch.empty(q.shape[0], device=dev)
+        grad = torch.empty((q.shape[0], 3), device=dev)
+        nn = torch.empty(q.shape[0], dtype=torch.int32, device=dev)
+        std = torch.empty(q.shape[0], device=dev)
+        _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), q.shape[0], 8, int(wf), 0,
+                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.ptr(o), _lib.stream())
+        outs.append((sdf, grad, nn, std))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_backend_selection(golden, dev):
     """The grid is used only when it is exact: after adjust_map (points moved, table not
     rebuilt) the table holds entries off their own voxel and the hash path must be taken."""

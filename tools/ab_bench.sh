@@ -8,7 +8,7 @@ if [ -z "$NO_TESTS" ]; then
 fi
 for split in 1 0; do  # PIN_QUERY_BIN
 for v in window cells; do
-    PIN_QUERY_BIN=$split PIN_GRID_SCAN=$v timeout -k 10 300 python bench.py --no-mapper --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_${split}_$v.json 2>gpurun_out/ab_${split}_$v.err || exit 1
-    python3 -c "import json;d=json.load(open('gpurun_out/ab_${split}_$v.json'));print('bin=$split $v', round(d['value']/1e9,3),'Gq/s kernel_ms', round(d['roofline']['kernel_ms'],4))"
+    PIN_QUERY_TILES=$split PIN_GRID_SCAN=$v timeout -k 10 300 python bench.py --no-mapper --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_${split}_$v.json 2>gpurun_out/ab_${split}_$v.err || exit 1
+    python3 -c "import json;d=json.load(open('gpurun_out/ab_${split}_$v.json'));print('tiles=$split $v', round(d['value']/1e9,3),'Gq/s kernel_ms', round(d['roofline']['kernel_ms'],4))"
 done
 done
