@@ -284,11 +284,7 @@ typedef struct PinTrainCfg {
     float weight_e;              /* eikonal weight (mapper.py:547) */
     float grad_scale;            /* multiplies loss and gradients: 1, or 1/world_size so that a SUM
                                     all-reduce of per-rank gradients is the gradient of the mean loss */
-    int32_t grad_stride;         /* floats per row of grad_features: 8 = plain [L+1,8] gradient (the
-                                    forward applies the certainty side effect with atomics); 16 = 64-B
-                                    rows {g0..g7, certainty delta, 0 x7}: the backward adds each
-                                    neighbour's weight to lane 8 in the same memory-side request as
-                                    its gradient and the forward leaves certainties alone */
+    int32_t reserved;
 } PinTrainCfg;
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
@@ -299,6 +295,8 @@ typedef struct PinTrainState {
     float* sdf;                  /* [rows] predicted sdf */
     float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL */
     int64_t* ts_update;          /* [L] amax with the main rows' ts (neural_points.py:644), may be NULL */
+    const int32_t* order;        /* [rows] processing order (pin_query_order over pin_train_rows), may be
+                                    NULL; ids/weights/x are stored per processing slot, sdf per row */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */
@@ -315,6 +313,9 @@ typedef struct PinAdamStep {
 
 /* decoder-parameter gradient layout of pin_train_backward's mlp_grad */
 #define PIN_MLP_GRAD_SIZE (PIN_HIDDEN_DIM * (PIN_FEATURE_DIM + 3) + 2 * PIN_HIDDEN_DIM + 1) /* W1,b1,W2,b2 */
+
+/* pin_train_rows -- coordinates [rows,3] of every row of one iteration (batch + stencil). */
+int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, void* stream);
 
 /*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping
@@ -335,7 +336,7 @@ static inline int64_t pin_train_workspace_bytes(int64_t rows) {
 /*
  * pin_train_backward -- gradient of  BCEWithLogits(sdf/sigma, sigmoid(label/sigma)) (mean)
  *   + weight_e * mean_k (|g_k| - 1)^2,  g_k = central differences of the stencil rows
- * (mapper.py:515-547) w.r.t. the local features (grad_features [L+1,grad_stride] += , may be NULL) and,
+ * (mapper.py:515-547) w.r.t. the local features (grad_features [L+1,8] += , may be NULL) and,
  * if mlp_grad != NULL, the decoder parameters (mlp_grad [PIN_MLP_GRAD_SIZE] += , summed in a
  * fixed order).  loss_out (1 double on the device, may be NULL) receives the loss.  workspace:
  * pin_train_workspace_bytes(rows) bytes, needed when loss_out or mlp_grad is non-NULL.

@@ -63,12 +63,12 @@ class PinMlp(ctypes.Structure):
 
 class PinTrainCfg(ctypes.Structure):
     _fields_ = [("n_main", i64), ("n_stencil", i64), ("decimation", i32), ("nn_k", i32), ("weighted_first", i32),
-                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("grad_stride", i32)]
+                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("reserved", i32)]
 
 
 class PinTrainState(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
-                ("certainties", c_void_p), ("ts_update", c_void_p)]
+                ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p)]
 
 
 class PinAdamStep(ctypes.Structure):
@@ -105,6 +105,7 @@ _SIGS = {
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_train_rows": [c_void_p, _P(PinTrainCfg), c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,

@@ -49,7 +49,9 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 template <bool WF, class Src>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
-                                                   PinTrainCfg c, int64_t r, PinTrainState st) {
+                                                   PinTrainCfg c, int64_t t, PinTrainState st) {
+    // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
+    const int64_t r = st.order ? st.order[t] : t;
     float qx, qy, qz;
     row_coord(coord, c, r, qx, qy, qz);
     TopK tk;
@@ -87,13 +89,13 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         const float w = valid && nn > 0 ? u[j] / S : 0.f;
         const float xj[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
         if (j < nn_k) {
-            st.ids[r * nn_k + j] = id;
-            st.weights[r * nn_k + j] = w;
+            st.ids[t * nn_k + j] = id;
+            st.weights[t * nn_k + j] = w;
         }
         if (valid) {
-            // training side effects (neural_points.py:640, :644); with 16-float gradient rows the
-            // certainty is added by the backward; ts: read first, the max is usually a no-op
-            if (st.certainties && c.grad_stride != 16) atomicAdd(st.certainties + id, w);
+            // training side effects (neural_points.py:640, :644); ts: read first, the max is
+            // usually a no-op
+            if (st.certainties) atomicAdd(st.certainties + id, w);
             if (qts >= 0 && st.ts_update && st.ts_update[id] < qts)
                 atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
         }
@@ -106,7 +108,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3);
             sdf = sdf + sk * w;  // sum_j sdf_j w_j (mapper.py:467-468)
             if (j < nn_k) {
-                float* xo = st.x + (r * nn_k + j) * 3;  // neighbour vectors for the backward
+                float* xo = st.x + (t * nn_k + j) * 3;  // neighbour vectors for the backward
                 xo[0] = v0;
                 xo[1] = v1;
                 xo[2] = v2;
@@ -117,7 +119,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         float gx[kD];
         sdf = mlp_sdf<false, 0, kD>(m, x, gx);
 #pragma unroll
-        for (int d = 0; d < kD; ++d) st.x[r * kD + d] = x[d];
+        for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
     }
     st.sdf[r] = sdf;
 }
@@ -128,10 +130,10 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[kWSize];
     const MlpW mw = stage_mlp(m, s_mlp);
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= c.n_main + 6 * c.n_stencil) return;
+    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    if (t >= c.n_main + 6 * c.n_stencil) return;
     const HashSource src(h, p);
-    train_forward_body<WF>(src, p, mw, coord, ts, c, r, st);
+    train_forward_body<WF>(src, p, mw, coord, ts, c, t, st);
 }
 
 template <bool WF>
@@ -140,10 +142,17 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[kWSize];
     const MlpW mw = stage_mlp(m, s_mlp);
+    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    if (t >= c.n_main + 6 * c.n_stencil) return;
+    const GridSource<false> src(g, p);
+    train_forward_body<WF>(src, p, mw, coord, ts, c, t, st);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_train_rows(const float* __restrict__ coord, PinTrainCfg c, float* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main + 6 * c.n_stencil) return;
-    const GridSource<false> src(g, p);
-    train_forward_body<WF>(src, p, mw, coord, ts, c, r, st);
+    row_coord(coord, c, r, out[3 * r], out[3 * r + 1], out[3 * r + 2]);
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
@@ -233,12 +242,13 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     __shared__ float s_mlp[kWSize];
     const MlpW mlpw = stage_mlp(m, s_mlp);
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
+    const int64_t row = live && st.order ? st.order[r] : r;          // the row it holds (sdf, label)
     const int nn_k = c.nn_k;
     const int wave = threadIdx.x >> 6;
     double loss = 0.0;
-    const float dsdf = live ? row_dsdf(c, st.sdf, label, r, loss) * c.grad_scale : 0.f;
+    const float dsdf = live ? row_dsdf(c, st.sdf, label, row, loss) * c.grad_scale : 0.f;
     loss *= (double)c.grad_scale;
     const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
     float* mw = MLP_GRAD ? mlds[wave] : nullptr;
@@ -296,25 +306,21 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         }
     }
     if (!grad_features) return;
-    // scatter: element e = (row, j, lane), lane fastest, L lanes per (row, neighbour): L = 8 for
-    // plain rows (a wave instruction covers 8 rows x 32 B), L = 9 for 64-B rows (lane 8 = the
-    // certainty; 7 rows per instruction).  One memory-side request per (row, neighbour).
+    // scatter: element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour)
+    // pairs x 32 contiguous bytes, one memory-side request each -- the cheapest atomic shape
+    // measured (LDS pre-aggregation per block, and 64-B rows carrying the certainty, were slower)
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int L = c.grad_stride == 16 ? kF + 1 : kF;
-    const int total = kBlock * nn_k * L;
+    const int total = kBlock * nn_k * kF;
     for (int e = threadIdx.x; e < total; e += kBlock) {
-        const int rj = e / L;
-        const int d = e - rj * L;
+        const int d = e & (kF - 1);
+        const int rj = e >> 3;
         const int lr = rj / nn_k, j = rj - lr * nn_k;
         const int64_t rr = row0 + lr;
         if (rr >= nrows) break;
         const int id = st.ids[rr * nn_k + j];
         if (id < 0) continue;
-        const float w = st.weights[rr * nn_k + j];
-        float g;
-        if (d == kF) g = w;   // certainty lane (64-B rows only)
-        else g = WF ? w * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
-        atomicAdd(grad_features + (int64_t)id * c.grad_stride + d, g);
+        const float g = WF ? st.weights[rr * nn_k + j] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }
 
@@ -388,13 +394,21 @@ k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_
 
 extern "C" {
 
+int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, void* stream) {
+    if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
+    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    if (rows == 0) return PIN_OK;
+    if (!coord || !rows_out) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_train_rows, grid_for(rows), dim3(kBlock), 0, as_stream(stream), coord, *cfg, rows_out);
+    return launch_status();
+}
+
 int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp,
                       const float* coord, const int64_t* ts, const PinTrainCfg* cfg, const PinTrainState* st,
                       void* stream) {
     if (!pts || !mlp || !cfg || !st || !coord || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
     if ((!hash && !grid) || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
-    if (cfg->grad_stride != 8 && cfg->grad_stride != 16) return PIN_ERR_ARG;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     auto s = as_stream(stream);
@@ -421,7 +435,6 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
                        double* loss_out, void* stream) {
     if (!pts || !mlp || !cfg || !st || !label || !st->ids || !st->weights || !st->x || !st->sdf) return PIN_ERR_ARG;
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
-    if (cfg->grad_stride != 8 && cfg->grad_stride != 16) return PIN_ERR_ARG;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     if ((loss_out || mlp_grad) && !workspace) return PIN_ERR_ARG;

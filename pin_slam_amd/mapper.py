@@ -15,9 +15,7 @@ Data parallel: with a process group of W > 1 ranks, every
 its own batch, the per-rank gradients are scaled by 1/W inside the backward and SUM
 all-reduced (RCCL over xGMI on ROCm), so every rank applies the same Adam step to its replica
 of the map.  Certainty deltas (SUM) and ts_update (MAX) are reconciled once at the end of
-mapping(): nothing inside an iteration reads them.  (train_step also accepts [L+1,16]
-gradient rows that carry the certainty delta in lane 8 -- measured slower than 32-B rows plus
-certainty atomics, so mapping() uses the latter.)
+mapping(): nothing inside an iteration reads them.
 
 ``sdf`` and ``get_numerical_gradient`` mirror utils/mapper.py:670-733 on the autograd-capable
 drop-in query_feature for callers outside the fused loop.
@@ -29,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .query import mlp_view
+from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_order
 
 
 def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -177,9 +175,7 @@ class Mapper:
             raise NotImplementedError("fused mapping trains the whole 11->64->1 decoder or none of it")
         world = self._world()
         dev = feats.device
-        # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441).  The gradient
-        # is a plain [L+1,8] buffer (32-B rows: the cheapest atomic shape measured); the forward
-        # applies the certainty side effect itself.
+        # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441)
         fdata = feats.data
         f_grad = torch.zeros_like(fdata)
         f_m = torch.zeros_like(fdata)
@@ -215,9 +211,8 @@ class Mapper:
         label = sdf_label.detach().to(torch.float32).contiguous()
         ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
         n = q.shape[0]
-        stride = int(grad_features.shape[1]) if grad_features is not None else 8
-        if stride not in (8, 16) or (grad_features is not None and not grad_features.is_contiguous()):
-            raise ValueError("grad_features must be a contiguous [L+1, 8] or [L+1, 16] float32 tensor")
+        if grad_features is not None and (grad_features.shape[1] != 8 or not grad_features.is_contiguous()):
+            raise ValueError("grad_features must be a contiguous [L+1, 8] float32 tensor")
         dec = int(c.gradient_decimation)
         eik = bool(c.ekional_loss_on and c.weight_e > 0)
         nd = (n + dec - 1) // dec if eik else 0
@@ -230,17 +225,26 @@ class Mapper:
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
                                sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
-                               grad_scale=float(np.float32(1.0 / world)), grad_stride=stride)
+                               grad_scale=float(np.float32(1.0 / world)), reserved=0)
         hv, pv = nm._views("local", True)
+        s = _lib.stream()
+        grid = nm.backend() == "grid"
+        gv = nm.grid_view("local", False) if grid else None
+        order = None
+        if grid and _TILE_QUERIES and rows >= _TILE_MIN:
+            # process the rows tile by tile (pin_query_order over the batch + stencil coordinates)
+            rows_xyz = torch.empty((rows, 3), dtype=torch.float32, device=q.device)
+            _lib.call("pin_train_rows", _lib.ptr(q), ctypes.byref(cfg), _lib.ptr(rows_xyz), s)
+            order = query_order(gv, rows_xyz)
+        self._order = order
         st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
-                                ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None)
+                                ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
+                                order=order.data_ptr() if order is not None else None)
         mv = mlp_view(self.geo_mlp)
         if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
             raise RuntimeError("local_geo_features must be a contiguous float32 tensor")
-        s = _lib.stream()
-        if nm.backend() == "grid":
-            gv = nm.grid_view("local", False)
+        if grid:
             _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), _lib.ptr(ts64),
                       ctypes.byref(cfg), ctypes.byref(st), s)
         else:
@@ -260,9 +264,8 @@ class Mapper:
         self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
-        sf = adam_scalars(c.lr, self._adam_t, c.adam_eps, grad_stride=int(f_grad.shape[1]))
         _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
-                  ctypes.byref(sf), s)
+                  ctypes.byref(st), s)
         if m_grad is not None:
             off = 0
             for p in mlp_params:

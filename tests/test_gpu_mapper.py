@@ -125,23 +125,32 @@ def test_mapping_call_fixture(golden, dev, backend, case, monkeypatch):
                                    err_msg=key)
 
 
-@pytest.mark.parametrize("case", CASES)
-def test_train_step_folded_certainty(golden, dev, case):
-    """64-B gradient rows (grad_stride 16, what mapping() uses): lanes 0..7 hold the feature
-    gradient and lane 8 the certainty side effect; certainties themselves stay untouched."""
-    z = golden(case)
-    nm, dec, mapper = _setup(z, dev, "grid")
-    cert0 = nm.local_point_certainties.clone()
-    acc = torch.zeros((nm.local_geo_features.shape[0], 16), dtype=torch.float32, device=dev)
-    coord = torch.as_tensor(z["it0_coord"], device=dev)
-    label = torch.as_tensor(z["it0_label"], device=dev)
-    ts = torch.as_tensor(z["it0_ts"], device=dev)
-    mapper.train_step(coord, label, ts, acc)
-    assert torch.equal(nm.local_point_certainties, cert0)
-    np.testing.assert_allclose(_np(acc[:, :8]), z["it0_feat_grad"], rtol=1e-4, atol=1e-8)
-    np.testing.assert_allclose(_np(cert0 + acc[:-1, 8]), z["it0_cert_after"], rtol=1e-5, atol=1e-4)
-    assert float(acc[:, 9:].abs().max()) == 0.0
-    np.testing.assert_array_equal(_np(nm.local_point_ts_update), z["it0_ts_after"])
+@pytest.mark.parametrize("wf", [True, False])
+def test_train_step_tile_order_invisible(dev, wf, monkeypatch):
+    """Large batches are processed in tile order (pin_train_rows + pin_query_order): per-row sdf
+    and ts are bitwise those of input order, gradients / certainties / loss agree to float-atomic
+    reordering."""
+    import pin_slam_amd.mapper as M
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    res = []
+    for tiles in (False, True):
+        monkeypatch.setattr(M, "_TILE_QUERIES", tiles)
+        nm, dec, pts = surface_map(400, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend="grid")
+        coord, label, ts = surface_pool(pts, 70000, device=dev)
+        ts = torch.randint(0, 5, ts.shape, device=dev)
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        fg = torch.zeros_like(nm.local_geo_features.data)
+        mg = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+        loss = float(mapper.train_step(coord, label, ts, fg, mg))
+        assert (mapper._order is not None) == tiles
+        res.append((loss, mapper.last_sdf.clone(), fg, mg, nm.local_point_certainties.clone(),
+                    nm.local_point_ts_update.clone()))
+    (l0, s0, f0, m0, c0, t0), (l1, s1, f1, m1, c1, t1) = res
+    assert torch.equal(s0, s1) and torch.equal(t0, t1)
+    assert l1 == pytest.approx(l0, rel=1e-9)
+    np.testing.assert_allclose(_np(f1), _np(f0), rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(_np(m1), _np(m0), rtol=1e-4, atol=1e-8)
+    np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
 
 
 def test_frozen_decoder_trains_features_only(golden, dev):
