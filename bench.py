@@ -10,9 +10,11 @@ processing order, then one pin_query_sdf_grid launch), inputs resident in HBM.  
 batch against its replica of the map ("weak" scaling, no data-path collective);
 the barrier + max-over-ranks timing is the only collective.
 
-Second leg (key "mapper", configs[3]): mapper iterations/s of Mapper.mapping on a 4M-point
-map with 1M sampled queries per iteration per GPU, feature gradients SUM all-reduced over
-RCCL when N > 1 (see mapper_leg).
+Further legs in the same line (informational; `value` stays the headline): "tracker"
+(configs[2], registration steps/s on 200K source points), "mesher" (configs[4], 512^3 grid
+SDF+mask, z-slabs per rank) and "mapper" (configs[3], iterations/s of Mapper.mapping on a
+4M-point map with 1M queries per iteration per GPU, feature gradients SUM all-reduced over
+RCCL when N > 1).
 
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
@@ -82,6 +84,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL on ROCm; gloo only to rehearse N ranks on "
                          "fewer GPUs -- ranks then share devices round robin)")
+    ap.add_argument("--no-tracker", action="store_true", help="skip the tracker leg (configs[2])")
+    ap.add_argument("--no-mesher", action="store_true", help="skip the mesher leg (configs[4])")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -151,6 +155,91 @@ def time_kernel(nm, dec, q, wf, backend, steps):
         torch.cuda.synchronize()
         return statistics.mean(a.elapsed_time(b) for a, b in ev)
     return mean_ms(launch), (mean_ms(order_pass) if order_pass else 0.0)
+
+
+TRACKER_SRC = 200_000      # configs[2]: source points per registration step
+MESH_RES = 512             # configs[4]: 512^3 grid
+MESH_BATCH = 1 << 20       # Mesher infer_bs (utils/config.py:569: bs * 64)
+
+
+def tracker_leg(nm, dec, pts, args, dev, world, rank):
+    """configs[2]: one Tracker.registration_step (fused SDF+grad query of 200K source points,
+    validity + Geman-McClure weights + f64 normal equations, 6x6 solve) per timed iteration,
+    source = map points within 60 m of a sensor, offset by a known SE(3) (0.5 deg yaw, 0.2 m)."""
+    g = torch.Generator(device="cpu").manual_seed(5 + rank)
+    centre = pts.mean(0)
+    near = pts[((pts[:, :2] - centre[:2]) ** 2).sum(1) < 60.0 ** 2]
+    src = near[torch.randint(0, near.shape[0], (TRACKER_SRC,), generator=g)].double()
+    yaw = np.deg2rad(0.5)
+    R = torch.tensor([[np.cos(yaw), -np.sin(yaw), 0], [np.sin(yaw), np.cos(yaw), 0], [0, 0, 1]], dtype=torch.float64)
+    src = ((src - torch.tensor([0.2, 0.0, 0.0], dtype=torch.float64)) @ R).float().to(dev)
+    from pin_slam_amd.synthetic import train_surface
+    fit_loss = train_surface(nm, dec, pts, iters=300)   # a fitted SDF, so the registration has valid points
+    cfg = nm.config
+    tr = P.Tracker(cfg, nm, dec)
+    zeros = torch.zeros(TRACKER_SRC, device=dev)
+
+    def step():
+        return tr.registration_step(src, None, zeros, None, 0, cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
+                                    cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    steps = max(args.steps // 2, 5)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
+            "queries_per_sec": TRACKER_SRC * steps / el, "ms_per_iter": el / steps * 1e3, "steps": steps,
+            "valid_points": int(out[4].shape[0]), "scaling": "replicas", "map_fit_loss": fit_loss,
+            "config": {"workload": "Tracker.registration_step, 200K source points, 1M-point map (configs[2])",
+                       "note": "includes the host 6x6 solve and its device->host copy of 31 doubles"}}
+
+
+def mesher_leg(nm, dec, pts, args, dev, world, rank):
+    """configs[4]: SDF-only + mc_mask (nn_count >= mesh_min_nn) over a 512^3 grid at 0.1 m
+    (Mesher.query_points' device work, batches of infer_bs), split in z-slabs over the ranks
+    (strong scaling); grid coordinates resident in HBM."""
+    from pin_slam_amd.query import query_sdf
+    res = 0.1
+    lo = pts.mean(0) - 0.5 * MESH_RES * res
+    z0 = rank * MESH_RES // world
+    z1 = (rank + 1) * MESH_RES // world
+    i = torch.arange(MESH_RES, device=dev, dtype=torch.float32)
+    zs = torch.arange(z0, z1, device=dev, dtype=torch.float32)
+    gx, gy, gz = torch.meshgrid(i, i, zs, indexing="ij")
+    coord = torch.stack([gx.reshape(-1), gy.reshape(-1), gz.reshape(-1)], 1) * res + lo.to(dev)
+    n = coord.shape[0]
+    mask = torch.empty(n, dtype=torch.bool, device=dev)
+    sdf = torch.empty(n, device=dev)
+    min_nn = int(nm.config.mesh_min_nn)
+
+    def run():
+        for b0 in range(0, n, MESH_BATCH):
+            s, _, nn, _, _ = query_sdf(nm, dec, coord[b0:b0 + MESH_BATCH], query_locally=False, want_grad=False,
+                                       zero_empty=True, want_certainty=False)
+            sdf[b0:b0 + MESH_BATCH] = s
+            mask[b0:b0 + MESH_BATCH] = nn >= min_nn
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t[0])
+    return {"metric": "mesher grid SDF queries/sec", "value": MESH_RES ** 3 / el, "unit": "queries/s",
+            "ms_per_grid": el * 1e3, "scaling": "strong", "masked_fraction": float(mask.float().mean()),
+            "config": {"workload": "512^3 grid at 0.1 m over the 1M-point map, SDF + mc_mask, batches of 2^20, "
+                                   "z-slabs per rank (configs[4])"}}
 
 
 def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
@@ -322,6 +411,10 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
+    if not args.no_mesher:
+        out["mesher"] = mesher_leg(nm, dec, pts, args, dev, world, rank)
+    if not args.no_tracker:   # last: it fits the map first
+        out["tracker"] = tracker_leg(nm, dec, pts, args, dev, world, rank)
     del nm, dec, pts, q
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)

@@ -64,3 +64,23 @@ def surface_pool(pts, n, seed=11, sigma=0.25, device="cuda"):
     coord = pts[idx].clone()
     coord[:, 2] += off
     return coord.to(device), (-off).to(device), torch.zeros(n, dtype=torch.int64, device=device)
+
+
+def train_surface(nm, dec, pts, iters=300, bs=16384, seed=3, pool=1 << 20):
+    """Fit the map + decoder to the synthetic surface with the fused Mapper (sdf label = -z offset),
+    so that SDF gradients are meaningful (tracker workloads).  Returns the last loss."""
+    from .mapper import Mapper
+    cfg = nm.config
+    old_bs = cfg.bs
+    cfg.bs = bs
+    for p in dec.parameters():
+        p.requires_grad_(True)
+    coord, label, ts = surface_pool(pts, pool, seed=seed, device=nm.neural_points.device)
+    mapper = Mapper(cfg, None, nm, dec)
+    mapper.set_pool(coord, label, ts)
+    torch.manual_seed(seed)
+    mapper.mapping(iters)
+    cfg.bs = old_bs
+    nm.reset_local_map(torch.zeros(3, device=nm.neural_points.device),
+                       torch.eye(3, device=nm.neural_points.device), 0)
+    return float(mapper.last_loss)
