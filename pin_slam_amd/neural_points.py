@@ -273,6 +273,12 @@ class NeuralPoints(nn.Module):
         pts = self.neural_points.contiguous()
         _lib.require_device(pts)
         M = pts.shape[0]
+        if M == 0:
+            # empty map: one rejected placeholder record (id -1), so the kernels' clamped gathers
+            # stay in bounds and every candidate is rejected (the reference raises IndexError here)
+            rec = torch.zeros((1, 4), dtype=torch.float32, device=pts.device)
+            rec[0, 3] = torch.tensor([-1], dtype=torch.int32).view(torch.float32)[0]
+            return rec
         rec = torch.empty((M, 4), dtype=torch.float32, device=pts.device)
         local = mode != "global"
         td = self.travel_dist

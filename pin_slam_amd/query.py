@@ -44,6 +44,8 @@ def points_view(records, features, positions, orientations, certainties, after_p
     positions = _f32(positions)
     orientations = _f32(orientations) if after_pgo else None
     certainties = _f32(certainties)
+    if certainties is not None and certainties.numel() == 0:   # empty map: never read, must be non-NULL
+        certainties = torch.zeros(1, dtype=torch.float32, device=certainties.device)
     s = _lib.PinPoints(records=records.data_ptr(), num_points=records.shape[0], features=features.data_ptr(),
                        positions=positions.data_ptr() if positions is not None else None,
                        orientations=orientations.data_ptr() if orientations is not None else None,
