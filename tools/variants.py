@@ -30,7 +30,8 @@ def run(args):
         for lib in libs:
             env = dict(os.environ, PIN_LIB=os.path.join(OUT, lib))
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-mapper", "--no-cpu-baseline",
-                                *args], env=env, capture_output=True, text=True, timeout=300)
+                                "--no-tracker", "--no-mesher", *args], env=env, capture_output=True, text=True,
+                               timeout=300)
             if r.returncode != 0:
                 print(lib, "FAILED", r.stderr[-2000:])
                 sys.exit(1)
