@@ -191,7 +191,7 @@ typedef struct PinRegParams {
 #define PIN_REG_NACC 31          /* [0] sum w, [1] sum |r|, [2] sum w r^2, [3] n_valid,
                                     [4..24] sum w J^T J (upper triangle, row major),
                                     [25..30] sum w r J,  J = [p x g, g] */
-#define PIN_REG_WORKSPACE_DOUBLES (1024 * PIN_REG_NACC)
+#define PIN_REG_WORKSPACE_DOUBLES (256 * PIN_REG_NACC)
 
 /*
  * pin_reg_normal_eq -- fused validity mask + Geman-McClure weights + f64 normal-equation

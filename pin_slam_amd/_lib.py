@@ -53,7 +53,7 @@ class PinRegParams(ctypes.Structure):
 
 
 REG_NACC = 31
-REG_WORKSPACE_DOUBLES = 1024 * REG_NACC
+REG_WORKSPACE_DOUBLES = 256 * REG_NACC
 
 
 class PinMlp(ctypes.Structure):

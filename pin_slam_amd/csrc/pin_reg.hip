@@ -20,7 +20,7 @@
 namespace {
 
 constexpr int kRegBlock = 256;
-constexpr int kRegMaxBlocks = 1024;
+constexpr int kRegMaxBlocks = 256;
 
 __device__ __forceinline__ double wave_sum(double v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
@@ -90,12 +90,19 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
     }
 }
 
-__global__ void __launch_bounds__(64) k_reg_final(const double* __restrict__ partials, int nblk,
-                                                  double* __restrict__ out) {
-    if (threadIdx.x >= PIN_REG_NACC) return;
+// out[k] = sum of the block partials in a fixed order: thread t serves accumulator t / 8
+// (31 x 8 = 248 threads), strided partial sums over the blocks, then a shuffle tree over
+// the 8 lanes of each accumulator
+__global__ void __launch_bounds__(256) k_reg_final(const double* __restrict__ partials, int nblk,
+                                                   double* __restrict__ out) {
+    const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
     double v = 0.0;
-    for (int b = 0; b < nblk; ++b) v += partials[(int64_t)b * PIN_REG_NACC + threadIdx.x];
-    out[threadIdx.x] = v;
+    if (k < PIN_REG_NACC)
+        for (int b = l; b < nblk; b += 8) v += partials[(int64_t)b * PIN_REG_NACC + k];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    if (k < PIN_REG_NACC && l == 0) out[k] = v;
 }
 
 }  // namespace
@@ -111,7 +118,7 @@ int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, 
     auto s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_reg_partials, dim3(nblk), dim3(kRegBlock), 0, s, points, sdf, grad, nn_count, sdf_std,
                        sdf_label, weight, n, *prm, workspace, valid_out);
-    hipLaunchKernelGGL(k_reg_final, dim3(1), dim3(64), 0, s, workspace, nblk, out);
+    hipLaunchKernelGGL(k_reg_final, dim3(1), dim3(256), 0, s, workspace, nblk, out);
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

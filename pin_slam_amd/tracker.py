@@ -51,10 +51,19 @@ def rotation_matrix_to_axis_angle(R: torch.Tensor):
     return torch.acos((torch.trace(R) - 1) / 2)
 
 
+def _expmap_np(axis_angle: np.ndarray) -> np.ndarray:
+    """utils/tracker.py:580-589 (Rodrigues) in f64 on the host."""
+    angle = np.linalg.norm(axis_angle)
+    axis = axis_angle / angle
+    K = np.array([[0.0, -axis[2], axis[1]], [axis[2], 0.0, -axis[0]], [-axis[1], axis[0], 0.0]])
+    return np.eye(3) + K * np.sin(angle) + (K @ K) * (1.0 - np.cos(angle))
+
+
 def _solve(acc: np.ndarray, lm_lambda: float, require_cov: bool, require_eigen: bool, device):
     """Normal equations from the kernel accumulators -> (dT 4x4 f64, cov, eigenvalues).
     The weight normalisation w /= 2 mean(w) (utils/tracker.py:394) is the factor
-    n / (2 sum w) on N and g."""
+    n / (2 sum w) on N and g.  The 6x6 algebra runs on the host in f64 (the reference's
+    torch f64 ops on a 6x6); the results go to the device in one copy each."""
     s_w, s_r, s_wr2, cnt = acc[0], acc[1], acc[2], acc[3]
     scale = cnt / (2.0 * s_w)
     N = np.zeros((6, 6))
@@ -68,17 +77,17 @@ def _solve(acc: np.ndarray, lm_lambda: float, require_cov: bool, require_eigen: 
     N_old = N.copy()
     N = N + lm_lambda * np.diag(np.diag(N))
     t = np.linalg.inv(N) @ g
-    tt = torch.tensor(t, dtype=torch.float64, device=device)
-    T = torch.eye(4, dtype=torch.float64, device=device)
-    T[:3, :3] = expmap(tt[:3])
-    T[:3, 3] = tt[3:]
+    T_np = np.eye(4)
+    T_np[:3, :3] = _expmap_np(t[:3])
+    T_np[:3, 3] = t[3:]
+    T = torch.from_numpy(T_np).to(device)
     eig = None
     if require_eigen:
-        eig = torch.linalg.eigvals(torch.tensor(N_old[3:, 3:], dtype=torch.float64, device=device)).real
+        eig = torch.from_numpy(np.linalg.eigvals(N_old[3:, 3:]).real.copy()).to(device)
     cov = None
     if require_cov:
         mse = s_wr2 / (2.0 * s_w)  # mean(w_norm * r^2)
-        cov = torch.tensor(np.linalg.inv(N_old) * mse, dtype=torch.float64, device=device)
+        cov = torch.from_numpy(np.linalg.inv(N_old) * mse).to(device)
     return T, cov, eig
 
 
@@ -100,14 +109,28 @@ def implicit_reg(points, sdf_grad, sdf_residual, weight, lm_lambda=0.0, require_
     return T, cov, eig
 
 
+_REG_BUF: dict = {}
+
+
+def _reg_buffers(dev):
+    """Per-device workspace + accumulator buffer and a pinned host mirror (reused every step;
+    the host read below synchronises the stream, so reuse is safe)."""
+    key = str(dev)
+    if key not in _REG_BUF:
+        ws = torch.empty(_lib.REG_WORKSPACE_DOUBLES + _lib.REG_NACC, dtype=torch.float64, device=dev)
+        host = torch.empty(_lib.REG_NACC, dtype=torch.float64, pin_memory=ws.is_cuda)
+        _REG_BUF[key] = (ws, host)
+    return _REG_BUF[key]
+
+
 def _reg_accumulate(points, sdf, grad, nn_count, sdf_std, label, weight, prm, valid_out=None):
-    dev = points.device
-    ws = torch.empty(_lib.REG_WORKSPACE_DOUBLES, dtype=torch.float64, device=dev)
-    out = torch.empty(_lib.REG_NACC, dtype=torch.float64, device=dev)
+    ws, host = _reg_buffers(points.device)
+    out = ws[_lib.REG_WORKSPACE_DOUBLES:]
     _lib.call("pin_reg_normal_eq", _lib.ptr(points), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count),
               _lib.ptr(sdf_std), _lib.ptr(label), _lib.ptr(weight), points.shape[0], prm, _lib.ptr(ws),
               _lib.ptr(out), _lib.ptr(valid_out), _lib.stream())
-    return out.cpu().numpy()
+    host.copy_(out)
+    return host.numpy().copy()
 
 
 class Tracker:
@@ -234,8 +257,9 @@ class Tracker:
         labels = sdf_labels.detach().to(torch.float32).contiguous() if sdf_labels is not None else None
         valid = torch.empty(pts.shape[0], dtype=torch.uint8, device=pts.device)
         acc = _reg_accumulate(pts, sdf, grad, nn, std, labels, None, prm, valid)
-        valid_points = points[valid.bool()]
         cnt = int(acc[3])
+        # the count is on the host already: gather the valid rows without another sync
+        valid_points = points[torch.nonzero_static(valid, size=cnt).squeeze(1)]
         if cnt < 10:
             T = torch.eye(4, device=points.device, dtype=torch.float64)
             return T, None, None, None, valid_points, 0.0, 0.0
