@@ -349,6 +349,116 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
                   void* stream);
 
+/* ======================================================================================
+ * Map maintenance: insert, local-map selection, prune, pose
+ * adjustment and re-hash of NeuralPoints, model/neural_points.py:205-428, with the voxel
+ * down-samplers of utils/tools.py:409-477.  Counts that size a caller's allocation are
+ * written to DEVICE int64 cells: the caller reads them (one host sync, as the reference's
+ * boolean indexing does) -- the calls themselves stay stream-ordered.
+ * ====================================================================================== */
+
+/* The per-point arrays of a NeuralPoints map.  Any array but positions may be NULL where a
+ * call says so; features has count + 1 rows (the last one is the padding row). */
+typedef struct PinMapArrays {
+    float* positions;     /* [count,3] f32                 neural_points          */
+    float* orientations;  /* [count,4] f32 (w,x,y,z)       point_orientations     */
+    int64_t* ts_create;   /* [count]                       point_ts_create        */
+    int64_t* ts_update;   /* [count]                       point_ts_update        */
+    float* certainties;   /* [count] f32                   point_certainties      */
+    float* features;      /* [count+1, feature_dim] f32    geo_features           */
+    int64_t count;
+    int32_t feature_dim;
+    int32_t reserved;
+} PinMapArrays;
+
+/* Workspace bytes every map-maintenance call below needs for n elements (points of the frame,
+ * or of the map for the whole-map calls). */
+int64_t pin_map_workspace_bytes(int64_t n);
+
+/*
+ * pin_voxel_down_sample -- one point index per voxel, in ascending order of the reference's
+ * flattened voxel key (torch.unique order):
+ *   value == NULL: the point closest to its voxel centre after quantising the distance to
+ *                  1000 levels, lowest index on ties  (voxel_down_sample_torch, tools.py:409-442)
+ *   value != NULL: the point with the smallest quantised value           (tools.py:444-477)
+ * Reproduces the key's v_size = grid.max() aliasing (tools.py:430-431), the packed
+ * "index + level * 10^digits" amin, and x86 float->int64 conversion of NaN/inf levels.
+ * out_idx: [n] int64 (the first *count entries are written); count: 1 device int64.  n >= 1.
+ */
+int pin_voxel_down_sample(const float* points, int64_t n, float voxel_size, const float* value, int64_t* out_idx,
+                          int64_t* count, void* workspace, void* stream);
+
+/*
+ * pin_map_insert -- the probe and table write of NeuralPoints.update (neural_points.py:214-242)
+ * for the down-sampled points points[sample_idx[i]], i < n:
+ *   hash_idx = table[slot];  new = map empty | hash_idx == -1 | |p_hash_idx - p|^2 > dist2_thre
+ *          | travel_dist[cur_ts] - travel_dist[ts_update[hash_idx]] > travel_thre;
+ *   new points get ids count, count+1, ... in sample order; table[slot] = (new ? id : hash_idx),
+ *   the last sample of a shared slot winning (CPU index_put order).
+ * new_rows: [n] int64 receives sample_idx[i] of each new point, in id order; n_new: 1 device
+ * int64.  positions/ts_update describe the current map (count points).
+ */
+int pin_map_insert(const float* points, const int64_t* sample_idx, int64_t n, float resolution, int32_t* table,
+                   int64_t buffer_size, const float* positions, const int64_t* ts_update, int64_t count,
+                   const float* travel_dist, int64_t cur_ts, float dist2_thre, float travel_thre, int64_t* new_rows,
+                   int64_t* n_new, void* workspace, void* stream);
+
+/*
+ * pin_hash_assign -- table[slot(points[rows[i]])] = rows[i], the last i winning a shared slot
+ * (recreate_hash kept_points=True, neural_points.py:405-411).  Leaves other slots alone.
+ */
+int pin_hash_assign(const float* points, const int64_t* rows, int64_t n, float resolution, int32_t* table,
+                    int64_t buffer_size, void* workspace, void* stream);
+
+/*
+ * pin_local_map -- local-map selection of reset_local_map (neural_points.py:272-303):
+ *   ts_used = use_mid_ts ? long((ts_create + ts_update) / 2) : ts_create;
+ *   local = |p - sensor|^2 < radius2 & (use_travel_dist ? |td[cur_ts] - td[ts_used]| < travel_thre
+ *                                                       : |cur_ts - ts_used| < diff_ts_local)
+ * sensor_position: 3 floats (sensor_f64 = 0) or 3 doubles (sensor_f64 = 1) on the device; the
+ * distance test runs in the promoted precision, as torch does for an f64 pose.
+ * local_mask [count+1] u8 (last = 1), global2local [count+1] (rank, or g2l_fill off the local
+ * map; last = -1), local_rows [count] (global rows of the local points, ascending), local_count
+ * (1 device int64).  map needs positions, ts_create (and ts_update when use_mid_ts).
+ */
+int pin_local_map(const PinMapArrays* map, const float* travel_dist, const void* sensor_position, int32_t sensor_f64,
+                  int64_t cur_ts, double radius2, float travel_thre, int32_t use_mid_ts, int32_t use_travel_dist,
+                  int64_t diff_ts_local, int64_t g2l_fill, uint8_t* local_mask, int64_t* global2local,
+                  int64_t* local_rows, int64_t* local_count, void* workspace, void* stream);
+
+/*
+ * pin_prune_rows -- prune_map's selection (neural_points.py:329-337): a point is pruned when
+ * |td[cur_ts] - td[ts_update]| > travel_thre and certainty < certainty_thre.  keep_rows [count]
+ * receives the kept rows ascending, keep_count (1 device int64) their number.
+ */
+int pin_prune_rows(const PinMapArrays* map, const float* travel_dist, int64_t cur_ts, float travel_thre,
+                   float certainty_thre, int64_t* keep_rows, int64_t* keep_count, void* workspace, void* stream);
+
+/*
+ * pin_map_gather -- dst.x[i] = src.x[rows[i]], i < n_rows, for every array non-NULL in dst
+ * (boolean-mask / index selection of reset_local_map :293-309, prune_map :339-349 and
+ * recreate_hash :414-421).  pad_row != 0 also copies the features padding row:
+ * dst.features[n_rows] = src.features[src.count].  dst.count is not read.
+ */
+int pin_map_gather(const PinMapArrays* src, const int64_t* rows, int64_t n_rows, int32_t pad_row,
+                   const PinMapArrays* dst, void* stream);
+
+/*
+ * pin_map_scatter -- dst.x[rows[i]] = src.x[i] for every array non-NULL in src (assign_local_to_
+ * global, neural_points.py:315-324); pad_row != 0 also writes src.features[n_rows] to
+ * dst.features[dst.count].
+ */
+int pin_map_scatter(const PinMapArrays* src, const int64_t* rows, int64_t n_rows, int32_t pad_row,
+                    const PinMapArrays* dst, void* stream);
+
+/*
+ * pin_map_adjust -- adjust_map (neural_points.py:355-370) in place: each point moves by the
+ * pose correction pose_diff[ts_used] ([T,4,4] f32 row-major; ts_used as in pin_local_map):
+ * p = R p + t, q = quat(R) * q (utils/tools.py:326-334, :356-369, :401-407).
+ */
+int pin_map_adjust(const PinMapArrays* map, const float* pose_diff, int64_t num_poses, int32_t use_mid_ts,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

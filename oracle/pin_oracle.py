@@ -106,7 +106,7 @@ def reset_local_map(st: MapState, sensor_position: np.ndarray, cur_ts: int, loca
     """model/neural_points.py:272-311 (travel-distance form)."""
     st.cur_ts = int(cur_ts)
     d2 = ((st.points - sensor_position.astype(np.float32)) ** 2).sum(-1)
-    ts_used = (st.ts_create + st.ts_update) // 2 if use_mid_ts else st.ts_create
+    ts_used = _ts_used(st, use_mid_ts)
     dtd = np.abs(st.travel_dist[cur_ts] - st.travel_dist[ts_used])
     mask = (d2 < local_map_radius ** 2) & (dtd < st.diff_travel_dist_local)
     st.local_points = st.points[mask]
@@ -499,6 +499,164 @@ def query_certainty(st: MapState, q: np.ndarray, resolution: float) -> np.ndarra
     c = st.certainties[idx]
     c[idx < 0] = 0.0
     return c.max(-1)
+
+
+# ---------------------------------------------------------------- map maintenance
+INT64_MIN = np.iinfo(np.int64).min
+
+
+def to_long(x) -> np.ndarray:
+    """torch CPU float32 -> int64 (``.long()``): truncation toward zero; NaN, +-inf and values
+    outside int64 give INT64_MIN (x86 cvttss2si "integer indefinite")."""
+    x = np.asarray(x, np.float32)
+    ok = np.isfinite(x) & (np.abs(x) < np.float32(2.0 ** 63))
+    out = np.full(x.shape, INT64_MIN, np.int64)
+    out[ok] = x[ok].astype(np.int64)
+    return out
+
+
+def voxel_down_sample(points: np.ndarray, voxel_size: float, value: Optional[np.ndarray] = None) -> np.ndarray:
+    """utils/tools.py:409-442 (value None: closest to the voxel centre) and :444-477 (smallest
+    value): one index per voxel in ascending flattened-key order.  Keeps the reference's
+    v_size = grid.max() key (which aliases c0 = v with c1 + 1), the 1000-level quantisation
+    and the packed "index + level * 10^digits" amin with int64 wrap-around."""
+    p = np.asarray(points, np.float32)
+    vs = np.float32(voxel_size)
+    n = p.shape[0]
+    grid = np.floor(p / vs)
+    offset = np.floor(p.min(0) / vs).astype(np.int64)
+    if value is None:
+        d = p - (grid + np.float32(0.5)) * vs
+        src = np.sqrt((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+    else:
+        src = np.asarray(value, np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        level = src / src.max() * np.float32(999)
+    c = grid.astype(np.int64) - offset
+    v = c.max()
+    key = c[:, 0] + c[:, 1] * v + c[:, 2] * v * v
+    uniq, inv = np.unique(key, return_inverse=True)
+    scale = 10 ** len(str(n - 1))
+    with np.errstate(over="ignore"):
+        packed = np.arange(n, dtype=np.int64) + to_long(level) * np.int64(scale)
+    best = np.full(uniq.shape[0], np.iinfo(np.int64).max, np.int64)
+    np.minimum.at(best, inv.reshape(-1), packed)
+    return np.mod(best, np.int64(scale))
+
+
+def _ts_used(st: MapState, use_mid_ts: bool) -> np.ndarray:
+    """((ts_create + ts_update) / 2).long(): true division to float32, truncation."""
+    if use_mid_ts:
+        return to_long((st.ts_create + st.ts_update).astype(np.float32) / np.float32(2))
+    return st.ts_create
+
+
+def empty_map(resolution: float, buffer_size: int, travel_dist: np.ndarray, diff_travel_dist_local: float,
+              feature_dim: int = 8) -> MapState:
+    z = np.zeros
+    return MapState(resolution=resolution, buffer_size=int(buffer_size),
+                    table=np.full(int(buffer_size), -1, np.int64), points=z((0, 3), np.float32),
+                    orientations=z((0, 4), np.float32), geo_features=z((1, feature_dim), np.float32),
+                    ts_create=z(0, np.int64), ts_update=z(0, np.int64), certainties=z(0, np.float32),
+                    travel_dist=np.asarray(travel_dist, np.float32), cur_ts=0,
+                    diff_travel_dist_local=float(diff_travel_dist_local), local_mask=z(1, bool),
+                    global2local=z(1, np.int64), local_points=None, local_orientations=None, local_features=None,
+                    local_certainties=None, local_ts_update=None)
+
+
+def map_update(st: MapState, points: np.ndarray, cur_ts: int) -> np.ndarray:
+    """model/neural_points.py:205-268 without the reset_local_map tail: down-sample, probe,
+    insert new / collided / stale samples with consecutive ids, last writer per slot.  New
+    features are zeros here (the reference draws them at random).  Returns sample_idx."""
+    res = st.resolution
+    sidx = voxel_down_sample(points, res)
+    sp = np.asarray(points, np.float32)[sidx]
+    slots = hash_slots(voxel_coords(sp, res), st.buffer_size)
+    hidx = st.table[slots]
+    M = st.points.shape[0]
+    if M == 0:
+        fresh = np.ones(sidx.shape[0], bool)
+    else:
+        d = st.points[hidx] - sp
+        d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        dtd = st.travel_dist[cur_ts] - st.travel_dist[st.ts_update[hidx]]
+        fresh = (hidx == -1) | (d2 > np.float32(3 * res ** 2)) | (dtd > np.float32(st.diff_travel_dist_local))
+    added = sp[fresh]
+    k = added.shape[0]
+    cur = hidx.copy()
+    cur[fresh] = np.arange(k, dtype=np.int64) + M
+    st.table[slots] = cur  # repeated slots: the last assignment stays (CPU index_put order)
+    st.points = np.concatenate([st.points, added])
+    quat = np.zeros((k, 4), np.float32)
+    quat[:, 0] = 1.0
+    st.orientations = np.concatenate([st.orientations, quat])
+    st.ts_create = np.concatenate([st.ts_create, np.full(k, cur_ts, np.int64)])
+    st.ts_update = np.concatenate([st.ts_update, np.full(k, cur_ts, np.int64)])
+    st.certainties = np.concatenate([st.certainties, np.zeros(k, np.float32)])
+    st.geo_features = np.concatenate([st.geo_features[:-1], np.zeros((k + 1, st.geo_features.shape[1]), np.float32)])
+    return sidx
+
+
+def prune_keep(st: MapState, thre: float) -> np.ndarray:
+    """model/neural_points.py:329-337: the rows prune_map keeps."""
+    dtd = np.abs(st.travel_dist[st.cur_ts] - st.travel_dist[st.ts_update])
+    prune = (dtd > np.float32(st.diff_travel_dist_local)) & (st.certainties < np.float32(thre))
+    return ~prune
+
+
+def select_rows(st: MapState, rows: np.ndarray) -> None:
+    """Index selection of every per-point array, features keeping the padding row."""
+    st.points = st.points[rows]
+    st.orientations = st.orientations[rows]
+    st.ts_create = st.ts_create[rows]
+    st.ts_update = st.ts_update[rows]
+    st.certainties = st.certainties[rows]
+    st.geo_features = st.geo_features[np.concatenate([rows, [-1]])]
+
+
+def recreate_hash(st: MapState, cur_ts: int, kept_points: bool, with_ts: bool, use_mid_ts: bool = False) -> None:
+    """model/neural_points.py:372-426 (the reset_local_map tail is the caller's)."""
+    res = st.resolution
+    st.table = np.full(st.buffer_size, -1, np.int64)
+    if with_ts:
+        value = np.abs(_ts_used(st, use_mid_ts) - cur_ts).astype(np.float32)
+    else:
+        value = -st.certainties
+    sidx = voxel_down_sample(st.points, res, value)
+    if kept_points:
+        slots = hash_slots(voxel_coords(st.points[sidx], res), st.buffer_size)
+        st.table[slots] = sidx
+    else:
+        select_rows(st, sidx)
+        st.table = build_table(st.points, res, st.buffer_size)
+
+
+def rotmat_to_quat(R: np.ndarray) -> np.ndarray:
+    """utils/tools.py:326-334."""
+    R = R.astype(np.float32)
+    qw = np.sqrt(np.float32(1.0) + R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2]) / np.float32(2.0)
+    qx = (R[:, 2, 1] - R[:, 1, 2]) / (np.float32(4.0) * qw)
+    qy = (R[:, 0, 2] - R[:, 2, 0]) / (np.float32(4.0) * qw)
+    qz = (R[:, 1, 0] - R[:, 0, 1]) / (np.float32(4.0) * qw)
+    return np.stack([qw, qx, qy, qz], 1)
+
+
+def quat_multiply(q1: np.ndarray, q2: np.ndarray) -> np.ndarray:
+    """utils/tools.py:356-369."""
+    w1, x1, y1, z1 = q1.T
+    w2, x2, y2, z2 = q2.T
+    return np.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2, w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                     w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2, w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], 1)
+
+
+def adjust_map(st: MapState, pose_diff: np.ndarray, use_mid_ts: bool = False) -> None:
+    """model/neural_points.py:355-370 with transform_batch_torch (utils/tools.py:401-407)."""
+    used = _ts_used(st, use_mid_ts)
+    T = pose_diff.astype(np.float32)[used]
+    p = st.points
+    st.points = ((T[:, :3, 0] * p[:, 0:1] + T[:, :3, 1] * p[:, 1:2]) + T[:, :3, 2] * p[:, 2:3]) + T[:, :3, 3]
+    dq = rotmat_to_quat(pose_diff[:, :3, :3])
+    st.orientations = quat_multiply(dq[used], st.orientations).astype(np.float32)
 
 
 # ---------------------------------------------------------------- fixture helpers

@@ -76,6 +76,12 @@ class PinAdamStep(ctypes.Structure):
                 ("bias_correction2_sqrt", f32), ("eps", f32), ("zero_grad", i32), ("grad_stride", i32)]
 
 
+class PinMapArrays(ctypes.Structure):
+    _fields_ = [("positions", c_void_p), ("orientations", c_void_p), ("ts_create", c_void_p), ("ts_update", c_void_p),
+                ("certainties", c_void_p), ("features", c_void_p), ("count", i64), ("feature_dim", i32),
+                ("reserved", i32)]
+
+
 MLP_GRAD_SIZE = HIDDEN_DIM * (FEATURE_DIM + 3) + 2 * HIDDEN_DIM + 1
 
 _P = ctypes.POINTER
@@ -111,7 +117,20 @@ _SIGS = {
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
+    "pin_map_workspace_bytes": [i64],
+    "pin_voxel_down_sample": [c_void_p, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_map_insert": [c_void_p, c_void_p, i64, f32, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, i64, f32, f32,
+                       c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_hash_assign": [c_void_p, c_void_p, i64, f32, c_void_p, i64, c_void_p, c_void_p],
+    "pin_local_map": [_P(PinMapArrays), c_void_p, c_void_p, i32, i64, ctypes.c_double, f32, i32, i32, i64, i64,
+                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_prune_rows": [_P(PinMapArrays), c_void_p, i64, f32, f32, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_map_gather": [_P(PinMapArrays), c_void_p, i64, i32, _P(PinMapArrays), c_void_p],
+    "pin_map_scatter": [_P(PinMapArrays), c_void_p, i64, i32, _P(PinMapArrays), c_void_p],
+    "pin_map_adjust": [_P(PinMapArrays), c_void_p, i64, i32, c_void_p],
 }
+# functions whose return value is not a status code
+_RESTYPES = {"pin_map_workspace_bytes": i64}
 
 _lib = None
 
@@ -132,7 +151,7 @@ def load():
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_int
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
     _lib = lib
     return lib
 
@@ -141,6 +160,13 @@ def call(name, *args):
     rc = getattr(load(), name)(*args)
     if rc != PIN_OK:
         raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)}")
+
+
+def map_workspace_bytes(n):
+    b = load().pin_map_workspace_bytes(int(n))
+    if b < 0:
+        raise RuntimeError(f"pin_map_workspace_bytes failed: {_ERRORS.get(b, b)}")
+    return b
 
 
 def ptr(t):

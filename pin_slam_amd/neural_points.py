@@ -11,8 +11,9 @@ different inside:
   (x, y, z, id) that fold the travel-distance filter and ``global2local`` into
   one 16-byte gather; records are rebuilt when any tensor they depend on is
   replaced or modified in place (tracked with ``Tensor._version``).
-* map maintenance (update / local map / rehash / prune / adjust) runs as
-  stream-ordered torch ops on the device plus the hash-rebuild kernel.
+* map maintenance (update / local map / rehash / prune / adjust) runs in the
+  pin_map.hip kernels (voxel down-sample, insert, local-map selection,
+  gathers/scatters); the only host syncs are the counts that size new tensors.
 
 Reference quirk kept for parity: ``reset_local_map`` builds ``global2local``
 with ``torch.full_like(<bool mask>, -1).long()`` (neural_points.py:301), which
@@ -44,39 +45,46 @@ def neighbor_offsets(num_nei_cells: int, search_alpha: float, device=None) -> to
     return grid[keep]
 
 
+_MAP_WS = {}
+
+
+def map_workspace(n: int, device) -> torch.Tensor:
+    """Device workspace of the map-maintenance kernels for n elements (grown, reused per device;
+    the calls are stream-ordered, so reuse across calls on one stream is safe)."""
+    need = _lib.map_workspace_bytes(max(int(n), 1))
+    key = str(device)
+    buf = _MAP_WS.get(key)
+    if buf is None or buf.numel() < need:
+        buf = torch.empty((need,), dtype=torch.uint8, device=device)
+        _MAP_WS[key] = buf
+    return buf
+
+
+def _down_sample(points: torch.Tensor, voxel_size: float, value) -> torch.Tensor:
+    p = points.detach().to(torch.float32).contiguous()
+    _lib.require_device(p)
+    n = p.shape[0]
+    if n == 0:
+        raise RuntimeError("voxel_down_sample: empty point cloud (the reference's min() raises too)")
+    v = value.detach().to(device=p.device, dtype=torch.float32).contiguous() if value is not None else None
+    out = torch.empty((n,), dtype=torch.int64, device=p.device)
+    cnt = torch.empty((1,), dtype=torch.int64, device=p.device)
+    _lib.call("pin_voxel_down_sample", _lib.ptr(p), n, float(np.float32(voxel_size)), _lib.ptr(v), _lib.ptr(out),
+              _lib.ptr(cnt), _lib.ptr(map_workspace(n, p.device)), _lib.stream())
+    return out[:int(cnt.item())]
+
+
 def voxel_down_sample(points: torch.Tensor, voxel_size: float) -> torch.Tensor:
-    """Index of one point per voxel: the one closest to the voxel centre after quantising
-    the distance to 1000 levels, lowest index on ties (semantics of utils/tools.py:409-442,
-    including its flattened-voxel key built with the single extent grid.max())."""
-    n = points.shape[0]
-    cell = torch.floor(points / voxel_size)
-    centre = (cell + 0.5) * voxel_size
-    d = ((points - centre) ** 2).sum(1) ** 0.5
-    q = (d / d.max() * 999).long()
-    c = cell.long() - torch.floor(points.min(dim=0)[0] / voxel_size).long()
-    ext = c.max()
-    key = c[:, 0] + c[:, 1] * ext + c[:, 2] * ext * ext
-    uniq, inv = torch.unique(key, return_inverse=True)
-    scale = 10 ** len(str(n - 1))
-    packed = torch.arange(n, device=points.device) + q * scale
-    best = torch.empty(uniq.shape, dtype=torch.int64, device=points.device)
-    best.scatter_reduce_(0, inv, packed, reduce="amin", include_self=False)
-    return best % scale
+    """Index of one point per voxel: the one closest to the voxel centre after quantising the
+    distance to 1000 levels, lowest index on ties, in ascending voxel-key order
+    (utils/tools.py:409-442, including its flattened key built with the single extent
+    grid.max()).  HIP: pin_voxel_down_sample."""
+    return _down_sample(points, voxel_size, None)
 
 
 def voxel_down_sample_min_value(points: torch.Tensor, voxel_size: float, value: torch.Tensor) -> torch.Tensor:
-    """One point per voxel with the minimum (quantised) value (utils/tools.py:444-477)."""
-    n = points.shape[0]
-    c = torch.floor(points / voxel_size).long() - torch.floor(points.min(dim=0)[0] / voxel_size).long()
-    v = (value / value.max() * 999).long()
-    ext = c.max()
-    key = c[:, 0] + c[:, 1] * ext + c[:, 2] * ext * ext
-    uniq, inv = torch.unique(key, return_inverse=True)
-    scale = 10 ** len(str(n - 1))
-    packed = torch.arange(n, device=points.device) + v * scale
-    best = torch.empty(uniq.shape, dtype=torch.int64, device=points.device)
-    best.scatter_reduce_(0, inv, packed, reduce="amin", include_self=False)
-    return best % scale
+    """One point per voxel with the minimum quantised value (utils/tools.py:444-477)."""
+    return _down_sample(points, voxel_size, value)
 
 
 def grid_window_collision_free(buffer_size: int, num_nei_cells: int) -> bool:
@@ -99,32 +107,6 @@ def hash_slots(points: torch.Tensor, resolution: float, buffer_size: int) -> tor
     g = torch.floor(points / resolution).to(torch.int64)
     h = (g * torch.tensor(PRIMES, dtype=torch.int64, device=points.device)).sum(-1)
     return torch.remainder(h, int(buffer_size))
-
-
-def last_writer(slots: torch.Tensor) -> torch.Tensor:
-    """Positions of the last occurrence of every distinct slot (CPU index_put order)."""
-    perm = torch.argsort(slots, stable=True)
-    s = slots[perm]
-    last = torch.ones_like(s, dtype=torch.bool)
-    last[:-1] = s[1:] != s[:-1]
-    return perm[last]
-
-
-def quat_multiply(q1: torch.Tensor, q2: torch.Tensor) -> torch.Tensor:
-    w1, x1, y1, z1 = q1.unbind(-1)
-    w2, x2, y2, z2 = q2.unbind(-1)
-    return torch.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
-                        w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
-                        w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
-                        w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], -1)
-
-
-def rotmat_to_quat(R: torch.Tensor) -> torch.Tensor:
-    qw = torch.sqrt(1.0 + R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2]) / 2.0
-    qx = (R[:, 2, 1] - R[:, 1, 2]) / (4 * qw)
-    qy = (R[:, 0, 2] - R[:, 2, 0]) / (4 * qw)
-    qz = (R[:, 1, 0] - R[:, 0, 1]) / (4 * qw)
-    return torch.stack([qw, qx, qy, qz], -1)
 
 
 class NeuralPoints(nn.Module):
@@ -382,70 +364,133 @@ class NeuralPoints(nn.Module):
                          reserved=0)
         return _View(g, (bricks, crec, cfeat, ccert, cgid, offs))
 
-    # ------------------------------------------------------------------ map update
+    # ------------------------------------------------------------------ map maintenance
+    def _travel_dist_dev(self, device):
+        if self.travel_dist is None:
+            raise TypeError("NeuralPoints.travel_dist is not set (the reference indexes it here too)")
+        return self._cached("travel_dist_f32", (self.travel_dist,), (str(device),),
+                            lambda: self.travel_dist.detach().to(device=device, dtype=torch.float32).contiguous())
+
+    def _map_arrays(self, local: bool = False, features: bool = True) -> _lib.PinMapArrays:
+        """PinMapArrays over the global (or local) tensors; every one must be contiguous."""
+        if local:
+            ts = (None, self.local_point_orientations, None, self.local_point_ts_update, self.local_point_certainties,
+                  self.local_geo_features.data if features else None)
+            pos, count = self.local_neural_points, self.local_neural_points.shape[0]
+        else:
+            ts = (None, self.point_orientations, self.point_ts_create, self.point_ts_update, self.point_certainties,
+                  self.geo_features.data if features else None)
+            pos, count = self.neural_points, self.neural_points.shape[0]
+        for t in (pos,) + ts[1:]:
+            if t is not None and not t.is_contiguous():
+                raise ValueError("pin_slam_amd: map tensors must be contiguous")
+        ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None  # noqa: E731
+        return _lib.PinMapArrays(positions=ptr(pos), orientations=ptr(ts[1]), ts_create=ptr(ts[2]),
+                                 ts_update=ptr(ts[3]), certainties=ptr(ts[4]), features=ptr(ts[5]), count=count,
+                                 feature_dim=self.geo_feature_dim, reserved=0)
+
+    def _select_global(self, rows: torch.Tensor, n: int):
+        """Replace every per-point array by its rows ``rows[:n]`` (features keep the padding row)."""
+        dev = self.neural_points.device
+        F = self.geo_feature_dim
+        out = dict(pos=torch.empty((n, 3), dtype=self.dtype, device=dev),
+                   quat=torch.empty((n, 4), dtype=self.dtype, device=dev),
+                   tc=torch.empty((n,), dtype=torch.long, device=dev), tu=torch.empty((n,), dtype=torch.long, device=dev),
+                   cert=torch.empty((n,), dtype=self.dtype, device=dev),
+                   feat=torch.empty((n + 1, F), dtype=self.dtype, device=dev))
+        dst = _lib.PinMapArrays(positions=out["pos"].data_ptr(), orientations=out["quat"].data_ptr(),
+                                ts_create=out["tc"].data_ptr(), ts_update=out["tu"].data_ptr(),
+                                certainties=out["cert"].data_ptr(), features=out["feat"].data_ptr(), count=n,
+                                feature_dim=F, reserved=0)
+        src = self._map_arrays()
+        _lib.call("pin_map_gather", ctypes.byref(src), _lib.ptr(rows), n, 1, ctypes.byref(dst), _lib.stream())
+        self.neural_points, self.point_orientations = out["pos"], out["quat"]
+        self.point_ts_create, self.point_ts_update = out["tc"], out["tu"]
+        self.point_certainties, self.geo_features = out["cert"], out["feat"]
+
     def update(self, points: torch.Tensor, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor, cur_ts):
         """model/neural_points.py:205-270: voxel down-sample, hash probe, insert new points
-        (free slot, collision or stale), last-writer-wins slot assignment, padded features."""
+        (free slot, collision or stale), last-writer-wins slot assignment, padded features.
+        HIP: pin_voxel_down_sample + pin_map_insert; one host sync for the number of new points."""
         res = self.resolution
-        sample_points = points[voxel_down_sample(points, res)]
-        slots = hash_slots(sample_points, res, self.buffer_size)
-        hash_idx = self.buffer_pt_index[slots].long()
-        if not self.is_empty():
-            d2 = ((self.neural_points[hash_idx] - sample_points) ** 2).sum(-1)
-            dtd = self.travel_dist[cur_ts] - self.travel_dist[self.point_ts_update[hash_idx]]
-            update_mask = (hash_idx == -1) | (d2 > 3 * res ** 2) | (dtd > self.diff_travel_dist_local)
-        else:
-            update_mask = torch.ones(hash_idx.shape, dtype=torch.bool, device=self.device)
-        added = sample_points[update_mask]
-        n_new = added.shape[0]
+        pts = points.detach().to(self.dtype).contiguous()
+        _lib.require_device(pts)
+        dev = pts.device
+        sidx = voxel_down_sample(pts, res)
+        n = sidx.shape[0]
         M = self.count()
-        cur_idx = hash_idx.clone()
-        cur_idx[update_mask] = torch.arange(n_new, dtype=torch.int64, device=self.device) + M
-        sel = last_writer(slots)
-        self.buffer_pt_index[slots[sel]] = cur_idx[sel].to(torch.int32)
+        td = self._travel_dist_dev(dev) if M > 0 else None
+        if td is not None and not 0 <= int(cur_ts) < td.shape[0]:
+            raise IndexError("travel_dist has no entry for cur_ts=%d" % int(cur_ts))
+        new_rows = torch.empty((max(n, 1),), dtype=torch.int64, device=dev)
+        n_new = torch.empty((1,), dtype=torch.int64, device=dev)
+        _lib.call("pin_map_insert", _lib.ptr(pts), _lib.ptr(sidx), n, float(np.float32(res)),
+                  _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.ptr(self.neural_points) if M else None,
+                  _lib.ptr(self.point_ts_update) if M else None, M, _lib.ptr(td), int(cur_ts),
+                  float(np.float32(3 * res ** 2)), float(np.float32(self.diff_travel_dist_local)), _lib.ptr(new_rows),
+                  _lib.ptr(n_new), _lib.ptr(map_workspace(n, dev)), _lib.stream())
+        torch.autograd.graph.increment_version(self.buffer_pt_index)
+        k = int(n_new.item())
+        added = pts[new_rows[:k]]
         self.neural_points = torch.cat((self.neural_points, added), 0)
-        quat = torch.zeros((n_new, 4), dtype=self.dtype, device=self.device)
+        quat = torch.zeros((k, 4), dtype=self.dtype, device=dev)
         quat[:, 0] = 1.0
         self.point_orientations = torch.cat((self.point_orientations, quat), 0)
-        ts = torch.full((n_new,), int(cur_ts), device=self.device, dtype=torch.long)
+        ts = torch.full((k,), int(cur_ts), device=dev, dtype=torch.long)
         self.point_ts_create = torch.cat((self.point_ts_create, ts), 0)
         self.point_ts_update = torch.cat((self.point_ts_update, ts), 0)
-        new_fts = self.geo_feature_std * torch.randn(n_new + 1, self.geo_feature_dim, device=self.device,
-                                                     dtype=self.dtype)
+        new_fts = self.geo_feature_std * torch.randn(k + 1, self.geo_feature_dim, device=dev, dtype=self.dtype)
         self.geo_features = torch.cat((self.geo_features[:-1], new_fts), 0)
         self.point_certainties = torch.cat(
-            (self.point_certainties, torch.zeros(n_new, device=self.device, dtype=self.dtype)), 0)
+            (self.point_certainties, torch.zeros(k, device=dev, dtype=self.dtype)), 0)
         self.reset_local_map(sensor_position, sensor_orientation, cur_ts)
 
     def reset_local_map(self, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor, cur_ts: int,
                         use_travel_dist: bool = True, diff_ts_local: int = 50):
-        """model/neural_points.py:272-313."""
+        """model/neural_points.py:272-313.  HIP: pin_local_map (mask, global2local, row list)
+        + pin_map_gather of the local arrays; one host sync for the local count."""
         self.cur_ts = cur_ts
         self.max_ts = max(self.max_ts, cur_ts)
-        dist2sensor = ((self.neural_points - sensor_position) ** 2).sum(-1)
-        if self.config.use_mid_ts:
-            ts_used = ((self.point_ts_create + self.point_ts_update) / 2).long()
-        else:
-            ts_used = self.point_ts_create
-        if use_travel_dist:
-            dtd = torch.abs(self.travel_dist[cur_ts] - self.travel_dist[ts_used])
-            mask = (dist2sensor < self.local_map_radius ** 2) & (dtd < self.diff_travel_dist_local)
-        else:
-            mask = (dist2sensor < self.local_map_radius ** 2) & (torch.abs(cur_ts - ts_used) < diff_ts_local)
-        self.local_neural_points = self.neural_points[mask]
-        self.local_point_orientations = self.point_orientations[mask]
-        self.local_point_certainties = self.point_certainties[mask]
-        self.local_point_ts_update = self.point_ts_update[mask]
-        mask = torch.cat((mask, torch.ones(1, dtype=torch.bool, device=mask.device)))
-        self.local_mask = mask
+        dev = self.neural_points.device
+        _lib.require_device(self.neural_points)
+        M = self.count()
+        sensor = torch.as_tensor(sensor_position).detach().to(dev).reshape(-1)[:3]
+        f64 = sensor.dtype == torch.float64
+        sensor = sensor.to(torch.float64 if f64 else torch.float32).contiguous()
+        td = self._travel_dist_dev(dev) if (use_travel_dist and M > 0) else None
+        if td is not None and not 0 <= int(cur_ts) < td.shape[0]:
+            raise IndexError("travel_dist has no entry for cur_ts=%d" % int(cur_ts))
+        mask = torch.empty((M + 1,), dtype=torch.uint8, device=dev)
+        g2l = torch.empty((M + 1,), dtype=torch.int64, device=dev)
+        rows = torch.empty((max(M, 1),), dtype=torch.int64, device=dev)
+        cnt = torch.empty((1,), dtype=torch.int64, device=dev)
         fill = -1 if self.strict_global2local else 1  # see module docstring (reference quirk)
-        g2l = torch.full(mask.shape, fill, dtype=torch.long, device=mask.device)
-        li = torch.nonzero(mask).flatten()
-        g2l[li] = torch.arange(li.shape[0], device=mask.device)
-        g2l[-1] = -1
+        src = self._map_arrays()
+        _lib.call("pin_local_map", ctypes.byref(src), _lib.ptr(td), _lib.ptr(sensor), int(f64), int(cur_ts),
+                  float(self.local_map_radius) ** 2, float(np.float32(self.diff_travel_dist_local)),
+                  int(bool(self.config.use_mid_ts)), int(bool(use_travel_dist)), int(diff_ts_local), fill,
+                  _lib.ptr(mask), _lib.ptr(g2l), _lib.ptr(rows), _lib.ptr(cnt), _lib.ptr(map_workspace(M, dev)),
+                  _lib.stream())
+        L = int(cnt.item())
+        F = self.geo_feature_dim
+        lpos = torch.empty((L, 3), dtype=self.dtype, device=dev)
+        lquat = torch.empty((L, 4), dtype=self.dtype, device=dev)
+        lcert = torch.empty((L,), dtype=self.dtype, device=dev)
+        lts = torch.empty((L,), dtype=torch.long, device=dev)
+        lfeat = torch.empty((L + 1, F), dtype=self.dtype, device=dev)
+        dst = _lib.PinMapArrays(positions=lpos.data_ptr(), orientations=lquat.data_ptr(), ts_create=None,
+                                ts_update=lts.data_ptr(), certainties=lcert.data_ptr(), features=lfeat.data_ptr(),
+                                count=L, feature_dim=F, reserved=0)
+        _lib.call("pin_map_gather", ctypes.byref(src), _lib.ptr(rows), L, 1, ctypes.byref(dst), _lib.stream())
+        self.local_neural_points = lpos
+        self.local_point_orientations = lquat
+        self.local_point_certainties = lcert
+        self.local_point_ts_update = lts
+        self.local_mask = mask.view(torch.bool)
         self.global2local = g2l
-        self.local_geo_features = nn.Parameter(self.geo_features[mask])
+        self.local_geo_features = nn.Parameter(lfeat)
         self.local_orientation = sensor_orientation
+        self._local_rows = (self.local_mask, rows[:L])
         self._local_snapshot = self._snapshot()
 
     def _snapshot(self):
@@ -463,76 +508,96 @@ class NeuralPoints(nn.Module):
         ts = (self.neural_points, self.local_neural_points, self.point_orientations, self.local_point_orientations)
         return all(snap[i][0]() is ts[i] and ts[i]._version == snap[i][1] for i in idx)
 
+    def _local_row_list(self):
+        lr = getattr(self, "_local_rows", None)
+        if lr is not None and lr[0] is self.local_mask:
+            return lr[1]
+        return torch.nonzero(self.local_mask[:-1]).flatten()
+
     def assign_local_to_global(self):
-        """model/neural_points.py:315-324."""
-        m = self.local_mask
-        if not self._unchanged_since_reset((0, 1)):
-            self.neural_points[m[:-1]] = self.local_neural_points
-        if not self._unchanged_since_reset((2, 3)):
-            self.point_orientations[m[:-1]] = self.local_point_orientations
+        """model/neural_points.py:315-324.  HIP: one pin_map_scatter over the local rows; the
+        position / orientation write-back is skipped while it is an exact no-op."""
+        rows = self._local_row_list()
+        L = rows.shape[0]
+        write_pos = not self._unchanged_since_reset((0, 1))
+        write_quat = not self._unchanged_since_reset((2, 3))
+        src = self._map_arrays(local=True)
+        if not write_pos:
+            src.positions = None
+        if not write_quat:
+            src.orientations = None
+        dst = self._map_arrays()
+        _lib.call("pin_map_scatter", ctypes.byref(src), _lib.ptr(rows), L, 1, ctypes.byref(dst), _lib.stream())
+        changed = [self.geo_features, self.point_certainties, self.point_ts_update]
+        changed += [self.neural_points] if write_pos else []
+        changed += [self.point_orientations] if write_quat else []
+        for t in changed:
+            torch.autograd.graph.increment_version(t)
         self._local_snapshot = self._snapshot()
-        self.geo_features[m] = self.local_geo_features.data
-        self.point_certainties[m[:-1]] = self.local_point_certainties
-        self.point_ts_update[m[:-1]] = self.local_point_ts_update
 
     def prune_map(self, prune_certainty_thre):
-        """model/neural_points.py:329-353."""
-        dtd = torch.abs(self.travel_dist[self.cur_ts] - self.travel_dist[self.point_ts_update])
-        prune = (dtd > self.diff_travel_dist_local) & (self.point_certainties < prune_certainty_thre)
-        count = int(prune.sum().item())
+        """model/neural_points.py:329-353.  HIP: pin_prune_rows + pin_map_gather."""
+        dev = self.neural_points.device
+        M = self.count()
+        td = self._travel_dist_dev(dev)
+        keep = torch.empty((max(M, 1),), dtype=torch.int64, device=dev)
+        cnt = torch.empty((1,), dtype=torch.int64, device=dev)
+        src = self._map_arrays(features=False)
+        _lib.call("pin_prune_rows", ctypes.byref(src), _lib.ptr(td), int(self.cur_ts),
+                  float(np.float32(self.diff_travel_dist_local)), float(np.float32(prune_certainty_thre)),
+                  _lib.ptr(keep), _lib.ptr(cnt), _lib.ptr(map_workspace(M, dev)), _lib.stream())
+        kept = int(cnt.item())
+        count = M - kept
         if count > 100:
             if not self.silence:
                 print("# Prune neural points: ", count)
-            keep = ~prune
-            self.neural_points = self.neural_points[keep]
-            self.point_orientations = self.point_orientations[keep]
-            self.point_ts_create = self.point_ts_create[keep]
-            self.point_ts_update = self.point_ts_update[keep]
-            self.point_certainties = self.point_certainties[keep]
-            self.geo_features = self.geo_features[torch.cat((keep, torch.ones(1, dtype=torch.bool,
-                                                                               device=keep.device)))]
+            self._select_global(keep, kept)
             return True
         return False
 
     def adjust_map(self, pose_diff_torch):
-        """model/neural_points.py:355-370: move every point by the pose correction of its frame."""
+        """model/neural_points.py:355-370: move every point by the pose correction of its frame
+        (new tensors, as the reference assigns new ones).  HIP: pin_map_adjust."""
         self.after_pgo = True
-        if self.config.use_mid_ts:
-            used_ts = ((self.point_ts_create + self.point_ts_update) / 2).long()
-        else:
-            used_ts = self.point_ts_create
-        T = pose_diff_torch[used_ts]
-        self.neural_points = (torch.matmul(T[:, :3, :3].to(self.neural_points),
-                                           self.neural_points.unsqueeze(-1))
-                              + T[:, :3, 3:].to(self.neural_points)).squeeze(-1)
-        dq = rotmat_to_quat(pose_diff_torch[:, :3, :3])
-        self.point_orientations = quat_multiply(dq[used_ts], self.point_orientations).to(self.dtype)
+        dev = self.neural_points.device
+        T = pose_diff_torch.detach().to(device=dev, dtype=torch.float32).contiguous()
+        pos = self.neural_points.clone()
+        quat = self.point_orientations.to(torch.float32).clone()
+        arr = _lib.PinMapArrays(positions=pos.data_ptr() if pos.numel() else None,
+                                orientations=quat.data_ptr() if quat.numel() else None,
+                                ts_create=self.point_ts_create.data_ptr() if pos.numel() else None,
+                                ts_update=self.point_ts_update.data_ptr() if pos.numel() else None,
+                                certainties=None, features=None, count=pos.shape[0], feature_dim=0, reserved=0)
+        _lib.call("pin_map_adjust", ctypes.byref(arr), _lib.ptr(T), T.shape[0], int(bool(self.config.use_mid_ts)),
+                  _lib.stream())
+        self.neural_points = pos
+        self.point_orientations = quat.to(self.dtype)
 
     def recreate_hash(self, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor,
                       kept_points: bool = True, with_ts: bool = True, cur_ts=0):
-        """model/neural_points.py:372-428."""
+        """model/neural_points.py:372-428.  HIP: pin_voxel_down_sample (min-value form), then
+        pin_hash_assign (kept points) or pin_map_gather + pin_hash_rebuild (merge)."""
         res = self.resolution
-        self.buffer_pt_index = torch.full((self.buffer_size,), -1, dtype=torch.int32, device=self.device)
+        dev = self.neural_points.device
+        self.buffer_pt_index.fill_(-1)
         if with_ts:
             if self.config.use_mid_ts:
                 ts_used = ((self.point_ts_create + self.point_ts_update) / 2).long()
             else:
                 ts_used = self.point_ts_create
-            sample_idx = voxel_down_sample_min_value(self.neural_points, res, torch.abs(ts_used - cur_ts).float())
+            value = torch.abs(ts_used - cur_ts).float()
         else:
-            sample_idx = voxel_down_sample_min_value(self.neural_points, res, -self.point_certainties)
+            value = -self.point_certainties
+        sample_idx = voxel_down_sample_min_value(self.neural_points, res, value)
+        n = sample_idx.shape[0]
         if kept_points:
-            slots = hash_slots(self.neural_points[sample_idx], res, self.buffer_size)
-            sel = last_writer(slots)
-            self.buffer_pt_index[slots[sel]] = sample_idx[sel].to(torch.int32)
+            pts = self.neural_points.contiguous()
+            _lib.call("pin_hash_assign", _lib.ptr(pts), _lib.ptr(sample_idx), n, float(np.float32(res)),
+                      _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.ptr(map_workspace(n, dev)),
+                      _lib.stream())
+            torch.autograd.graph.increment_version(self.buffer_pt_index)
         else:
-            self.neural_points = self.neural_points[sample_idx]
-            self.point_orientations = self.point_orientations[sample_idx]
-            self.point_ts_create = self.point_ts_create[sample_idx]
-            self.point_ts_update = self.point_ts_update[sample_idx]
-            self.point_certainties = self.point_certainties[sample_idx]
-            pad = torch.cat((sample_idx, torch.tensor([-1], device=sample_idx.device)))
-            self.geo_features = self.geo_features[pad]
+            self._select_global(sample_idx, n)
             self.rebuild_hash()
         if sensor_position is not None:
             self.reset_local_map(sensor_position, sensor_orientation, cur_ts)
@@ -545,6 +610,7 @@ class NeuralPoints(nn.Module):
         pts = self.neural_points.contiguous()
         _lib.call("pin_hash_rebuild", _lib.ptr(pts), pts.shape[0], float(np.float32(self.resolution)),
                   _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.stream())
+        torch.autograd.graph.increment_version(self.buffer_pt_index)
 
     def clear_temp(self, clean_more: bool = False):
         """model/neural_points.py:678-693."""
@@ -557,6 +623,7 @@ class NeuralPoints(nn.Module):
         self.local_point_ts_update = None
         self.local_mask = None
         self.global2local = None
+        self._local_rows = None
         self._cache = {}
         if clean_more:
             self.point_ts_create = None

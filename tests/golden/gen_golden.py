@@ -29,6 +29,8 @@ Reference call sites exercised (file:line in /root/reference):
   utils/tracker.py:176         query_source_points
   utils/tracker.py:277         registration_step / implicit_reg
   utils/mesher.py:41           query_points
+  model/neural_points.py:329   prune_map / :355 adjust_map / :372 recreate_hash
+  utils/tools.py:409,444       voxel_down_sample_torch / voxel_down_sample_min_value_torch
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
 """
@@ -492,6 +494,125 @@ def gen_mesher_case(name, cfg_kwargs, n_side, seed):
     print(name, "grid", voxel_num_xyz, "mask", int(mask.sum()))
 
 
+def scan_frame(center, radius, spacing, rng):
+    """A dense patch of the surface around ``center`` (several points per 0.3 m voxel, so the
+    down-sample has work to do), jittered."""
+    a = np.arange(-radius, radius, spacing)
+    X, Y = np.meshgrid(a + center[0], a + center[1], indexing="ij")
+    keep = (X - center[0]) ** 2 + (Y - center[1]) ** 2 < radius ** 2
+    x, y = X[keep], Y[keep]
+    pts = np.stack([x, y, surface_z(x, y)], 1).astype(np.float32)
+    pts += rng.normal(0, spacing * 0.3, pts.shape).astype(np.float32)
+    return pts
+
+
+def vds_cases(rng):
+    """Inputs for voxel_down_sample_torch / voxel_down_sample_min_value_torch (utils/tools.py
+    :409-477), including the degenerate ones the quantisation and key formulas meet."""
+    plane = np.stack(np.meshgrid(np.arange(0, 3, 0.07), np.arange(0, 3, 0.07), indexing="ij"), -1).reshape(-1, 2)
+    cases = {
+        "cloud": rng.uniform(-3, 3, (5000, 3)).astype(np.float32),
+        # c = (v, 0, 0) and (0, 1, 0) share a key: the v_size = grid.max() aliasing
+        "plane": np.concatenate([plane, np.zeros((plane.shape[0], 1))], 1).astype(np.float32),
+        "far": (rng.uniform(-2, 2, (3000, 3)) + np.array([1000.0, -2500.0, 30.0])).astype(np.float32),
+        "one": np.array([[0.1, 0.2, 0.3]], np.float32),
+        "same_voxel": rng.uniform(0.01, 0.29, (200, 3)).astype(np.float32),
+    }
+    values = {
+        "cloud": rng.integers(0, 7, 5000).astype(np.float32),
+        "plane": -rng.uniform(0, 5, plane.shape[0]).astype(np.float32),
+        "far": np.zeros(3000, np.float32),  # 0 / 0: NaN quantised values
+        "one": np.array([3.0], np.float32),
+        "same_voxel": rng.uniform(0, 1, 200).astype(np.float32),
+    }
+    return cases, values
+
+
+def gen_map_case(name, seed, use_mid_ts=False, fill_all=False):
+    """Map maintenance, on the reference's own code: a sequence of
+    NeuralPoints.update calls (model/neural_points.py:205-270; voxel down-sample, probe,
+    collisions in a small table, stale re-inserts after the travel distance grows), each
+    followed by reset_local_map (:272-313), then prune_map (:329-353), recreate_hash
+    (:372-428, both modes), adjust_map (:355-370), and the down-sample functions alone."""
+    rng = np.random.default_rng(seed)
+    # CPU index_put with repeated slots runs multi-threaded and then keeps an arbitrary writer
+    # (observed: ~1 in 10 runs of a frame differs); one thread gives its serial semantics, the
+    # last writer wins -- the rule restated by the oracle and the kernels
+    torch.set_num_threads(1)
+    cfg = make_config(buffer_size=1 << 15, local_map_radius=15.0)
+    cfg.local_map_travel_dist_ratio = 1.0
+    cfg.use_mid_ts = use_mid_ts
+    npm = NeuralPoints(cfg)
+    path = [(0.0, 0.0), (8.0, 0.0), (16.0, 3.0), (8.0, 1.0), (0.0, 0.0), (-8.0, -2.0)]
+    npm.travel_dist = torch.tensor([0.0, 8.0, 16.5, 25.0, 33.0, 41.5, 50.0], dtype=torch.float32)
+    rec = dict(buffer_size=np.int64(cfg.buffer_size), resolution=np.float32(cfg.voxel_size_m),
+               voxel_size_m=np.float64(cfg.voxel_size_m),
+               local_map_radius=np.float64(cfg.local_map_radius),
+               diff_travel_dist_local=np.float64(npm.diff_travel_dist_local), use_mid_ts=np.bool_(use_mid_ts),
+               travel_dist=npm.travel_dist.numpy().copy(), frames=np.int64(len(path)))
+    for f, (cx, cy) in enumerate(path):
+        pts = scan_frame((cx, cy), 9.0, 0.12, rng)
+        sensor = torch.tensor([cx, cy, 1.5], dtype=torch.float32)
+        sidx = rtools.voxel_down_sample_torch(torch.from_numpy(pts), cfg.voxel_size_m)
+        npm.update(torch.from_numpy(pts), sensor, torch.eye(3), f)
+        rec.update({f"f{f}_points": pts, f"f{f}_sensor": sensor.numpy(), f"f{f}_sample_idx": sidx.numpy(),
+                    f"f{f}_count": np.int64(npm.count()), f"f{f}_table": npm.buffer_pt_index.numpy().astype(np.int32),
+                    f"f{f}_local_mask": npm.local_mask.numpy().copy(),
+                    f"f{f}_global2local": npm.global2local.numpy().copy()})
+        print(name, "frame", f, "points", pts.shape[0], "samples", sidx.shape[0], "map", npm.count(),
+              "local", int(npm.local_mask.sum()) - 1)
+    last = len(path) - 1
+    rec.update(seq_positions=npm.neural_points.numpy().copy(), seq_orientations=npm.point_orientations.numpy().copy(),
+               seq_ts_create=npm.point_ts_create.numpy().copy(), seq_ts_update=npm.point_ts_update.numpy().copy(),
+               seq_certainties=npm.point_certainties.numpy().copy())
+    M = npm.count()
+    g = torch.Generator().manual_seed(seed)
+    # certainties and update times as mapping would leave them, then prune
+    npm.point_certainties = torch.rand(M, generator=g) * 4.0
+    npm.point_ts_update = torch.maximum(npm.point_ts_create, torch.randint(0, len(path), (M,), generator=g))
+    npm.geo_features = torch.randn(M + 1, cfg.feature_dim, generator=g)
+    rec.update(pre_certainties=npm.point_certainties.numpy().copy(), pre_ts_update=npm.point_ts_update.numpy().copy(),
+               pre_features=npm.geo_features.numpy().copy(), prune_thre=np.float64(1.5))
+    pruned = npm.prune_map(1.5)
+    rec.update(prune_done=np.bool_(pruned), prune_positions=npm.neural_points.numpy().copy(),
+               prune_orientations=npm.point_orientations.numpy().copy(),
+               prune_ts_create=npm.point_ts_create.numpy().copy(), prune_ts_update=npm.point_ts_update.numpy().copy(),
+               prune_certainties=npm.point_certainties.numpy().copy(), prune_features=npm.geo_features.numpy().copy())
+    sensor = torch.from_numpy(rec[f"f{last}_sensor"])
+    npm.recreate_hash(sensor, torch.eye(3), kept_points=True, with_ts=True, cur_ts=last)
+    rec.update(rehash_ts_table=npm.buffer_pt_index.numpy().astype(np.int32),
+               rehash_ts_local_mask=npm.local_mask.numpy().copy())
+    # pose corrections per frame, as after a loop closure (small SE(3) each)
+    T = torch.eye(4).repeat(len(path), 1, 1)
+    for f in range(len(path)):
+        ang = float(rng.normal(0, 0.02))
+        c, s_ = np.cos(ang), np.sin(ang)
+        T[f, :3, :3] = torch.tensor([[c, -s_, 0], [s_, c, 0], [0, 0, 1]], dtype=torch.float32)
+        T[f, :3, 3] = torch.from_numpy(rng.normal(0, 0.05, 3).astype(np.float32))
+    npm.point_orientations = torch.from_numpy(
+        np.asarray(random_quats(npm.count(), g).numpy(), np.float32))
+    rec.update(adjust_pose_diff=T.numpy().copy(), adjust_orientations_in=npm.point_orientations.numpy().copy())
+    npm.adjust_map(T)
+    rec.update(adjust_positions=npm.neural_points.numpy().copy(),
+               adjust_orientations=npm.point_orientations.numpy().copy())
+    npm.recreate_hash(sensor, torch.eye(3), kept_points=False, with_ts=False, cur_ts=last)
+    rec.update(merge_positions=npm.neural_points.numpy().copy(), merge_orientations=npm.point_orientations.numpy().copy(),
+               merge_ts_create=npm.point_ts_create.numpy().copy(), merge_ts_update=npm.point_ts_update.numpy().copy(),
+               merge_certainties=npm.point_certainties.numpy().copy(), merge_features=npm.geo_features.numpy().copy(),
+               merge_table=npm.buffer_pt_index.numpy().astype(np.int32), merge_local_mask=npm.local_mask.numpy().copy(),
+               merge_global2local=npm.global2local.numpy().copy())
+    print(name, "pruned", pruned, "after prune", rec["prune_positions"].shape[0], "after merge", npm.count())
+    cases, values = vds_cases(rng)
+    for key, pts in cases.items():
+        t = torch.from_numpy(pts)
+        rec[f"vds_{key}_points"] = pts
+        rec[f"vds_{key}_values"] = values[key]
+        rec[f"vds_{key}_idx"] = rtools.voxel_down_sample_torch(t, 0.3).numpy()
+        rec[f"vds_{key}_min_idx"] = rtools.voxel_down_sample_min_value_torch(t, 0.3, torch.from_numpy(values[key])).numpy()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    torch.set_num_threads(8)
+
+
 def gen_neighborhoods():
     cfg = make_config()
     npm = NeuralPoints(cfg)
@@ -508,7 +629,9 @@ def gen_neighborhoods():
 def main(only=None):
     if only:   # regenerate selected cases only, e.g.  gen_golden.py tracker_wf tracker_nwf
         cases = {"tracker_wf": lambda: gen_tracker_case("tracker_wf", dict(weighted_first=True), 3000, seed=6),
-                 "tracker_nwf": lambda: gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7)}
+                 "tracker_nwf": lambda: gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7),
+                 "map_seq": lambda: gen_map_case("map_seq", seed=9),
+                 "map_seq_mid": lambda: gen_map_case("map_seq_mid", seed=10, use_mid_ts=True)}
         for name in only:
             cases[name]()
         return
@@ -522,6 +645,8 @@ def main(only=None):
     gen_tracker_case("tracker_wf", dict(weighted_first=True), 3000, seed=6)
     gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7)
     gen_mesher_case("mesher_wf", dict(weighted_first=True), 60, seed=8)
+    gen_map_case("map_seq", seed=9)
+    gen_map_case("map_seq_mid", seed=10, use_mid_ts=True)
     with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
         for k, v in meta.items():
             f.write(f"{k}: {v}\n")

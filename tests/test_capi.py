@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     hdr = open(os.path.join(ROOT, "include", "pin_slam_amd.h")).read()
-    return sorted(set(re.findall(r"^int (pin_\w+)\(", hdr, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t) (pin_\w+)\(", hdr, flags=re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 STRUCTS = ["PinHash", "PinPoints", "PinGridDims", "PinGrid", "PinMlp", "PinRegParams", "PinTrainCfg",
-           "PinTrainState", "PinAdamStep"]
+           "PinTrainState", "PinAdamStep", "PinMapArrays"]
 
 
 def test_struct_layouts_match_header(tmp_path):
