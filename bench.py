@@ -86,6 +86,7 @@ def parse():
                          "fewer GPUs -- ranks then share devices round robin)")
     ap.add_argument("--no-tracker", action="store_true", help="skip the tracker leg (configs[2])")
     ap.add_argument("--no-mesher", action="store_true", help="skip the mesher leg (configs[4])")
+    ap.add_argument("--no-map-update", action="store_true", help="skip the map-maintenance leg (8f rank 1)")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -160,6 +161,7 @@ def time_kernel(nm, dec, q, wf, backend, steps):
 TRACKER_SRC = 200_000      # configs[2]: source points per registration step
 MESH_RES = 512             # configs[4]: 512^3 grid
 MESH_BATCH = 1 << 20       # Mesher infer_bs (utils/config.py:569: bs * 64)
+MAP_FRAME = 131_072        # 8f rank 1: points per scan frame (a 64-beam lidar sweep)
 
 
 def tracker_leg(nm, dec, pts, args, dev, world, rank):
@@ -240,6 +242,69 @@ def mesher_leg(nm, dec, pts, args, dev, world, rank):
             "ms_per_grid": el * 1e3, "scaling": "strong", "masked_fraction": float(mask.float().mean()),
             "config": {"workload": "512^3 grid at 0.1 m over the 1M-point map, SDF + mc_mask, batches of 2^20, "
                                    "z-slabs per rank (configs[4])"}}
+
+
+def map_leg(args, dev, world, rank):
+    """NeuralPoints.update per frame (voxel down-sample, hash probe +
+    insert, reset_local_map over the whole map + local gathers) of a 131,072-point scan
+    (50 m disk, the sensor advancing 2 m per frame) into the 1M-point surface map."""
+    from pin_slam_amd.synthetic import surface_scan
+    nm, _, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7))
+    nm.local_map_radius = 50.0
+    nm.diff_travel_dist_local = 250.0
+    nsteps = max(args.steps // 2, 5)
+    nw = 3
+    T = nw + nsteps
+    nm.travel_dist = torch.arange(T, dtype=torch.float32, device=dev) * 2.0
+    frames = [surface_scan(100.0 + 2.0 * k, 150.0, 50.0, MAP_FRAME, seed=100 + k + 1000 * rank, device=dev)
+              for k in range(T)]
+    sensors = [torch.tensor([100.0 + 2.0 * k, 150.0, 1.7], device=dev) for k in range(T)]
+    M0 = nm.count()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = map_cpu_baseline(nm, frames[0], sensors[0])
+    for k in range(nw):
+        nm.update(frames[k], sensors[k], None, k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(nw, T):
+        nm.update(frames[k], sensors[k], None, k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t[0])
+    res = {"metric": "map update frames/sec", "value": nsteps * world / el, "unit": "frames/s",
+           "points_per_sec": MAP_FRAME * nsteps * world / el, "ms_per_frame": el / nsteps * 1e3, "steps": nsteps,
+           "map_points_before": M0, "map_points_after": nm.count(), "local_points": nm.local_count(),
+           "scaling": "replicas",
+           "config": {"workload": "NeuralPoints.update (+ reset_local_map) of 131072-point scans into the 1M-point "
+                                  "surface map, 5e7-slot table, local radius 50 m (SURVEY.md 8f rank 1)",
+                      "note": "per frame: two host syncs (new-point and local-point counts size the new tensors)"}}
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
+    return res
+
+
+def map_cpu_baseline(nm, frame, sensor):
+    """The numpy oracle's map_update + reset_local_map of one frame into the same map (1 core)."""
+    from oracle import pin_oracle as O
+    c = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    st = O.empty_map(float(nm.resolution), nm.buffer_size, c(nm.travel_dist), float(nm.diff_travel_dist_local))
+    st.table = c(nm.buffer_pt_index).astype(np.int64)
+    st.points, st.orientations = c(nm.neural_points), c(nm.point_orientations)
+    st.ts_create, st.ts_update = c(nm.point_ts_create), c(nm.point_ts_update)
+    st.certainties, st.geo_features = c(nm.point_certainties), c(nm.geo_features)
+    f = c(frame)
+    t0 = time.perf_counter()
+    O.map_update(st, f, 0)
+    O.reset_local_map(st, c(sensor), 0, float(nm.local_map_radius))
+    el = time.perf_counter() - t0
+    return {"value": 1.0 / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "one 131072-point frame into the 1M-point map (oracle map_update + reset_local_map)"}
 
 
 def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
@@ -416,6 +481,8 @@ def main():
     if not args.no_tracker:   # last: it fits the map first
         out["tracker"] = tracker_leg(nm, dec, pts, args, dev, world, rank)
     del nm, dec, pts, q
+    if not args.no_map_update:
+        out["map_update"] = map_leg(args, dev, world, rank)
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)
     if rank == 0:

@@ -344,32 +344,38 @@ k_keep_flags(const int64_t* __restrict__ tu, const float* __restrict__ cert, int
 }
 
 // ----------------------------------------------------------------------------- gather / scatter
-// One thread per (row, 4-byte word) over the concatenated row payloads: every array moves as
-// coalesced 4-byte words; dst row i <- src row rows[i] (gather) or the reverse (scatter).
-struct Move {
-    const char* src;
-    char* dst;
-    int words;  // 4-byte words per row
-};
-
+// One thread per row: every array of the row moves with 16/8/4-byte loads and stores.  The
+// local / kept row lists are ascending, so neighbouring lanes touch neighbouring rows.
 template <bool SCATTER>
 __global__ void __launch_bounds__(kBlock)
-k_move_rows(const int64_t* __restrict__ rows, int64_t n_rows, Move m0, Move m1, Move m2, Move m3, Move m4, Move m5,
-            int total_words) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t i = t / total_words;
+k_move_rows(const int64_t* __restrict__ rows, int64_t n_rows, PinMapArrays src, PinMapArrays dst, uint32_t sel,
+            int F) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n_rows) return;
-    int w = (int)(t - i * total_words);
-    const Move ms[6] = {m0, m1, m2, m3, m4, m5};
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        if (w < ms[a].words) {
-            const int64_t r = rows[i];
-            const int64_t s_row = SCATTER ? i : r, d_row = SCATTER ? r : i;
-            ((uint32_t*)ms[a].dst)[d_row * ms[a].words + w] = ((const uint32_t*)ms[a].src)[s_row * ms[a].words + w];
-            return;
+    const int64_t r = rows[i];
+    const int64_t s = SCATTER ? i : r, d = SCATTER ? r : i;
+    if (sel & 1) {
+        const float* a = src.positions + 3 * s;
+        float* b = dst.positions + 3 * d;
+        const float x = a[0], y = a[1], z = a[2];
+        b[0] = x;
+        b[1] = y;
+        b[2] = z;
+    }
+    if (sel & 2) ((float4*)dst.orientations)[d] = ((const float4*)src.orientations)[s];
+    if (sel & 4) dst.ts_create[d] = src.ts_create[s];
+    if (sel & 8) dst.ts_update[d] = src.ts_update[s];
+    if (sel & 16) dst.certainties[d] = src.certainties[s];
+    if (sel & 32) {
+        if (F == 8) {
+            const float4* a = (const float4*)(src.features + 8 * s);
+            float4* b = (float4*)(dst.features + 8 * d);
+            const float4 u = a[0], v = a[1];
+            b[0] = u;
+            b[1] = v;
+        } else {
+            for (int k = 0; k < F; ++k) dst.features[(int64_t)F * d + k] = src.features[(int64_t)F * s + k];
         }
-        w -= ms[a].words;
     }
 }
 
@@ -381,27 +387,23 @@ int move_rows(const PinMapArrays* src, const PinMapArrays* dst, const int64_t* r
               bool scatter, hipStream_t s) {
     if (!src || !dst || n_rows < 0 || (n_rows > 0 && !rows)) return PIN_ERR_ARG;
     const PinMapArrays* sel = scatter ? src : dst;  // which side's non-NULL arrays choose what moves
-    const int F = (src->features && dst->features) ? (sel->feature_dim > 0 ? sel->feature_dim : kF) : 0;
-    Move m[6] = {};
-    int k = 0, total = 0;
-    auto add = [&](const void* a, void* b, int words, bool on) {
-        if (!on) return true;
-        if (!a || !b) return false;
-        m[k++] = Move{(const char*)a, (char*)b, words};
-        total += words;
-        return true;
-    };
-    bool ok = add(src->positions, dst->positions, 3, sel->positions != nullptr) &&
-              add(src->orientations, dst->orientations, 4, sel->orientations != nullptr) &&
-              add(src->ts_create, dst->ts_create, 2, sel->ts_create != nullptr) &&
-              add(src->ts_update, dst->ts_update, 2, sel->ts_update != nullptr) &&
-              add(src->certainties, dst->certainties, 1, sel->certainties != nullptr) &&
-              add(src->features, dst->features, F, sel->features != nullptr);
-    if (!ok) return PIN_ERR_ARG;
-    if (total > 0 && n_rows > 0)
-        hipLaunchKernelGGL(scatter ? k_move_rows<true> : k_move_rows<false>, dim3(blocks_for(n_rows * total)),
-                           dim3(kBlock), 0, s, rows, n_rows, m[0], m[1], m[2], m[3], m[4], m[5], total);
-    if (pad_row && F > 0 && sel->features) {
+    const void* a[6] = {src->positions, src->orientations, src->ts_create, src->ts_update, src->certainties,
+                        src->features};
+    const void* b[6] = {dst->positions, dst->orientations, dst->ts_create, dst->ts_update, dst->certainties,
+                        dst->features};
+    const void* c[6] = {sel->positions, sel->orientations, sel->ts_create, sel->ts_update, sel->certainties,
+                        sel->features};
+    uint32_t mask = 0;
+    for (int k = 0; k < 6; ++k) {
+        if (!c[k]) continue;
+        if (!a[k] || !b[k]) return PIN_ERR_ARG;
+        mask |= 1u << k;
+    }
+    const int F = sel->feature_dim > 0 ? sel->feature_dim : kF;
+    if (mask && n_rows > 0)
+        hipLaunchKernelGGL(scatter ? k_move_rows<true> : k_move_rows<false>, dim3(blocks_for(n_rows)), dim3(kBlock),
+                           0, s, rows, n_rows, *src, *dst, mask, F);
+    if (pad_row && (mask & 32)) {
         const int64_t srow = scatter ? n_rows : src->count, drow = scatter ? dst->count : n_rows;
         hipLaunchKernelGGL(k_copy_words, dim3(1), dim3(64), 0, s, (const uint32_t*)(src->features + srow * F),
                            (uint32_t*)(dst->features + drow * F), F);
@@ -466,7 +468,7 @@ int pin_voxel_down_sample(const float* points, int64_t n, float voxel_size, cons
     int64_t scale = 10;
     for (int64_t m = n - 1; m >= 10; m /= 10) scale *= 10;
     hipLaunchKernelGGL(k_vds_init, dim3(1), dim3(64), 0, s, st);
-    hipLaunchKernelGGL(k_vds_stats, dim3((unsigned)std::min<int64_t>(blocks_for(n), 1024)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(k_vds_stats, dim3((unsigned)std::min<int64_t>(blocks_for(n), 128)), dim3(kBlock), 0, s,
                        points, n, voxel_size, value, st);
     hipLaunchKernelGGL(k_vds_keys, dim3(blocks_for(n)), dim3(kBlock), 0, s, points, n, voxel_size, value, st, scale,
                        keys_a, pk_a);

@@ -48,6 +48,17 @@ def surface_map(n_side, res=0.3, seed=42, device="cuda", buffer_size=int(5e7), n
     return nm, dec, pts
 
 
+def surface_scan(cx, cy, radius, n, seed=0, sigma=0.02, device="cuda"):
+    """A lidar-like frame: n points area-uniform in a disk of ``radius`` around (cx, cy) on the
+    surface, z noise N(0, sigma^2).  Returns [n,3] f32 on ``device``."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r = radius * torch.sqrt(torch.rand(n, generator=g, dtype=torch.float64))
+    a = 2 * torch.pi * torch.rand(n, generator=g, dtype=torch.float64)
+    x, y = cx + r * torch.cos(a), cy + r * torch.sin(a)
+    z = 0.5 * torch.sin(x / 7.0) * torch.cos(y / 5.0) + 0.15 + sigma * torch.randn(n, generator=g, dtype=torch.float64)
+    return torch.stack([x, y, z], 1).to(torch.float32).to(device)
+
+
 def surface_queries(pts, n, seed=7, sigma=0.25, device="cuda"):
     g = torch.Generator(device="cpu").manual_seed(seed)
     idx = torch.randint(0, pts.shape[0], (n,), generator=g)
