@@ -438,7 +438,8 @@ int pin_prune_rows(const PinMapArrays* map, const float* travel_dist, int64_t cu
  * pin_map_gather -- dst.x[i] = src.x[rows[i]], i < n_rows, for every array non-NULL in dst
  * (boolean-mask / index selection of reset_local_map :293-309, prune_map :339-349 and
  * recreate_hash :414-421).  pad_row != 0 also copies the features padding row:
- * dst.features[n_rows] = src.features[src.count].  dst.count is not read.
+ * dst.features[n_rows] = src.features[src.count].  dst.count is not read.  A negative row
+ * index writes zeros (gather) or is skipped (scatter).
  */
 int pin_map_gather(const PinMapArrays* src, const int64_t* rows, int64_t n_rows, int32_t pad_row,
                    const PinMapArrays* dst, void* stream);

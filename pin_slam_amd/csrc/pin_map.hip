@@ -353,6 +353,18 @@ k_move_rows(const int64_t* __restrict__ rows, int64_t n_rows, PinMapArrays src, 
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n_rows) return;
     const int64_t r = rows[i];
+    if (r < 0) {   // no source row: a gather writes zeros, a scatter skips
+        if (SCATTER) return;
+        const int64_t d = i;
+        if (sel & 1) dst.positions[3 * d] = dst.positions[3 * d + 1] = dst.positions[3 * d + 2] = 0.f;
+        if (sel & 2) ((float4*)dst.orientations)[d] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (sel & 4) dst.ts_create[d] = 0;
+        if (sel & 8) dst.ts_update[d] = 0;
+        if (sel & 16) dst.certainties[d] = 0.f;
+        if (sel & 32)
+            for (int k = 0; k < F; ++k) dst.features[(int64_t)F * d + k] = 0.f;
+        return;
+    }
     const int64_t s = SCATTER ? i : r, d = SCATTER ? r : i;
     if (sel & 1) {
         const float* a = src.positions + 3 * s;
