@@ -71,7 +71,8 @@ typedef struct PinGrid {
     const float* crec;           /* [n_occ,4]: x, y, z, bits(id) of the cell's point (its record) */
     const int32_t* cgid;         /* [n_occ] global point index of each compact record */
     int64_t n_occ;
-    const int32_t* offsets;      /* [pin_cells_padded(Kc)] packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 */
+    const int32_t* offsets;      /* [pin_cells_padded(Kc)] packed (dx+128) | (dy+128)<<8 | (dz+128)<<16,
+                                    then num_columns column entries (see num_columns) */
     float resolution;
     int32_t num_cells;           /* Kc, reference cell order (model/neural_points.py:430-439) */
     float max_valid_dist2;
@@ -80,7 +81,10 @@ typedef struct PinGrid {
     int32_t fat;                 /* 1: features/certainty read from cfeat/ccert; 0: from PinPoints by id */
     int32_t window;              /* max |offset| component (num_nei_cells); <= 2 enables the
                                     brick-window scan (<= 8 bricks cover the neighbourhood) */
-    int32_t reserved;
+    int32_t num_columns;         /* 0, or the cells regrouped as (x, y) columns: entry c at
+                                    offsets[pin_cells_padded(Kc) + c] = (dx+128) | (dy+128)<<8 |
+                                    (dz0+128)<<16 | nz<<24 covers cells dz0 .. dz0+nz-1 of the
+                                    column; the columns in order list exactly the cells in order */
 } PinGrid;
 
 /* Geo decoder, hidden_level = 1 (model/decoder.py:16-88). */

@@ -44,7 +44,7 @@ class PinGridDims(ctypes.Structure):
 class PinGrid(ctypes.Structure):
     _fields_ = [("bricks", c_void_p), ("dims", PinGridDims), ("crec", c_void_p), ("cgid", c_void_p), ("n_occ", i64),
                 ("offsets", c_void_p), ("resolution", f32), ("num_cells", i32), ("max_valid_dist2", f32),
-                ("cfeat", c_void_p), ("ccert", c_void_p), ("fat", i32), ("window", i32), ("reserved", i32)]
+                ("cfeat", c_void_p), ("ccert", c_void_p), ("fat", i32), ("window", i32), ("num_columns", i32)]
 
 
 class PinRegParams(ctypes.Structure):

@@ -160,6 +160,12 @@ __device__ __forceinline__ uint32_t sel8(const uint32_t (&w)[8], int k) {
     return (k & 4) ? b1 : b0;
 }
 
+// one of 4 registers by a per-lane 2-bit index
+__device__ __forceinline__ uint32_t sel4(const uint32_t* w, int k) {
+    const uint32_t a0 = (k & 1) ? w[1] : w[0], a1 = (k & 1) ? w[3] : w[2];
+    return (k & 2) ? a1 : a0;
+}
+
 template <bool FAT>
 struct GridSource {
     static constexpr int kChunk = PIN_GRID_CHUNK;
@@ -218,6 +224,45 @@ struct GridSource {
         const int tid = threadIdx.x;
         const int Kc = gr.num_cells;
         int nn = 0;
+        if (gr.num_columns > 0) {
+            // Column scan: per (x, y) column of the neighbourhood, the column's 4-bit z nibbles
+            // of its two z-bricks give an 8-bit z-occupancy word; the column's cell run is a
+            // shifted window of it, so empty cells cost nothing and only occupied cells are
+            // ranked and listed (in the reference cell order: columns in order, z ascending).
+            const int32_t* __restrict__ cols = offs + ((Kc + 15) & ~15);
+            const int zr0 = lz - 4 * bz0;   // query z inside the 8-cell z span, 2..5
+            int cnt = 0;
+            for (int c = 0; c < gr.num_columns; ++c) {
+                const int col = cols[c];
+                const int nz = (col >> 24) & 255;
+                if (__any(cnt + nz > kSeg)) {   // list full: consume it first (only for Kc > 32)
+                    records_from_list<CH>(s_list, cnt, crec, qx, qy, qz, maxd2, tk, nn);
+                    cnt = 0;
+                }
+                const int cx = lx + ((col & 255) - 128);
+                const int cy = ly + (((col >> 8) & 255) - 128);
+                const int kxy = ((cx >> 2) - bx0) | (((cy >> 2) - by0) << 1);
+                const uint32_t lo0 = sel4(wl, kxy), hi0 = sel4(wh, kxy);
+                const uint32_t lo1 = sel4(wl + 4, kxy), hi1 = sel4(wh + 4, kxy);
+                const int sh = ((cx & 3) << 4) | ((cy & 3) << 2);
+                const uint32_t n0 = (uint32_t)((((uint64_t)hi0 << 32) | lo0) >> sh) & 15u;
+                const uint32_t n1 = (uint32_t)((((uint64_t)hi1 << 32) | lo1) >> sh) & 15u;
+                const int zs = zr0 + (((col >> 16) & 255) - 128);
+                uint32_t run = ((n0 | (n1 << 4)) >> zs) & ((1u << nz) - 1u);
+                while (run) {
+                    const int z = zs + __builtin_ctz(run);
+                    run &= run - 1u;
+                    const bool up = z >= 4;
+                    const uint64_t bits = up ? (((uint64_t)hi1 << 32) | lo1) : (((uint64_t)hi0 << 32) | lo0);
+                    const uint32_t pre = up ? sel4(wp + 4, kxy) : sel4(wp, kxy);
+                    const int bit = sh | (z & 3);
+                    s_list[cnt][tid] = (int)(pre + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
+                    ++cnt;
+                }
+            }
+            records_from_list<CH>(s_list, cnt, crec, qx, qy, qz, maxd2, tk, nn);
+            return nn;
+        }
         for (int s0 = 0; s0 < Kc; s0 += kSeg) {
             const int s1 = Kc < s0 + kSeg ? Kc : s0 + kSeg;
             int cnt = 0;
@@ -234,29 +279,38 @@ struct GridSource {
                     ++cnt;
                 }
             }
-            // trip count = the longest list among the ACTIVE lanes (__any ignores lanes that
-            // returned early in a partial last wave)
-            for (int j0 = 0; __any(j0 < cnt); j0 += CH) {
-                int ci[CH];
-#pragma unroll
-                for (int u = 0; u < CH; ++u) {
-                    const int v = s_list[j0 + u][tid];   // j0 + u < kSeg: stale slots are masked
-                    ci[u] = (j0 + u < cnt) ? v : -1;
-                }
-                float4 r[CH];
-#pragma unroll
-                for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
-#pragma unroll
-                for (int u = 0; u < CH; ++u) {
-                    const int id = __float_as_int(r[u].w);
-                    const float d2 = dist2(r[u].x, r[u].y, r[u].z, qx, qy, qz);
-                    const bool ok = ci[u] >= 0 && id != -1 && d2 <= maxd2;
-                    nn += ok ? 1 : 0;
-                    tk.insert(ok ? d2 : INFINITY, ci[u]);
-                }
-            }
+            records_from_list<CH>(s_list, cnt, crec, qx, qy, qz, maxd2, tk, nn);
         }
         return nn;
+    }
+
+    // Records of the lane's listed candidates, CH gathers per round trip; the trip count is the
+    // longest list among the ACTIVE lanes (__any ignores lanes that returned early in a partial
+    // last wave).
+    template <int CH>
+    __device__ __forceinline__ static void records_from_list(const int (*s_list)[kBlock], int cnt,
+                                                             const float4* __restrict__ crec, float qx, float qy,
+                                                             float qz, float maxd2, TopK& tk, int& nn) {
+        const int tid = threadIdx.x;
+        for (int j0 = 0; __any(j0 < cnt); j0 += CH) {
+            int ci[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int v = s_list[j0 + u < kSeg ? j0 + u : kSeg - 1][tid];   // stale slots are masked
+                ci[u] = (j0 + u < cnt) ? v : -1;
+            }
+            float4 r[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int id = __float_as_int(r[u].w);
+                const float d2 = dist2(r[u].x, r[u].y, r[u].z, qx, qy, qz);
+                const bool ok = ci[u] >= 0 && id != -1 && d2 <= maxd2;
+                nn += ok ? 1 : 0;
+                tk.insert(ok ? d2 : INFINITY, ci[u]);
+            }
+        }
     }
 
     // Per-cell scan (any window): CH cell lookups back to back, then CH record gathers.

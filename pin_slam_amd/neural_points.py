@@ -36,6 +36,27 @@ from .query import QueryFeatureFn, hash_view, points_view
 PRIMES = (73856093, 19349669, 83492791)
 
 
+def neighbor_columns(dx: np.ndarray):
+    """The neighbour cells regrouped as (x, y) columns for the column scan of the grid kernels:
+    entries (dx+128) | (dy+128)<<8 | (dz0+128)<<16 | nz<<24, one per run of consecutive cells with
+    the same (dx, dy) and dz ascending by 1.  Visiting the columns in order visits the cells in
+    the reference order (meshgrid 'ij', model/neural_points.py:430-439).  None when a column
+    would repeat (not a ball) or a run exceeds 5 cells."""
+    cols, seen = [], set()
+    i = 0
+    while i < len(dx):
+        x, y, z0 = (int(v) for v in dx[i])
+        j = i + 1
+        while j < len(dx) and int(dx[j][0]) == x and int(dx[j][1]) == y and int(dx[j][2]) == z0 + (j - i):
+            j += 1
+        if (x, y) in seen or j - i > 5:
+            return None
+        seen.add((x, y))
+        cols.append((x + 128) | ((y + 128) << 8) | ((z0 + 128) << 16) | ((j - i) << 24))
+        i = j
+    return cols
+
+
 def neighbor_offsets(num_nei_cells: int, search_alpha: float, device=None) -> torch.Tensor:
     """Integer cell offsets inside the (c + alpha) sphere, in meshgrid 'ij' order
     (model/neural_points.py:430-439)."""
@@ -212,12 +233,17 @@ class NeuralPoints(nn.Module):
         return self._cells
 
     def _offset_table(self):
-        """Packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 per neighbour cell, reference order."""
+        """Packed (dx+128) | (dy+128)<<8 | (dz+128)<<16 per neighbour cell, reference order, padded
+        to 16 entries, then the column table of PinGrid.num_columns (see neighbor_columns)."""
         if self._offsets is None:
             dx = self._cells_host.astype(np.int64)
             packed = (dx[:, 0] + 128) | ((dx[:, 1] + 128) << 8) | ((dx[:, 2] + 128) << 16)
             pad = np.zeros((self.neighbor_K + 15) // 16 * 16, dtype=np.int32)
             pad[:self.neighbor_K] = packed
+            cols = neighbor_columns(dx) if self.neighbor_window <= 2 else None
+            self._num_columns = 0 if cols is None else len(cols)
+            if cols is not None:
+                pad = np.concatenate([pad, np.asarray(cols, dtype=np.int64).astype(np.int32)])
             self._offsets = torch.from_numpy(pad).to(self.device)
         return self._offsets
 
@@ -361,7 +387,7 @@ class NeuralPoints(nn.Module):
                          num_cells=int(self.neighbor_K), max_valid_dist2=float(np.float32(self.max_valid_dist2)),
                          cfeat=cfeat.data_ptr() if cfeat is not None else None,
                          ccert=ccert.data_ptr() if ccert is not None else None, fat=int(fat), window=99 if os.environ.get("PIN_GRID_SCAN") == "cells" else self.neighbor_window,
-                         reserved=0)
+                         num_columns=0 if os.environ.get("PIN_GRID_SCAN") == "bricks" else self._num_columns)
         return _View(g, (bricks, crec, cfeat, ccert, cgid, offs))
 
     # ------------------------------------------------------------------ map maintenance
