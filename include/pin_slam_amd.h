@@ -247,7 +247,7 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
 
 /* Workspace bytes of pin_query_order for n queries. */
 static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
-    return 4 * 1024 * ((n + 8191) / 8192 + 1);
+    return 4 * 1024 * ((n + 1023) / 1024 + 1);
 }
 
 /*

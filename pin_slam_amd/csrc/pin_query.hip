@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "pin_device.h"
@@ -361,6 +362,12 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
 // outputs still go to its own index, so results are unchanged.
 constexpr int kMaxTiles = 1024;
 constexpr int kPartThreads = 1024;   // one thread per tile in the scatter's prefix step
+#ifndef PIN_PART_BATCH
+#define PIN_PART_BATCH 64                // count-matrix rows loaded per round trip in the scatter
+#endif
+#ifndef PIN_PART_ROWS
+#define PIN_PART_ROWS 64                 // max count-matrix rows (blocks) before PER doubles
+#endif
 
 struct TileMap {
     int64_t ox, oy, oz;
@@ -423,21 +430,17 @@ k_part_scatter(const float* __restrict__ q, int64_t n, TileMap t, const int* __r
     const int k = threadIdx.x;
     int pre = 0, tot = 0;
     if (k < t.ntiles) {
-        int b = 0;
-        for (; b + 4 <= nblk; b += 4) {
-            int v[4];
+        // all rows of the column in flight, PIN_PART_BATCH at a time (nblk <= ~100)
+        for (int b = 0; b < nblk; b += PIN_PART_BATCH) {
+            int v[PIN_PART_BATCH];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = cnt[(int64_t)(b + u) * t.ntiles + k];
+            for (int u = 0; u < PIN_PART_BATCH; ++u)
+                v[u] = b + u < nblk ? cnt[(int64_t)(b + u) * t.ntiles + k] : 0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < PIN_PART_BATCH; ++u) {
                 tot += v[u];
                 pre += b + u < (int)blockIdx.x ? v[u] : 0;
             }
-        }
-        for (; b < nblk; ++b) {
-            const int v = cnt[(int64_t)b * t.ntiles + k];
-            tot += v;
-            pre += b < (int)blockIdx.x ? v : 0;
         }
     }
     int incl = tot;
@@ -492,15 +495,20 @@ int partition_queries(const PinGrid& g, const float* q, int64_t n, void* workspa
     const TileMap t = tile_map(g);
     order = out;
     int* cnt = (int*)workspace;
-    if (n <= (int64_t)64 * 8 * kPartThreads) {
-        const int nblk = (int)((n + 8 * kPartThreads - 1) / (8 * kPartThreads));
-        hipLaunchKernelGGL(k_part_count<8>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
-        hipLaunchKernelGGL(k_part_scatter<8>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
-    } else {
-        const int nblk = (int)((n + 16 * kPartThreads - 1) / (16 * kPartThreads));
-        hipLaunchKernelGGL(k_part_count<16>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
-        hipLaunchKernelGGL(k_part_scatter<16>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
-    }
+    // the fewest queries per thread that keep the count matrix within PIN_PART_ROWS rows
+    // (each scatter thread reads its tile's whole column)
+    auto launch = [&](auto per_tag) {
+        constexpr int PER = decltype(per_tag)::value;
+        const int nblk = (int)((n + PER * kPartThreads - 1) / (PER * kPartThreads));
+        hipLaunchKernelGGL(k_part_count<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
+        hipLaunchKernelGGL(k_part_scatter<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
+    };
+    const int64_t rows = PIN_PART_ROWS;
+    if (n <= rows * 1 * kPartThreads) launch(std::integral_constant<int, 1>());
+    else if (n <= rows * 2 * kPartThreads) launch(std::integral_constant<int, 2>());
+    else if (n <= rows * 4 * kPartThreads) launch(std::integral_constant<int, 4>());
+    else if (n <= rows * 8 * kPartThreads) launch(std::integral_constant<int, 8>());
+    else launch(std::integral_constant<int, 16>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

@@ -127,7 +127,7 @@ def query_order(gv, q):
     """pin_query_order: a tile-grouped processing order for the queries q [N,3] (device int32)."""
     n = q.shape[0]
     order = torch.empty((n,), dtype=torch.int32, device=q.device)
-    ws = torch.empty((1024 * ((n + 8191) // 8192 + 1),), dtype=torch.int32, device=q.device)
+    ws = torch.empty((1024 * ((n + 1023) // 1024 + 1),), dtype=torch.int32, device=q.device)  # pin_query_order_workspace_bytes / 4
     _lib.call("pin_query_order", gv.ref(), _lib.ptr(q), n, _lib.ptr(order), _lib.ptr(ws), _lib.stream())
     return order
 

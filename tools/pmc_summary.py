@@ -14,7 +14,7 @@ def main(root, match=""):
             name = r["Kernel_Name"]
             if match and match not in name:
                 continue
-            short = name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+            short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             agg[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))
     for (k, c), v in sorted(agg.items()):
         print(f"{k[:60]:60s} {c:28s} n={len(v):3d} mean={sum(v) / len(v):.6g}")

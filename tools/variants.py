@@ -30,13 +30,13 @@ def run(args):
         for lib in libs:
             env = dict(os.environ, PIN_LIB=os.path.join(OUT, lib))
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-mapper", "--no-cpu-baseline",
-                                "--no-tracker", "--no-mesher", *args], env=env, capture_output=True, text=True,
+                                "--no-tracker", "--no-mesher", "--no-map-update", *args], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
                 print(lib, "FAILED", r.stderr[-2000:])
                 sys.exit(1)
             d = json.loads(r.stdout.strip().splitlines()[-1])
-            print(f"rep{rep} {lib:24s} {d['value'] / 1e9:.3f} Gq/s  kernel {d['roofline']['kernel_ms'] * 1e3:.1f} us",
+            print(f"rep{rep} {lib:24s} {d['value'] / 1e9:.3f} Gq/s  kernel {d['roofline']['kernel_ms'] * 1e3:.1f} us  order {d['roofline'].get('order_pass_ms', 0) * 1e3:.1f} us",
                   flush=True)
 
 
