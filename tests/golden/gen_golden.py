@@ -31,6 +31,7 @@ Reference call sites exercised (file:line in /root/reference):
   utils/mesher.py:41           query_points
   model/neural_points.py:329   prune_map / :355 adjust_map / :372 recreate_hash
   utils/tools.py:409,444       voxel_down_sample_torch / voxel_down_sample_min_value_torch
+  utils/tools.py:224           save_implicit_map (pin_map_ref.pth: the reference's own map file)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
 """
@@ -613,6 +614,35 @@ def gen_map_case(name, seed, use_mid_ts=False, fill_all=False):
     torch.set_num_threads(8)
 
 
+def gen_pin_map_case(name="pin_map_ref", seed=12):
+    """A map file written by the reference itself (utils/tools.py:224-238 save_implicit_map):
+    a pickled NeuralPoints + geo decoder state_dict, small table so the file stays small, plus
+    the reference's SDF/gradient over the saved map (query_locally True and False) to check a
+    loaded map end to end."""
+    import shutil
+    import tempfile
+    cfg = make_config(buffer_size=1 << 13, local_map_radius=6.0)
+    npm, _ = build_map(cfg, 40, seed)
+    npm.reset_local_map(torch.tensor([1.0, -1.0, 0.0]), torch.eye(3), 9)
+    npm.local_geo_features.data += 0.01   # local copy differs from the global one
+    dec = decoder(cfg)
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "model"))
+        rtools.save_implicit_map(tmp, npm, dec)
+        shutil.copy(os.path.join(tmp, "model", "pin_map.pth"), os.path.join(OUT, f"{name}.pth"))
+    q = make_queries(npm, cfg, 600, seed)
+    rec = dict(queries=q)
+    for ql in (0, 1):
+        o = run_query(npm, dec, cfg, q, query_locally=bool(ql))
+        rec[f"q{ql}_sdf"], rec[f"q{ql}_grad"], rec[f"q{ql}_nn_counts"] = o["sdf"], o["grad"], o["nn_counts"]
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec["local_features"] = npm.local_geo_features.detach().numpy().copy()
+    rec["local_neural_points"] = npm.local_neural_points.numpy().copy()
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "points", npm.count(), "local", npm.local_count())
+
+
 def gen_neighborhoods():
     cfg = make_config()
     npm = NeuralPoints(cfg)
@@ -631,7 +661,8 @@ def main(only=None):
         cases = {"tracker_wf": lambda: gen_tracker_case("tracker_wf", dict(weighted_first=True), 3000, seed=6),
                  "tracker_nwf": lambda: gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7),
                  "map_seq": lambda: gen_map_case("map_seq", seed=9),
-                 "map_seq_mid": lambda: gen_map_case("map_seq_mid", seed=10, use_mid_ts=True)}
+                 "map_seq_mid": lambda: gen_map_case("map_seq_mid", seed=10, use_mid_ts=True),
+                 "pin_map_ref": lambda: gen_pin_map_case()}
         for name in only:
             cases[name]()
         return
@@ -647,6 +678,7 @@ def main(only=None):
     gen_mesher_case("mesher_wf", dict(weighted_first=True), 60, seed=8)
     gen_map_case("map_seq", seed=9)
     gen_map_case("map_seq_mid", seed=10, use_mid_ts=True)
+    gen_pin_map_case()
     with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
         for k, v in meta.items():
             f.write(f"{k}: {v}\n")
