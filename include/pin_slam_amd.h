@@ -464,6 +464,39 @@ int pin_map_scatter(const PinMapArrays* src, const int64_t* rows, int64_t n_rows
 int pin_map_adjust(const PinMapArrays* map, const float* pose_diff, int64_t num_poses, int32_t use_mid_ts,
                    void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Training samples along the scan rays (utils/data_sampler.py:20-192) + pose transform
+ * (utils/mapper.py:133-215 via transform_torch, utils/tools.py:386-399).
+ * Scalars that the reference evaluates in Python double before touching a tensor are passed
+ * pre-rounded to f32. */
+typedef struct PinSampleCfg {
+    int32_t surface_n, front_n, behind_n;  /* surface_sample_n, free_front_n, free_behind_n */
+    float surface_range;         /* surface_sample_range_m */
+    float two_range;             /* f32(2.0 * surface_sample_range_m)  (sigma_ratio * range) */
+    float front_min_ratio;       /* free_sample_begin_ratio */
+    float end_dist;              /* free_sample_end_dist_m */
+    int32_t dist_weight_on;      /* weight = dist_weight_base - (d / max_range) * dist_weight_scale */
+    float dist_weight_base;      /* f32(1 + dist_weight_scale * 0.5) */
+    float dist_weight_scale;
+    float max_range;
+    int32_t behind_dropoff_on;   /* weight *= clamp((dropoff_max - disp) / dropoff_diff, 0, 1) * 0.8 + 0.2 */
+    float dropoff_max;           /* free_sample_end_dist_m */
+    float dropoff_diff;          /* f32(end - 0.2 * end) */
+    const float* pose;           /* [4,4] row-major f32 sensor pose (device), read if global_coord */
+} PinSampleCfg;
+
+/*
+ * pin_sample_rays -- DataSampler.sample (utils/data_sampler.py:20-192) for n rays (points in the
+ * sensor frame): writes n * (1 + surface_n + front_n + behind_n) rows in the reference's ray-wise
+ * order: coord [rows,3] (sensor frame), sdf_label [rows], weight [rows] (negative = free space),
+ * and, if global_coord != NULL, transform_torch(coord, pose) [rows,3].  randn_surface [surface_n*n],
+ * rand_front [front_n*n], rand_behind [behind_n*n] are the reference's draws (torch.randn /
+ * torch.rand, part-major).
+ */
+int pin_sample_rays(const float* points, int64_t n, const float* randn_surface, const float* rand_front,
+                    const float* rand_behind, const PinSampleCfg* cfg, float* coord, float* sdf_label, float* weight,
+                    float* global_coord, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

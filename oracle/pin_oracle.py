@@ -659,6 +659,82 @@ def adjust_map(st: MapState, pose_diff: np.ndarray, use_mid_ts: bool = False) ->
     st.orientations = quat_multiply(dq[used], st.orientations).astype(np.float32)
 
 
+# ---------------------------------------------------------------- training samples
+def fma32(a, b, c):
+    """f32 fused multiply-add (the f32 product is exact in f64; the sum is rounded once more
+    to f32 -- double rounding can differ from a true fma in rare halfway cases)."""
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
+def sample_rays(points: np.ndarray, randn_surface: np.ndarray, rand_front: np.ndarray, rand_behind: np.ndarray,
+                surface_n: int, front_n: int, behind_n: int, surface_range: float, front_min_ratio: float,
+                end_dist: float, dist_weight_on: bool, dist_weight_scale: float, max_range: float,
+                behind_dropoff_on: bool):
+    """utils/data_sampler.py:20-192 (DataSampler.sample) given its random draws, in f32 with the
+    reference's op order.  Python-double scalar subexpressions are rounded once to f32 (as
+    torch does when they meet a float tensor); ``scalar / tensor`` is Tensor.__rtruediv__ =
+    reciprocal(tensor) * scalar.  Returns (coord [N*A,3], sdf_label [N*A], weight [N*A]) in the
+    final ray-wise order (:165-171)."""
+    f = np.float32
+    p = points.astype(f)
+    n = p.shape[0]
+    d = np.sqrt(fma32(p[:, 2], p[:, 2], fma32(p[:, 1], p[:, 1], p[:, 0] * p[:, 0])))   # :43, torch's CPU norm
+    inv = f(1.0) / d
+    two_range = f(2.0 * surface_range)
+    disp_parts, ratio_parts, surf_parts = [np.zeros(n, f)], [np.ones(n, f)], [np.ones(n, bool)]   # :45-46
+    rs = randn_surface.astype(f).reshape(surface_n, n)
+    for k in range(surface_n):                                                        # :50-53
+        disp = rs[k] * f(surface_range)
+        disp_parts.append(disp)
+        ratio_parts.append(disp / d + f(1.0))
+        surf_parts.append(np.ones(n, bool))
+    rf = rand_front.astype(f).reshape(front_n, n)
+    for k in range(front_n):                                                          # :72-78
+        fmax = f(1.0) - inv * two_range
+        fdiff = fmax - f(front_min_ratio)
+        ratio = rf[k] * fdiff + f(front_min_ratio)
+        ratio_parts.append(ratio)
+        disp_parts.append((ratio - f(1.0)) * d)
+        surf_parts.append(np.zeros(n, bool))
+    rb = rand_behind.astype(f).reshape(behind_n, n)
+    for k in range(behind_n):                                                         # :85-91
+        bmax = inv * f(end_dist) + f(1.0)
+        bmin = f(1.0) + inv * two_range
+        ratio = rb[k] * (bmax - bmin) + bmin
+        ratio_parts.append(ratio)
+        disp_parts.append((ratio - f(1.0)) * d)
+        surf_parts.append(np.zeros(n, bool))
+    A = 1 + surface_n + front_n + behind_n
+    disp = np.stack(disp_parts, 1)          # [n, A]: ray-wise order
+    ratio = np.stack(ratio_parts, 1)
+    surf = np.stack(surf_parts, 1)
+    coord = p[:, None, :] * ratio[..., None]                                          # :106
+    w = np.ones((n, A), f)
+    if dist_weight_on:                                                                # :120-121
+        wd = f(1 + dist_weight_scale * 0.5) - (d / f(max_range)) * f(dist_weight_scale)
+        w = np.where(surf, wd[:, None], w)
+    if behind_dropoff_on:                                                             # :125-134
+        dmin, dmax = 0.2 * end_dist, end_dist
+        dw = (f(dmax) - disp) / f(dmax - dmin)
+        dw = np.clip(dw, f(0.0), f(1.0)) * f(0.8) + f(0.2)
+        w = w * dw
+    w = np.where(surf, w, w * f(-1.0))                                                # :137
+    return coord.reshape(n * A, 3).astype(f), (disp * f(-1.0)).reshape(-1).astype(f), w.reshape(-1).astype(f)
+
+
+def transform_points(points: np.ndarray, pose: np.ndarray) -> np.ndarray:
+    """utils/tools.py:386-399 transform_torch: [p, 1] @ T^T with T cast to the points' f32; the
+    CPU sgemm accumulates x, y, z, 1 in order with fused multiply-adds."""
+    f = np.float32
+    T = pose.astype(f)
+    p = points.astype(f)
+    out = np.empty_like(p)
+    for a in range(3):
+        acc = fma32(p[:, 2], T[a, 2], fma32(p[:, 1], T[a, 1], p[:, 0] * T[a, 0]))
+        out[:, a] = acc + T[a, 3]
+    return out
+
+
 # ---------------------------------------------------------------- fixture helpers
 def map_from_fixture(z, prefix: str = "map_") -> MapState:
     g = lambda k: z[prefix + k]  # noqa: E731

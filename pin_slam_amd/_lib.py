@@ -41,6 +41,13 @@ class PinGridDims(ctypes.Structure):
     _fields_ = [("ox", i64), ("oy", i64), ("oz", i64), ("nbx", i32), ("nby", i32), ("nbz", i32), ("reserved", i32)]
 
 
+class PinSampleCfg(ctypes.Structure):
+    _fields_ = [("surface_n", i32), ("front_n", i32), ("behind_n", i32), ("surface_range", f32), ("two_range", f32),
+                ("front_min_ratio", f32), ("end_dist", f32), ("dist_weight_on", i32), ("dist_weight_base", f32),
+                ("dist_weight_scale", f32), ("max_range", f32), ("behind_dropoff_on", i32), ("dropoff_max", f32),
+                ("dropoff_diff", f32), ("pose", c_void_p)]
+
+
 class PinGrid(ctypes.Structure):
     _fields_ = [("bricks", c_void_p), ("dims", PinGridDims), ("crec", c_void_p), ("cgid", c_void_p), ("n_occ", i64),
                 ("offsets", c_void_p), ("resolution", f32), ("num_cells", i32), ("max_valid_dist2", f32),
@@ -109,6 +116,8 @@ _SIGS = {
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_sample_rays": [c_void_p, i64, c_void_p, c_void_p, c_void_p, _P(PinSampleCfg), c_void_p, c_void_p, c_void_p,
+                        c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_rows": [c_void_p, _P(PinTrainCfg), c_void_p, c_void_p],

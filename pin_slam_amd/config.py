@@ -33,6 +33,32 @@ class Config:
         self.pos_input_dim = 3
         self.color_on = False
         self.semantic_on = False
+        # sampler + data pool (:139-154, :205-207)
+        self.surface_sample_n = 3
+        self.free_sample_begin_ratio = 0.3
+        self.free_sample_end_dist_m = 1.0
+        self.free_front_n = 2
+        self.free_behind_n = 1
+        self.dist_weight_on = True
+        self.dist_weight_scale = 0.8
+        self.behind_dropoff_on = False
+        self.window_radius = 50.0
+        self.pool_capacity = int(1e7)
+        self.bs_new_sample = 2048
+        self.new_certainty_thre = 1.0
+        self.pool_filter_freq = 10
+        self.new_sample_ratio_thre = 0.01
+        self.adaptive_mode = False
+        self.from_sample_points = True
+        self.from_all_samples = False
+        self.map_surface_ratio = 0.5
+        self.prune_map_on = False
+        self.max_prune_certainty = 2.0
+        self.dynamic_certainty_thre = 4.0
+        self.dynamic_sdf_ratio_thre = 1.5
+        self.pgo_on = False
+        self.track_on = False
+        self.color_channel = 0
         # decoder (:179-198)
         self.mlp_bias_on = True
         self.geo_mlp_level = 1
@@ -80,3 +106,5 @@ class Config:
             self.infer_bs = self.bs * 64            # utils/config.py:569
         if "local_map_radius" not in overrides:
             self.local_map_radius = self.max_range + 2.0  # utils/config.py:574
+        if "window_radius" not in overrides:
+            self.window_radius = max(self.max_range, 6.0)  # utils/config.py:572

@@ -27,7 +27,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_order
+from .data_sampler import DataSampler
+from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_order, query_sdf
 
 
 def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -84,6 +85,8 @@ class Mapper:
             self.require_gradient = False
         self.total_iter = 0
         self.sdf_scale = config.logistic_gaussian_ratio * config.sigma_sigmoid_m
+        self.sampler = DataSampler(config)
+        self.ray_sample_count = 1 + config.surface_sample_n + config.free_behind_n + config.free_front_n
         self.new_idx = None
         self.ba_done_flag = False
         self.train_less = False
@@ -103,6 +106,123 @@ class Mapper:
         self._adam_t = 0
 
     # ---------------------------------------------------------------- data pool
+    def dynamic_filter(self, points_torch, type_2_on: bool = False):
+        """utils/mapper.py:79-108 (strategy 1): measurements in confidently free space are
+        dynamic.  One fused query (local map, SDF + certainty) instead of query_feature + sdf."""
+        if type_2_on:
+            raise NotImplementedError("dynamic_filter type_2 (gradient-norm test) is not on the fused path")
+        sdf, _, _, cert, _ = query_sdf(self.neural_points, self.geo_mlp, points_torch, query_locally=True,
+                                       want_grad=False, want_certainty=True)
+        c = self.config
+        return (cert < c.dynamic_certainty_thre) | (sdf < c.dynamic_sdf_ratio_thre * c.voxel_size_m)
+
+    def _used_poses(self):
+        """utils/mapper.py:205-211."""
+        ds, c = self.dataset, self.config
+        if ds is None:
+            return self.used_poses
+        if getattr(c, "pgo_on", False):
+            return torch.tensor(np.array(ds.pgo_poses), device=self.device, dtype=torch.float64)
+        if getattr(c, "track_on", False):
+            return torch.tensor(np.array(ds.odom_poses), device=self.device, dtype=torch.float64)
+        if getattr(ds, "gt_pose_provided", False):
+            return torch.tensor(np.array(ds.gt_poses), device=self.device, dtype=torch.float64)
+        return self.used_poses
+
+    def process_frame(self, point_cloud_torch, frame_label_torch, cur_pose_torch, frame_id: int,
+                      filter_dynamic: bool = False, draws=None):
+        """utils/mapper.py:110-321: sample the frame's rays (one fused launch, samples in the sensor
+        and the world frame), grow the neural-point map with the near-surface samples, append to
+        the data pool, window-filter the pool every pool_filter_freq frames and mark the new,
+        uncertain near-surface samples (query_certainty) for get_batch.  ``draws`` replays given
+        sampler draws (tests)."""
+        c = self.config
+        frame_origin = cur_pose_torch[:3, 3]
+        frame_orientation = cur_pose_torch[:3, :3]
+        frame_point = point_cloud_torch[:, :3]
+        self.static_mask = torch.ones(frame_point.shape[0], dtype=torch.bool, device=self.device)
+        if filter_dynamic:                                                               # :124-131
+            from .tracker import transform_torch
+            self.static_mask = self.dynamic_filter(transform_torch(frame_point, cur_pose_torch))
+            frame_point = frame_point[self.static_mask]
+        frame_color = None
+        if getattr(c, "color_on", False):
+            frame_color = point_cloud_torch[:, 3:]
+            if filter_dynamic:
+                frame_color = frame_color[self.static_mask]
+        if frame_label_torch is not None and filter_dynamic:
+            frame_label_torch = frame_label_torch[self.static_mask]
+        coord, sdf_label, normal_label, sem_label, color_label, weight, global_coord = self.sampler.sample(
+            frame_point, None, frame_label_torch, frame_color, pose=cur_pose_torch, draws=draws)   # :149-151
+        time_repeat = torch.full((coord.shape[0],), int(frame_id), dtype=torch.long, device=self.device)
+        self.cur_sample_count = sdf_label.shape[0]
+        self.pool_sample_count = self.sdf_label_pool.shape[0]
+        if getattr(c, "from_sample_points", True):                                       # :163-171
+            if getattr(c, "from_all_samples", False):
+                update_points = coord
+            else:   # transform of the selected rows == the selected rows of the transform (row-wise)
+                update_points = global_coord[torch.abs(sdf_label) < c.surface_sample_range_m * c.map_surface_ratio, :]
+        else:
+            from .tracker import transform_torch
+            update_points = transform_torch(frame_point, cur_pose_torch)
+        if getattr(c, "prune_map_on", False):                                            # :174-176
+            if self.neural_points.prune_map(c.max_prune_certainty):
+                self.neural_points.recreate_hash(None, None, True, True, frame_id)
+        self.neural_points.update(update_points, frame_origin, frame_orientation, frame_id)   # :177
+        self.coord_pool = torch.cat((self.coord_pool, coord), 0)                         # :185-188
+        self.weight_pool = torch.cat((self.weight_pool, weight), 0)
+        self.sdf_label_pool = torch.cat((self.sdf_label_pool, sdf_label), 0)
+        self.time_pool = torch.cat((self.time_pool, time_repeat), 0)
+        self.sem_label_pool = None if sem_label is None else (
+            sem_label if self.sem_label_pool is None else torch.cat((self.sem_label_pool, sem_label.to(
+                self.sem_label_pool.dtype)), 0))
+        self.color_pool = None if color_label is None else (
+            color_label if self.color_pool is None else torch.cat((self.color_pool, color_label), 0))
+        self.normal_label_pool = None
+        self.used_poses = self._used_poses()                                             # :205-211
+        if self.ba_done_flag:                                                            # :214-217
+            self.global_coord_pool = transform_batch_torch(self.coord_pool, self.used_poses[self.time_pool])
+            self.ba_done_flag = False
+        else:
+            self.global_coord_pool = torch.cat((self.global_coord_pool, global_coord), 0)
+        if (frame_id + 1) % int(c.pool_filter_freq) == 0:                                # :226-262
+            rel = self.global_coord_pool - frame_origin.to(self.global_coord_pool)
+            filter_mask = torch.sum(rel ** 2, dim=-1) < c.window_radius ** 2
+            true_indices = torch.nonzero(filter_mask).squeeze()
+            pool_sample_count = true_indices.shape[0]
+            if pool_sample_count > c.pool_capacity:
+                discard_count = pool_sample_count - int(c.pool_capacity)
+                discarded_index = torch.randint(0, pool_sample_count, (discard_count,), device=self.device)
+                filter_mask[true_indices[discarded_index]] = False
+            self.coord_pool = self.coord_pool[filter_mask]
+            self.global_coord_pool = self.global_coord_pool[filter_mask]
+            self.sdf_label_pool = self.sdf_label_pool[filter_mask]
+            self.weight_pool = self.weight_pool[filter_mask]
+            self.time_pool = self.time_pool[filter_mask]
+            if sem_label is not None:
+                self.sem_label_pool = self.sem_label_pool[filter_mask]
+            if color_label is not None:
+                self.color_pool = self.color_pool[filter_mask]
+            cur_sample_filter_mask = filter_mask[-self.cur_sample_count:]
+            self.cur_sample_count = int(cur_sample_filter_mask.sum().item())
+            self.pool_sample_count = int(filter_mask.sum().item())
+        else:
+            self.cur_sample_count = coord.shape[0]
+            self.pool_sample_count = self.coord_pool.shape[0]
+        if int(getattr(c, "bs_new_sample", 0)) > 0:                                      # :269-304
+            cur = self.global_coord_pool[-self.cur_sample_count:]
+            cur_label = self.sdf_label_pool[-self.cur_sample_count:]
+            nm = self.neural_points
+            nm.set_search_neighborhood(num_nei_cells=1, search_alpha=0.0)
+            cert = nm.query_certainty(cur) if cur.shape[0] > 0 else torch.zeros(0, device=self.device)
+            nm.set_search_neighborhood(num_nei_cells=c.num_nei_cells, search_alpha=c.search_alpha)
+            self.new_idx = torch.where((cert < c.new_certainty_thre) &
+                                       (torch.abs(cur_label) < c.surface_sample_range_m * 3.0))[0]
+            self.new_idx += (self.pool_sample_count - self.cur_sample_count)
+            new_sample_count = self.new_idx.shape[0]
+            self.train_less = bool(getattr(c, "adaptive_mode", False) and
+                                   new_sample_count / max(self.cur_sample_count, 1) < c.new_sample_ratio_thre)
+
     def set_pool(self, coord, sdf_label, ts, weight=None, global_coord=None):
         """Install a training-sample pool (the output of Mapper.process_frame, utils/mapper.py:110-321)."""
         self.coord_pool = coord

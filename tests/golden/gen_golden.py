@@ -32,6 +32,8 @@ Reference call sites exercised (file:line in /root/reference):
   model/neural_points.py:329   prune_map / :355 adjust_map / :372 recreate_hash
   utils/tools.py:409,444       voxel_down_sample_torch / voxel_down_sample_min_value_torch
   utils/tools.py:224           save_implicit_map (pin_map_ref.pth: the reference's own map file)
+  utils/data_sampler.py:20     DataSampler.sample (random draws recorded) + utils/tools.py:386 transform_torch
+  utils/mapper.py:110          Mapper.process_frame (sampler draws recorded per frame)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
 """
@@ -643,6 +645,134 @@ def gen_pin_map_case(name="pin_map_ref", seed=12):
     print(name, "points", npm.count(), "local", npm.local_count())
 
 
+class _RecordingTorch:
+    """Stands in for the torch module inside utils/data_sampler.py: everything delegates to torch,
+    and the random draws (randn / rand) are recorded in call order."""
+
+    def __init__(self):
+        self.draws = []
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    def randn(self, *a, **kw):
+        t = torch.randn(*a, **kw)
+        self.draws.append(("randn", t.clone()))
+        return t
+
+    def rand(self, *a, **kw):
+        t = torch.rand(*a, **kw)
+        self.draws.append(("rand", t.clone()))
+        return t
+
+
+def scan_points(n, seed):
+    """Sensor-frame points of a synthetic lidar sweep (ranges 2..60 m, some near the sensor)."""
+    rng = np.random.default_rng(seed)
+    az = rng.uniform(-np.pi, np.pi, n)
+    el = rng.uniform(-0.4, 0.1, n)
+    r = rng.uniform(2.0, 60.0, n)
+    r[:16] = rng.uniform(0.5, 1.2, 16)     # close to the sensor: free-space ratios go negative
+    p = np.stack([r * np.cos(el) * np.cos(az), r * np.cos(el) * np.sin(az), r * np.sin(el)], 1)
+    return p.astype(np.float32)
+
+
+def gen_sampler_case(name, seed, **cfg_over):
+    """utils/data_sampler.py:20-192 (DataSampler.sample) with its random draws recorded, plus the
+    pose transform of the samples (utils/tools.py:386-399 transform_torch)."""
+    import utils.data_sampler as rds
+    cfg = make_config()
+    for k, v in cfg_over.items():
+        setattr(cfg, k, v)
+    sampler = rds.DataSampler(cfg)
+    pts = torch.from_numpy(scan_points(3000, seed))
+    rec_torch = _RecordingTorch()
+    real = rds.torch
+    rds.torch = rec_torch
+    try:
+        torch.manual_seed(seed)
+        coord, sdf_label, normal, sem, color, weight = sampler.sample(pts, None, None, None)
+    finally:
+        rds.torch = real
+    kinds = [k for k, _ in rec_torch.draws]
+    assert kinds == ["randn", "rand", "rand"], kinds
+    yaw = 0.3
+    pose = np.eye(4)
+    pose[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
+    pose[:3, 3] = [12.5, -3.25, 1.75]
+    pose_t = torch.from_numpy(pose)
+    glob = rtools.transform_torch(coord, pose_t)
+    rec = dict(points=pts.numpy(), randn_surface=rec_torch.draws[0][1].numpy().ravel(),
+               rand_front=rec_torch.draws[1][1].numpy().ravel(), rand_behind=rec_torch.draws[2][1].numpy().ravel(),
+               coord=coord.numpy(), sdf_label=sdf_label.numpy(), weight=weight.numpy(), pose=pose,
+               global_coord=glob.numpy())
+    for k in ["surface_sample_range_m", "surface_sample_n", "free_front_n", "free_behind_n", "free_sample_begin_ratio",
+              "free_sample_end_dist_m", "dist_weight_on", "dist_weight_scale", "max_range", "behind_dropoff_on"]:
+        rec[f"cfg_{k}"] = np.asarray(getattr(cfg, k))
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "rows", coord.shape[0])
+
+
+def gen_process_frame_case(name="process_frame", seed=15, frames=4):
+    """utils/mapper.py:110-321 Mapper.process_frame over a few frames into an empty map (sampler
+    draws recorded per frame; pool filter every 2nd frame, no capacity discards), with the pool,
+    new_idx and map after every frame."""
+    import types as _types
+    import utils.data_sampler as rds
+    cfg = make_config(buffer_size=1 << 16, local_map_radius=30.0)
+    cfg.track_on = True
+    cfg.pool_filter_freq = 2
+    cfg.window_radius = 40.0
+    cfg.max_range = 60.0
+    npm = NeuralPoints(cfg)
+    npm.travel_dist = torch.arange(frames, dtype=torch.float32) * 3.0
+    poses = []
+    for k in range(frames):
+        yaw = 0.05 * k
+        T = np.eye(4)
+        T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
+        T[:3, 3] = [3.0 * k, 0.5 * k, 0.1 * k]
+        poses.append(T)
+    dataset = _types.SimpleNamespace(odom_poses=poses, pgo_poses=poses, gt_poses=poses, gt_pose_provided=False,
+                                     stop_status=False)
+    dec = decoder(cfg)
+    mapper = rmapper.Mapper(cfg, dataset, npm, dec, None, None)
+    rec = {}
+    for k in range(frames):
+        pts = torch.from_numpy(scan_points(1500, seed + k))
+        rt = _RecordingTorch()
+        real = rds.torch
+        rds.torch = rt
+        try:
+            torch.manual_seed(seed + 100 + k)
+            mapper.process_frame(pts, None, torch.from_numpy(poses[k]), k)
+        finally:
+            rds.torch = real
+        rec[f"f{k}_points"] = pts.numpy()
+        rec[f"f{k}_randn_surface"] = rt.draws[0][1].numpy().ravel()
+        rec[f"f{k}_rand_front"] = rt.draws[1][1].numpy().ravel()
+        rec[f"f{k}_rand_behind"] = rt.draws[2][1].numpy().ravel()
+        rec[f"f{k}_pose"] = poses[k]
+        rec[f"f{k}_coord_pool"] = mapper.coord_pool.numpy().copy()
+        rec[f"f{k}_global_coord_pool"] = mapper.global_coord_pool.numpy().copy()
+        rec[f"f{k}_sdf_label_pool"] = mapper.sdf_label_pool.numpy().copy()
+        rec[f"f{k}_weight_pool"] = mapper.weight_pool.numpy().copy()
+        rec[f"f{k}_time_pool"] = mapper.time_pool.numpy().copy()
+        rec[f"f{k}_new_idx"] = mapper.new_idx.numpy().copy()
+        rec[f"f{k}_neural_points"] = npm.neural_points.numpy().copy()
+        rec[f"f{k}_point_certainties"] = npm.point_certainties.numpy().copy()
+        rec[f"f{k}_pool_sample_count"] = np.int64(mapper.pool_sample_count)
+        rec[f"f{k}_cur_sample_count"] = np.int64(mapper.cur_sample_count)
+    rec["frames"] = np.int64(frames)
+    rec["travel_dist"] = npm.travel_dist.numpy()
+    for k in ["buffer_size", "local_map_radius", "pool_filter_freq", "window_radius", "max_range",
+              "surface_sample_range_m", "voxel_size_m", "bs_new_sample", "new_certainty_thre", "map_surface_ratio",
+              "local_map_travel_dist_ratio", "pool_capacity"]:
+        rec[f"cfg_{k}"] = np.asarray(getattr(cfg, k))
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "pool", mapper.pool_sample_count, "points", npm.count(), "new", mapper.new_idx.shape[0])
+
+
 def gen_neighborhoods():
     cfg = make_config()
     npm = NeuralPoints(cfg)
@@ -662,7 +792,12 @@ def main(only=None):
                  "tracker_nwf": lambda: gen_tracker_case("tracker_nwf", dict(weighted_first=False, nn_k=6), 3000, seed=7),
                  "map_seq": lambda: gen_map_case("map_seq", seed=9),
                  "map_seq_mid": lambda: gen_map_case("map_seq_mid", seed=10, use_mid_ts=True),
-                 "pin_map_ref": lambda: gen_pin_map_case()}
+                 "pin_map_ref": lambda: gen_pin_map_case(),
+                 "sampler": lambda: (gen_sampler_case("sampler_default", 13),
+                                     gen_sampler_case("sampler_dropoff", 14, behind_dropoff_on=True, surface_sample_n=4,
+                                                      free_front_n=3, free_behind_n=2, free_sample_end_dist_m=1.5,
+                                                      dist_weight_on=False, surface_sample_range_m=0.3)),
+                 "process_frame": lambda: gen_process_frame_case()}
         for name in only:
             cases[name]()
         return
@@ -679,6 +814,10 @@ def main(only=None):
     gen_map_case("map_seq", seed=9)
     gen_map_case("map_seq_mid", seed=10, use_mid_ts=True)
     gen_pin_map_case()
+    gen_sampler_case("sampler_default", 13)
+    gen_sampler_case("sampler_dropoff", 14, behind_dropoff_on=True, surface_sample_n=4, free_front_n=3,
+                     free_behind_n=2, free_sample_end_dist_m=1.5, dist_weight_on=False, surface_sample_range_m=0.3)
+    gen_process_frame_case()
     with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
         for k, v in meta.items():
             f.write(f"{k}: {v}\n")

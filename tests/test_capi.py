@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 STRUCTS = ["PinHash", "PinPoints", "PinGridDims", "PinGrid", "PinMlp", "PinRegParams", "PinTrainCfg",
-           "PinTrainState", "PinAdamStep", "PinMapArrays"]
+           "PinTrainState", "PinAdamStep", "PinMapArrays", "PinSampleCfg"]
 
 
 def test_struct_layouts_match_header(tmp_path):

@@ -1,0 +1,130 @@
+"""Training samples and the data pool: DataSampler.sample
+(utils/data_sampler.py:20-192), transform_torch (utils/tools.py:386-399) and Mapper.process_frame
+(utils/mapper.py:110-321).
+
+Fixtures: tests/golden/sampler_*.npz and process_frame.npz, produced by the reference itself with
+its random draws recorded (tests/golden/gen_golden.py); the kernels replay the same draws.
+Tolerance: bit-exact for samples, labels, weights, world coordinates, pools, new_idx and the map
+(elementwise f32 work in the reference's op order, incl. torch's CPU fma norm and sgemm chain).
+Not pinned: the pool's capacity discards (torch.randint over the window-filtered pool) -- the
+fixture's pool never exceeds pool_capacity.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pin_oracle as O
+
+SAMPLER_CASES = ["sampler_default", "sampler_dropoff"]
+
+
+def _oracle_sample(z):
+    c = lambda k: z["cfg_" + k].item()  # noqa: E731
+    return O.sample_rays(z["points"], z["randn_surface"], z["rand_front"], z["rand_behind"], c("surface_sample_n"),
+                         c("free_front_n"), c("free_behind_n"), c("surface_sample_range_m"),
+                         c("free_sample_begin_ratio"), c("free_sample_end_dist_m"), c("dist_weight_on"),
+                         c("dist_weight_scale"), c("max_range"), c("behind_dropoff_on"))
+
+
+@pytest.mark.parametrize("case", SAMPLER_CASES)
+def test_oracle_sampler_matches_reference(golden, case):
+    z = golden(case)
+    coord, label, w = _oracle_sample(z)
+    np.testing.assert_array_equal(coord, z["coord"])
+    np.testing.assert_array_equal(label, z["sdf_label"])
+    np.testing.assert_array_equal(w, z["weight"])
+    np.testing.assert_array_equal(O.transform_points(z["coord"], z["pose"]), z["global_coord"])
+
+
+def _config(z, dev, **extra):
+    import pin_slam_amd as P
+    c = lambda k: z["cfg_" + k].item()  # noqa: E731
+    kw = dict(surface_sample_n=c("surface_sample_n"), free_front_n=c("free_front_n"), free_behind_n=c("free_behind_n"),
+              surface_sample_range_m=c("surface_sample_range_m"), free_sample_begin_ratio=c("free_sample_begin_ratio"),
+              free_sample_end_dist_m=c("free_sample_end_dist_m"), dist_weight_on=c("dist_weight_on"),
+              dist_weight_scale=c("dist_weight_scale"), max_range=c("max_range"),
+              behind_dropoff_on=c("behind_dropoff_on"))
+    kw.update(extra)
+    return P.Config(device=dev, **kw)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return "cuda"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", SAMPLER_CASES)
+def test_sample_rays_kernel_matches_reference(golden, dev, case):
+    from pin_slam_amd.data_sampler import DataSampler
+    z = golden(case)
+    cfg = _config(z, dev)
+    s = DataSampler(cfg)
+    t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    draws = (t(z["randn_surface"]), t(z["rand_front"]), t(z["rand_behind"]))
+    coord, label, normal, sem, color, w, glob = s.sample(t(z["points"]), None, None, None, pose=t(z["pose"]),
+                                                         draws=draws)
+    assert normal is None and sem is None and color is None
+    np.testing.assert_array_equal(coord.cpu().numpy(), z["coord"])
+    np.testing.assert_array_equal(label.cpu().numpy(), z["sdf_label"])
+    np.testing.assert_array_equal(w.cpu().numpy(), z["weight"])
+    np.testing.assert_array_equal(glob.cpu().numpy(), z["global_coord"])
+
+
+@pytest.mark.gpu
+def test_sample_rays_draw_order_and_labels(dev):
+    """Without replayed draws the sampler consumes the generator like the reference (randn, rand,
+    rand), and sem / color labels follow the reference's layout (free samples 0)."""
+    import pin_slam_amd as P
+    from pin_slam_amd.data_sampler import DataSampler
+    cfg = P.Config(device=dev)
+    s = DataSampler(cfg)
+    pts = torch.randn(100, 3, device=dev) * 10
+    sem = torch.arange(100, device=dev)
+    col = torch.rand(100, 3, device=dev)
+    torch.manual_seed(3)
+    out = s.sample(pts, None, sem, col)
+    torch.manual_seed(3)
+    d = (torch.randn(300, 1, device=dev), torch.rand(200, 1, device=dev), torch.rand(100, 1, device=dev))
+    ref = s.sample(pts, None, sem, col, draws=d)
+    for a, b in zip(out, ref):
+        if a is not None:
+            assert torch.equal(a, b)
+    A = 7
+    semr = out[3].reshape(100, A)
+    assert torch.equal(semr[:, :4], sem.int().unsqueeze(1).expand(100, 4)) and int(semr[:, 4:].abs().sum()) == 0
+    colr = out[4].reshape(100, A, 3)
+    assert torch.equal(colr[:, 2], col) and float(colr[:, 4:].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+def test_process_frame_matches_reference(golden, dev):
+    import types
+    import pin_slam_amd as P
+    z = golden("process_frame")
+    c = lambda k: z["cfg_" + k].item()  # noqa: E731
+    cfg = P.Config(device=dev, buffer_size=c("buffer_size"), local_map_radius=c("local_map_radius"),
+                   pool_filter_freq=c("pool_filter_freq"), window_radius=c("window_radius"), max_range=c("max_range"),
+                   surface_sample_range_m=c("surface_sample_range_m"), voxel_size_m=c("voxel_size_m"),
+                   bs_new_sample=c("bs_new_sample"), new_certainty_thre=c("new_certainty_thre"),
+                   map_surface_ratio=c("map_surface_ratio"), local_map_travel_dist_ratio=c("local_map_travel_dist_ratio"),
+                   pool_capacity=c("pool_capacity"), track_on=True, query_nn_k=8)
+    nm = P.NeuralPoints(cfg)
+    nm.travel_dist = torch.as_tensor(z["travel_dist"], device=dev)
+    F = int(z["frames"])
+    poses = [z[f"f{k}_pose"] for k in range(F)]
+    ds = types.SimpleNamespace(odom_poses=poses, stop_status=False, gt_pose_provided=False)
+    dec = P.Decoder(cfg, 64, 1, 1)
+    mapper = P.Mapper(cfg, ds, nm, dec)
+    t = lambda a: torch.as_tensor(a, device=dev)  # noqa: E731
+    for k in range(F):
+        draws = (t(z[f"f{k}_randn_surface"]), t(z[f"f{k}_rand_front"]), t(z[f"f{k}_rand_behind"]))
+        mapper.process_frame(t(z[f"f{k}_points"]), None, t(poses[k]), k, draws=draws)
+        for name in ["coord_pool", "global_coord_pool", "sdf_label_pool", "weight_pool", "time_pool", "new_idx"]:
+            np.testing.assert_array_equal(getattr(mapper, name).cpu().numpy(), z[f"f{k}_{name}"], err_msg=f"{name} @{k}")
+        np.testing.assert_array_equal(nm.neural_points.cpu().numpy(), z[f"f{k}_neural_points"])
+        np.testing.assert_array_equal(nm.point_certainties.cpu().numpy(), z[f"f{k}_point_certainties"])
+        assert mapper.pool_sample_count == int(z[f"f{k}_pool_sample_count"])
+        assert mapper.cur_sample_count == int(z[f"f{k}_cur_sample_count"])
