@@ -87,6 +87,7 @@ def parse():
     ap.add_argument("--no-tracker", action="store_true", help="skip the tracker leg (configs[2])")
     ap.add_argument("--no-mesher", action="store_true", help="skip the mesher leg (configs[4])")
     ap.add_argument("--no-map-update", action="store_true", help="skip the map-maintenance leg (8f rank 1)")
+    ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -289,6 +290,81 @@ def map_leg(args, dev, world, rank):
     return res
 
 
+FRAME_RAYS = 65_536         # 8f rank 4: rays per mapping frame (a down-sampled 64-beam sweep)
+
+
+def process_frame_leg(args, dev, world, rank):
+    """Mapper.process_frame per frame -- DataSampler.sample of 65,536 rays
+    (7 samples each, sensor + world frame in one launch), NeuralPoints.update with the near-surface
+    samples, data-pool append, window filter every 10th frame, query_certainty of the new samples
+    -- on the 1M-point surface map, the sensor advancing 2 m per frame."""
+    import types
+    from pin_slam_amd.synthetic import surface_scan
+    nm, dec, pts = surface_map(N_SIDE, device=dev, buffer_size=int(5e7))
+    cfg = nm.config
+    cfg.bs_new_sample = 2048
+    cfg.pool_filter_freq = 10
+    cfg.track_on = True
+    nsteps = max(args.steps // 2, 10)
+    nw = 3
+    T = nw + nsteps
+    nm.local_map_radius = 50.0
+    nm.diff_travel_dist_local = 250.0
+    nm.travel_dist = torch.arange(T, dtype=torch.float32, device=dev) * 2.0
+    poses, frames = [], []
+    for k in range(T):
+        c = np.array([100.0 + 2.0 * k, 150.0, 1.7])
+        pose = np.eye(4)
+        pose[:3, 3] = c
+        poses.append(pose)
+        w = surface_scan(c[0], c[1], 50.0, FRAME_RAYS, seed=300 + k + 1000 * rank, device=dev)
+        frames.append((w - torch.as_tensor(c, dtype=torch.float32, device=dev)).contiguous())
+    ds = types.SimpleNamespace(odom_poses=poses, stop_status=False, gt_pose_provided=False)
+    mapper = P.Mapper(cfg, ds, nm, dec)
+    pose_t = [torch.as_tensor(p, device=dev) for p in poses]
+    for k in range(nw):
+        mapper.process_frame(frames[k], None, pose_t[k], k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(nw, T):
+        mapper.process_frame(frames[k], None, pose_t[k], k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t[0])
+    res = {"metric": "mapper frames/sec (process_frame)", "value": nsteps * world / el, "unit": "frames/s",
+           "samples_per_sec": FRAME_RAYS * mapper.ray_sample_count * nsteps * world / el,
+           "ms_per_frame": el / nsteps * 1e3, "steps": nsteps, "pool_samples": int(mapper.pool_sample_count),
+           "map_points": nm.count(), "new_samples": int(mapper.new_idx.shape[0]), "scaling": "replicas",
+           "config": {"workload": "Mapper.process_frame: 65536-ray frames, 7 samples/ray, into the 1M-point surface "
+                                  "map (SURVEY.md 8f rank 4)"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = sampler_cpu_baseline(cfg, frames[0])
+    return res
+
+
+def sampler_cpu_baseline(cfg, frame):
+    """The numpy oracle's DataSampler.sample + transform of one frame (1 core); map update and
+    pool bookkeeping excluded (the map_update leg times the former)."""
+    from oracle import pin_oracle as O
+    f = frame.cpu().numpy()
+    n = f.shape[0]
+    rng = np.random.default_rng(0)
+    rs, rf, rb = rng.normal(size=3 * n).astype(np.float32), rng.random(2 * n, np.float32), rng.random(n, np.float32)
+    t0 = time.perf_counter()
+    coord, _, _ = O.sample_rays(f, rs, rf, rb, 3, 2, 1, cfg.surface_sample_range_m, cfg.free_sample_begin_ratio,
+                                cfg.free_sample_end_dist_m, cfg.dist_weight_on, cfg.dist_weight_scale, cfg.max_range,
+                                cfg.behind_dropoff_on)
+    O.transform_points(coord, np.eye(4))
+    el = time.perf_counter() - t0
+    return {"value": 1.0 / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "oracle sample_rays + transform of one 65536-ray frame (sampling only)"}
+
+
 def map_cpu_baseline(nm, frame, sensor):
     """The numpy oracle's map_update + reset_local_map of one frame into the same map (1 core)."""
     from oracle import pin_oracle as O
@@ -483,6 +559,8 @@ def main():
     del nm, dec, pts, q
     if not args.no_map_update:
         out["map_update"] = map_leg(args, dev, world, rank)
+    if not args.no_process_frame:
+        out["process_frame"] = process_frame_leg(args, dev, world, rank)
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)
     if rank == 0:

@@ -497,6 +497,15 @@ int pin_sample_rays(const float* points, int64_t n, const float* randn_surface, 
                     const float* rand_behind, const PinSampleCfg* cfg, float* coord, float* sdf_label, float* weight,
                     float* global_coord, void* stream);
 
+/*
+ * pin_deskew -- deskewing (utils/tools.py:540-567) in place: rows of `stride` floats whose first
+ * three are x, y, z; ts [n] point times, ts_minmax [2] = (min, max) of ts (device, e.g.
+ * torch.aminmax); pose [4,4] row-major f32 (T_last<-cur).  s = (ts - min) / (max - min) -
+ * ts_mid_pose; p <- exp(s log R) p + s t  (roma.rotmat_slerp(I, R, s), Rodrigues in f32).
+ */
+int pin_deskew(float* points, int64_t n, int64_t stride, const float* ts, const float* ts_minmax, const float* pose,
+               float ts_mid_pose, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

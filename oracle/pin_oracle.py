@@ -735,6 +735,49 @@ def transform_points(points: np.ndarray, pose: np.ndarray) -> np.ndarray:
     return out
 
 
+def rotmat_to_rotvec(R: np.ndarray) -> np.ndarray:
+    """roma.rotmat_to_rotvec (roma 1.x, not installed here; its published algorithm): unit
+    quaternion from the largest of (trace, diagonal) branch, w >= 0, then 2 atan2(|v|, w) v/|v|."""
+    R = R.astype(np.float64)
+    tr = np.trace(R)
+    cand = [tr, R[0, 0], R[1, 1], R[2, 2]]
+    k = int(np.argmax(cand))
+    if k == 0:
+        q = [1 + tr, R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]]
+    elif k == 1:
+        q = [R[2, 1] - R[1, 2], 1 + R[0, 0] - R[1, 1] - R[2, 2], R[0, 1] + R[1, 0], R[0, 2] + R[2, 0]]
+    elif k == 2:
+        q = [R[0, 2] - R[2, 0], R[0, 1] + R[1, 0], 1 + R[1, 1] - R[0, 0] - R[2, 2], R[1, 2] + R[2, 1]]
+    else:
+        q = [R[1, 0] - R[0, 1], R[0, 2] + R[2, 0], R[1, 2] + R[2, 1], 1 + R[2, 2] - R[0, 0] - R[1, 1]]
+    q = np.asarray(q) / np.linalg.norm(q)
+    if q[0] < 0:
+        q = -q
+    vn = np.linalg.norm(q[1:])
+    return q[1:] * (2 * np.arctan2(vn, q[0]) / vn if vn > 1e-12 else 2.0)
+
+
+def rotvec_to_rotmat(w: np.ndarray) -> np.ndarray:
+    th = np.linalg.norm(w)
+    K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+    if th < 1e-8:
+        return np.eye(3) + K + 0.5 * K @ K
+    return np.eye(3) + np.sin(th) / th * K + (1 - np.cos(th)) / th ** 2 * K @ K
+
+
+def deskewing(points: np.ndarray, ts: np.ndarray, pose: np.ndarray, ts_mid_pose: float = 0.5) -> np.ndarray:
+    """utils/tools.py:540-567 in f64: s = normalised ts - ts_mid; R(s) = roma.rotmat_slerp(I, R, s)
+    = exp(s log R); p <- R(s) p + s t.  PARITY UNPINNED: roma is absent here, so this follows
+    roma's published algorithm, not outputs of the reference."""
+    t = ts.reshape(-1).astype(np.float64)
+    s = (t - t.min()) / (t.max() - t.min()) - ts_mid_pose
+    w = rotmat_to_rotvec(pose[:3, :3])
+    out = points.astype(np.float64).copy()
+    for i in range(out.shape[0]):
+        out[i, :3] = rotvec_to_rotmat(s[i] * w) @ out[i, :3] + s[i] * pose[:3, 3]
+    return out
+
+
 # ---------------------------------------------------------------- fixture helpers
 def map_from_fixture(z, prefix: str = "map_") -> MapState:
     g = lambda k: z[prefix + k]  # noqa: E731

@@ -116,6 +116,7 @@ _SIGS = {
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_deskew": [c_void_p, i64, i64, c_void_p, c_void_p, c_void_p, f32, c_void_p],
     "pin_sample_rays": [c_void_p, i64, c_void_p, c_void_p, c_void_p, _P(PinSampleCfg), c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p],
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,

@@ -98,3 +98,75 @@ int pin_sample_rays(const float* points, int64_t n, const float* randn_surface, 
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ deskewing (utils/tools.py:540-567)
+// Per point: s = (ts - min) / (max - min) - ts_mid; R(s) = exp(s log R_pose) (roma.rotmat_slerp from
+// the identity: the relative rotation's rotation vector scaled by s, Rodrigues), t(s) = s t_pose;
+// p <- R(s) p + t(s) for the first three channels of each row, in place (the reference aliases
+// its input).  log R is taken through the unit quaternion (largest-component branch), as roma
+// does, then 2 atan2(|v|, w) v / |v|.
+namespace {
+
+__device__ __forceinline__ void rotmat_to_rotvec(const float* T, float& wx, float& wy, float& wz) {
+    const float r00 = T[0], r01 = T[1], r02 = T[2], r10 = T[4], r11 = T[5], r12 = T[6], r20 = T[8], r21 = T[9],
+                r22 = T[10];
+    const float tr = r00 + r11 + r22;
+    float qw, qx, qy, qz;
+    if (tr >= r00 && tr >= r11 && tr >= r22) {
+        qw = 1.0f + tr; qx = r21 - r12; qy = r02 - r20; qz = r10 - r01;
+    } else if (r00 >= r11 && r00 >= r22) {
+        qw = r21 - r12; qx = 1.0f + r00 - r11 - r22; qy = r01 + r10; qz = r02 + r20;
+    } else if (r11 >= r22) {
+        qw = r02 - r20; qx = r01 + r10; qy = 1.0f + r11 - r00 - r22; qz = r12 + r21;
+    } else {
+        qw = r10 - r01; qx = r02 + r20; qy = r12 + r21; qz = 1.0f + r22 - r00 - r11;
+    }
+    const float qn = sqrtf(qw * qw + qx * qx + qy * qy + qz * qz);
+    qw /= qn; qx /= qn; qy /= qn; qz /= qn;
+    if (qw < 0.f) { qw = -qw; qx = -qx; qy = -qy; qz = -qz; }
+    const float vn = sqrtf(qx * qx + qy * qy + qz * qz);
+    const float ang = 2.0f * atan2f(vn, qw);
+    const float k = vn > 1e-12f ? ang / vn : 2.0f;   // small angle: 2 / w with w ~ 1
+    wx = qx * k; wy = qy * k; wz = qz * k;
+}
+
+__global__ void __launch_bounds__(kSampleBlock)
+k_deskew(float* __restrict__ pts, int64_t n, int64_t stride, const float* __restrict__ ts,
+         const float* __restrict__ minmax, const float* __restrict__ pose, float ts_mid) {
+    const int64_t i = (int64_t)blockIdx.x * kSampleBlock + threadIdx.x;
+    if (i >= n) return;
+    float wx, wy, wz;
+    rotmat_to_rotvec(pose, wx, wy, wz);
+    const float s = (ts[i] - minmax[0]) / (minmax[1] - minmax[0]) - ts_mid;
+    const float ax = s * wx, ay = s * wy, az = s * wz;
+    const float th2 = ax * ax + ay * ay + az * az;
+    const float th = sqrtf(th2);
+    float a, b;   // R = I + a [w]x + b [w]x^2
+    if (th < 1e-4f) {
+        a = 1.0f - th2 / 6.0f;
+        b = 0.5f - th2 / 24.0f;
+    } else {
+        a = sinf(th) / th;
+        b = (1.0f - cosf(th)) / th2;
+    }
+    float* p = pts + i * stride;
+    const float x = p[0], y = p[1], z = p[2];
+    // [w]x p = w x p ; [w]x^2 p = w x (w x p)
+    const float cx = ay * z - az * y, cy = az * x - ax * z, cz = ax * y - ay * x;
+    const float dx = ay * cz - az * cy, dy = az * cx - ax * cz, dz = ax * cy - ay * cx;
+    p[0] = x + a * cx + b * dx + s * pose[3];
+    p[1] = y + a * cy + b * dy + s * pose[7];
+    p[2] = z + a * cz + b * dz + s * pose[11];
+}
+
+}  // namespace
+
+extern "C" int pin_deskew(float* points, int64_t n, int64_t stride, const float* ts, const float* ts_minmax,
+                          const float* pose, float ts_mid_pose, void* stream) {
+    if (n < 0 || stride < 3) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    if (!points || !ts || !ts_minmax || !pose) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_deskew, dim3((unsigned)((n + kSampleBlock - 1) / kSampleBlock)), dim3(kSampleBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), points, n, stride, ts, ts_minmax, pose, ts_mid_pose);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}

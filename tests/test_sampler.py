@@ -128,3 +128,41 @@ def test_process_frame_matches_reference(golden, dev):
         np.testing.assert_array_equal(nm.point_certainties.cpu().numpy(), z[f"f{k}_point_certainties"])
         assert mapper.pool_sample_count == int(z[f"f{k}_pool_sample_count"])
         assert mapper.cur_sample_count == int(z[f"f{k}_cur_sample_count"])
+
+
+def test_oracle_deskew_identity_and_composition():
+    """Host checks of the deskew restatement (parity unpinned: roma is absent): zero motion is the
+    identity, s = 0 rows are unchanged, and the two half-steps of a pose compose to it."""
+    rng = np.random.default_rng(0)
+    p = rng.normal(0, 20, (50, 4))
+    ts = np.linspace(0, 1, 50)
+    np.testing.assert_allclose(O.deskewing(p, ts, np.eye(4))[:, :3], p[:, :3], atol=1e-12)
+    yaw = 0.2
+    T = np.eye(4)
+    T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0], [np.sin(yaw), np.cos(yaw), 0], [0, 0, 1]]
+    T[:3, 3] = [1.0, -0.5, 0.1]
+    np.testing.assert_allclose(O.rotvec_to_rotmat(O.rotmat_to_rotvec(T[:3, :3])), T[:3, :3], atol=1e-12)
+    out = O.deskewing(p, ts, T, ts_mid_pose=0.0)   # s = ts: last row gets the whole pose
+    np.testing.assert_allclose(out[-1, :3], T[:3, :3] @ p[-1, :3] + T[:3, 3], atol=1e-9)
+    np.testing.assert_allclose(out[0, :3], p[0, :3], atol=1e-12)
+    np.testing.assert_array_equal(out[:, 3], p[:, 3])
+
+
+@pytest.mark.gpu
+def test_deskew_kernel_matches_oracle(dev):
+    """pin_deskew vs the f64 restatement (tolerance 2e-5 m absolute on 60 m scans: f32 Rodrigues)."""
+    from pin_slam_amd.tools import deskewing
+    rng = np.random.default_rng(1)
+    p = rng.normal(0, 25, (20000, 4)).astype(np.float32)
+    ts = rng.uniform(3.0, 3.1, (20000, 1)).astype(np.float32)
+    for ang, tr in [(0.3, [0.8, -0.2, 0.05]), (1e-6, [0.0, 0.0, 0.0]), (2.9, [2.0, 1.0, -1.0])]:
+        ax = np.array([0.3, -0.5, 0.8])
+        ax /= np.linalg.norm(ax)
+        T = np.eye(4)
+        T[:3, :3] = O.rotvec_to_rotmat(ax * ang)
+        T[:3, 3] = tr
+        want = O.deskewing(p, ts, T)
+        got = deskewing(torch.as_tensor(p, device=dev).clone(), torch.as_tensor(ts, device=dev),
+                        torch.as_tensor(T, device=dev))
+        np.testing.assert_allclose(got.cpu().numpy()[:, :3], want[:, :3], rtol=0, atol=2e-5)
+        np.testing.assert_array_equal(got.cpu().numpy()[:, 3], p[:, 3])
