@@ -7,30 +7,40 @@
 
 * replaces ``model.neural_points.NeuralPoints`` and ``model.decoder.Decoder`` by the drop-in
   classes, so every later ``from model.neural_points import NeuralPoints`` binds ours;
-* transplants the hot-path methods onto the reference's ``utils.mapper.Mapper``,
-  ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, keeping everything else
-  of those classes (data sampling, bundle adjustment, marching cubes, ...) as it is.
+* replaces ``utils.data_sampler.DataSampler`` (and the name ``utils.mapper`` imported) by the
+  fused sampler, and ``deskewing`` in ``utils.tools`` / ``dataset.slam_dataset`` by the kernel;
+* transplants the hot-path methods onto the reference's ``utils.mapper.Mapper`` (incl.
+  ``process_frame``), ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, keeping
+  everything else of those classes (bundle adjustment, marching cubes, ...) as it is.
 
 It returns the list of (module, attribute) pairs it patched.  Nothing in the package calls it.
 """
 import importlib
 
+from .data_sampler import DataSampler
 from .decoder import Decoder
 from .mapper import Mapper
 from .mesher import Mesher
 from .neural_points import NeuralPoints
+from .tools import deskewing
 from .tracker import Tracker
 
-MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient")
+MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient",
+                  "process_frame", "dynamic_filter", "_used_poses")
 TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
 MESHER_METHODS = ("query_points",)
 
 
-def install(neural_points=True, decoder=True, mapper=True, tracker=True, mesher=True):
+def install(neural_points=True, decoder=True, mapper=True, tracker=True, mesher=True, sampler=True):
     patched = []
 
-    def setcls(modname, name, obj):
-        mod = importlib.import_module(modname)
+    def setcls(modname, name, obj, optional=False):
+        try:
+            mod = importlib.import_module(modname)
+        except ImportError:
+            if optional:
+                return
+            raise
         setattr(mod, name, obj)
         patched.append((modname, name))
 
@@ -44,6 +54,11 @@ def install(neural_points=True, decoder=True, mapper=True, tracker=True, mesher=
         setcls("model.neural_points", "NeuralPoints", NeuralPoints)
     if decoder:
         setcls("model.decoder", "Decoder", Decoder)
+    if sampler:
+        setcls("utils.data_sampler", "DataSampler", DataSampler)
+        setcls("utils.mapper", "DataSampler", DataSampler)
+        setcls("utils.tools", "deskewing", deskewing)
+        setcls("dataset.slam_dataset", "deskewing", deskewing, optional=True)
     if mapper:
         methods("utils.mapper", "Mapper", Mapper, MAPPER_METHODS)
     if tracker:
