@@ -46,10 +46,15 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
     else qz = (blk & 1) ? qz - c.eps : qz + c.eps;
 }
 
+#ifndef PIN_CERT_T8
+#define PIN_CERT_T8 1   // certainty side effect: flush transposed, 8 lanes per row (see k_train_forward_grid)
+#endif
+
 template <bool WF, class Src>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
-                                                   PinTrainCfg c, int64_t t, PinTrainState st) {
+                                                   PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
+                                                   float (&cw)[kK]) {
     // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
     const int64_t r = st.order ? st.order[t] : t;
     float qx, qy, qz;
@@ -92,10 +97,14 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             st.ids[t * nn_k + j] = id;
             st.weights[t * nn_k + j] = w;
         }
+        cid[j] = valid ? id : -1;
+        cw[j] = w;
         if (valid) {
             // training side effects (neural_points.py:640, :644); ts: read first, the max is
             // usually a no-op
+#if !PIN_CERT_T8
             if (st.certainties) atomicAdd(st.certainties + id, w);
+#endif
             if (qts >= 0 && st.ts_update && st.ts_update[id] < qts)
                 atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
         }
@@ -124,6 +133,31 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     st.sdf[r] = sdf;
 }
 
+// The certainty side effect is a float atomic add per (row, neighbour): memory-side, and with
+// one lane per row every wave-instruction hits 64 unrelated 64-B segments (the slow shape,
+// MI355X_MICROARCH.md Global float atomics).  Flushed transposed instead -- through LDS, 8 lanes
+// per row, 8 rows per instruction -- a row's neighbours (adjacent cells) share segments.
+__device__ __forceinline__ void flush_certainty(float* __restrict__ cert, const int (&cid)[kK], const float (&cw)[kK]) {
+#if PIN_CERT_T8
+    __shared__ int s_id[kBlock * kK];
+    __shared__ float s_w[kBlock * kK];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        s_id[tid * kK + j] = cid[j];
+        s_w[tid * kK + j] = cw[j];
+    }
+    __syncthreads();
+    const int base = (tid & ~63) * kK, lane = tid & 63;
+#pragma unroll
+    for (int u = 0; u < kK; ++u) {
+        const int e = base + u * 64 + lane;
+        const int id = s_id[e];
+        if (id >= 0) atomicAdd(cert + id, s_w[e]);
+    }
+#endif
+}
+
 template <bool WF>
 __global__ void __launch_bounds__(kBlock)
 k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
@@ -131,9 +165,15 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     __shared__ float s_mlp[kWSize];
     const MlpW mw = stage_mlp(m, s_mlp);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
-    if (t >= c.n_main + 6 * c.n_stencil) return;
-    const HashSource src(h, p);
-    train_forward_body<WF>(src, p, mw, coord, ts, c, t, st);
+    int cid[kK];
+    float cw[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
+    if (t < c.n_main + 6 * c.n_stencil) {
+        const HashSource src(h, p);
+        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw);
+    }
+    if (st.certainties) flush_certainty(st.certainties, cid, cw);
 }
 
 template <bool WF>
@@ -143,9 +183,17 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
     __shared__ float s_mlp[kWSize];
     const MlpW mw = stage_mlp(m, s_mlp);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
-    if (t >= c.n_main + 6 * c.n_stencil) return;
-    const GridSource<false> src(g, p);
-    train_forward_body<WF>(src, p, mw, coord, ts, c, t, st);
+    int cid[kK];
+    float cw[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
+    if (t < c.n_main + 6 * c.n_stencil) {
+        const GridSource<false> src(g, p);
+        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw);
+    }
+#ifndef PIN_CERT_SKIP
+    if (st.certainties) flush_certainty(st.certainties, cid, cw);
+#endif
 }
 
 __global__ void __launch_bounds__(kBlock)

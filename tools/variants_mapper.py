@@ -10,7 +10,8 @@ OUT = os.path.join(ROOT, "tools", "exp_libs")
 for rep in range(2):
     for lib in sorted(f for f in os.listdir(OUT) if f.endswith(".so")):
         env = dict(os.environ, PIN_LIB=os.path.join(OUT, lib))
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--steps", "5"],
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--steps", "5",
+                            "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame"],
                            env=env, capture_output=True, text=True, timeout=400)
         if r.returncode:
             print(lib, "FAILED", r.stderr[-1500:])
