@@ -529,6 +529,7 @@ constexpr int kWSize = kWB2 + 4;
 struct MlpW {
     const float* w;   // LDS
     float sdf_scale;
+    float* xs;        // per-wave LDS scratch (64 x 12 floats) of the MFMA decoder, or nullptr
 };
 
 // W1[c][i] in the staged layout
@@ -551,7 +552,7 @@ __device__ __forceinline__ MlpW stage_mlp(const PinMlp& m, float* s_w) {
         s_w[e] = v;
     }
     __syncthreads();
-    return MlpW{s_w, m.sdf_scale};
+    return MlpW{s_w, m.sdf_scale, nullptr};
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -595,6 +596,102 @@ __device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], fl
         for (int i = 0; i < NOUT; ++i) gx[i] = (g2[i].x + g2[i].y) * m.sdf_scale;
     }
     return ((out2.x + out2.y) + m.w[kWB2]) * m.sdf_scale;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// LDS ordering between lanes of one wave (a wave's DS instructions execute in order; this keeps
+// the compiler from moving them across the exchange point)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The decoder of the wave's 64 queries as one batched GEMM on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32, exact f32 products; model/decoder.py:66-88):
+//   P^T = W1 X^T             M = 64 hidden (4 tiles), N = 64 queries (4 tiles), K = 11 -> 12
+//   sdf = s (w2 . relu(P + b1) + b2)    relu and the w2 dot on the accumulator tiles
+//   gx^T = W1^T G^T,  G = w2 o 1[P + b1 > 0]    the masked tile is the next MFMA's B operand as
+//                     it stands (K-step s pairs hidden unit 16mt + 4k + s with lane group k)
+// X goes through 3 KB of LDS (xs) to reach the B-operand layout, and gx back through it.
+// gx: the NOUT input gradients from input OFF on (OFF 0 / 11 weighted_first, OFF 8 / 3 for the
+// neighbour-vector gradient of per-neighbour decoding).  Every lane of the wave must call this
+// (lanes without a query pass zeros).
+template <bool GRAD, int OFF, int NOUT>
+__device__ __forceinline__ float mlp_sdf_wave(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+    float* xs = m.xs;
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15, grp = lane >> 4;
+    float4* xr = (float4*)(xs + lane * kWRow);
+    xr[0] = make_float4(x[0], x[1], x[2], x[3]);
+    xr[1] = make_float4(x[4], x[5], x[6], x[7]);
+    xr[2] = make_float4(x[8], x[9], x[10], 0.f);
+    wave_lds_sync();
+    float bq[4][3];   // B[k = grp][j = col] = X[q = 16 nt + col][i = 4 ks + grp]
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) bq[nt][ks] = xs[(16 * nt + col) * kWRow + 4 * ks + grp];
+    float outp[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4 gacc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) gacc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int mt = 0; mt < 4; ++mt) {
+        float a[3];       // A[i = col -> hidden 16 mt + col][k = grp -> input 4 ks + grp]
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) a[ks] = m.w[w1_at(16 * mt + col, 4 * ks + grp)];   // input 11 is the 0 pad
+        float b1v[4], w2v[4], ga[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int c = 16 * mt + 4 * grp + r;   // hidden unit of accumulator row r
+            b1v[r] = m.w[kWB1 + c];
+            w2v[r] = m.w[kWW2 + c];
+            ga[r] = (GRAD && col < NOUT) ? m.w[w1_at(c, OFF + col)] : 0.f;   // A[i = col][k = grp] = W1[c][OFF+col]
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ks], bq[nt][ks], d, 0, 0, 0);
+            float g[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float pre = d[r] + b1v[r];
+                const bool on = pre > 0.f;
+                outp[nt] = on ? fmaf(w2v[r], pre, outp[nt]) : outp[nt];
+                g[r] = on ? w2v[r] : 0.f;
+            }
+            if (GRAD) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gacc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[r], g[r], gacc[nt], 0, 0, 0);
+            }
+        }
+    }
+    // w2 . relu: sum the four lane groups of each query column; lane q keeps column q
+    float out = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        float v = outp[nt];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        out = (grp == nt) ? v : out;
+    }
+    if (GRAD) {
+        wave_lds_sync();   // every lane has read its B operands
+        if (4 * grp < NOUT) {     // rows i = 4 grp + r < 12 hold outputs
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                *(float4*)(xs + (16 * nt + col) * kWRow + 4 * grp) =
+                    make_float4(gacc[nt][0], gacc[nt][1], gacc[nt][2], gacc[nt][3]);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int i = 0; i < NOUT; ++i) gx[i] = xs[lane * kWRow + i] * m.sdf_scale;
+        wave_lds_sync();   // the next call's X staging reuses xs
+    }
+    return (out + m.w[kWB2]) * m.sdf_scale;
 }
 
 }  // namespace pin

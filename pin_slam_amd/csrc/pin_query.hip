@@ -15,6 +15,14 @@
 
 #include "pin_device.h"
 
+// Per-neighbour decoder (weighted_first False) of the fused grid kernel as one f32-MFMA GEMM per
+// neighbour slot (mlp_sdf_wave).  Off: measured 123 us vs 102 us on VALU for 262K queries -- the
+// f32 MFMA runs at the packed-f32 VALU rate on gfx950 and an 11-input hidden unit needs ~4 VALU
+// ops of post-processing (bias, ReLU, w2, mask) for ~5.5 packed FMAs saved.
+#ifndef PIN_MLP_MFMA
+#define PIN_MLP_MFMA 0
+#endif
+
 using namespace pin;
 
 namespace {
@@ -267,9 +275,15 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
             w[j] = valid && nn > 0 ? u[j] / S : 0.f;
             cert = cert + in.cert * w[j];
             sk[j] = 0.f;
-            if (!valid) continue;
             float g3[3];
-            sk[j] = mlp_sdf<GRAD, kF, 3>(m, in.x, g3);
+            if (m.xs) {   // the wave's 64 neighbour-j decodes as one MFMA GEMM (all lanes take part)
+                const float v = mlp_sdf_wave<GRAD, kF, 3>(m, in.x, g3);
+                if (!valid) continue;
+                sk[j] = v;
+            } else {
+                if (!valid) continue;
+                sk[j] = mlp_sdf<GRAD, kF, 3>(m, in.x, g3);
+            }
             if (GRAD) {
                 float r0 = g3[0], r1 = g3[1], r2 = g3[2];
                 if (PGO) quat_rotate_active(in.quat, g3[0], g3[1], g3[2], r0, r1, r2);
@@ -301,6 +315,7 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
             for (int a = 0; a < 3; ++a) gq[a] = A[a] - mean * C[a] + G[a];
         }
     }
+    if (i < 0) return;   // a lane that only kept the wave whole for the MFMA decoder
     if (sdf_out) sdf_out[i] = sdf;
     if (GRAD && grad_out) {
         grad_out[3 * i] = gq[0];
@@ -318,7 +333,8 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
                                                float* __restrict__ sdf_out, float* __restrict__ grad_out,
                                                int* __restrict__ nn_out, float* __restrict__ cert_out,
                                                float* __restrict__ std_out) {
-    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const int64_t iq = i >= 0 ? i : 0;   // i < 0: no query (the lane only completes its wave)
+    const float qx = q[3 * iq], qy = q[3 * iq + 1], qz = q[3 * iq + 2];
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
@@ -346,10 +362,20 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
                  int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out,
                  const int* __restrict__ order) {
     __shared__ float s_mlp[kWSize];
-    const MlpW mw = stage_mlp(m, s_mlp);
+    MlpW mw = stage_mlp(m, s_mlp);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
+#if PIN_MLP_MFMA
+    __shared__ float s_xs[kBlock / 64][64 * kWRow];
+    if (!WF) {   // the MFMA decoder needs whole waves: lanes past n run query 0 and write nothing
+        mw.xs = s_xs[threadIdx.x >> 6];
+        if ((t & ~(int64_t)63) >= n) return;
+    } else if (t >= n) {
+        return;
+    }
+#else
     if (t >= n) return;
-    const int64_t i = order ? order[t] : t;
+#endif
+    const int64_t i = t < n ? (order ? order[t] : t) : -1;
     const GridSource<FAT> src(g, p);
     query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
 }
@@ -519,7 +545,8 @@ __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoin
                                                    float* __restrict__ weights, int64_t* __restrict__ nn_counts,
                                                    float* __restrict__ cert_out, int* __restrict__ ids,
                                                    int* __restrict__ gids) {
-    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const int64_t iq = i >= 0 ? i : 0;   // i < 0: no query (the lane only completes its wave)
+    const float qx = q[3 * iq], qy = q[3 * iq + 1], qz = q[3 * iq + 2];
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
