@@ -88,6 +88,7 @@ def parse():
     ap.add_argument("--no-mesher", action="store_true", help="skip the mesher leg (configs[4])")
     ap.add_argument("--no-map-update", action="store_true", help="skip the map-maintenance leg (8f rank 1)")
     ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
+    ap.add_argument("--no-nwf-leg", action="store_true", help="skip the per-neighbour-decoding leg")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -157,6 +158,32 @@ def time_kernel(nm, dec, q, wf, backend, steps):
         torch.cuda.synchronize()
         return statistics.mean(a.elapsed_time(b) for a, b in ev)
     return mean_ms(launch), (mean_ms(order_pass) if order_pass else 0.0)
+
+
+def nwf_leg(nm, dec, q, args, world):
+    """The same batch and map with per-neighbour decoding (weighted_first False: SDF = IDW mean
+    of the 8 neighbours' decoded SDFs, plus its std and gradient) -- what the reference's lidar
+    configs (config/lidar_slam/run_kitti.yaml etc.) run."""
+    def step():
+        return P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False, want_std=True,
+                           weighted_first=False)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=q.device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t[0])
+    return {"metric": "SDF+grad+std queries/sec, per-neighbour decoding", "value": q.shape[0] * args.steps * world / el,
+            "unit": "queries/s", "ms_per_step": el / args.steps * 1e3, "scaling": "weak",
+            "config": {"workload": "configs[1] batch and map, weighted_first False (8 decoder evaluations per query)"}}
 
 
 TRACKER_SRC = 200_000      # configs[2]: source points per registration step
@@ -552,6 +579,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
+    if wf and not args.no_nwf_leg:
+        out["per_neighbour"] = nwf_leg(nm, dec, q, args, world)
     if not args.no_mesher:
         out["mesher"] = mesher_leg(nm, dec, pts, args, dev, world, rank)
     if not args.no_tracker:   # last: it fits the map first

@@ -7,7 +7,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/gpu_tests.log
 for rep in 1 2; do
 for v in columns bricks; do
-    PIN_GRID_SCAN=$v timeout -k 10 120 python bench.py --no-mapper --no-tracker --no-mesher --no-map-update --no-process-frame --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
+    PIN_GRID_SCAN=$v timeout -k 10 120 python bench.py --no-mapper --no-tracker --no-mesher --no-map-update --no-process-frame --no-nwf-leg --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
     python - "$v" <<'PY'
 import json, sys
 d = json.loads(open(f"gpurun_out/ab_{sys.argv[1]}.json").read().strip().splitlines()[-1])

@@ -30,7 +30,7 @@ def run(args):
         for lib in libs:
             env = dict(os.environ, PIN_LIB=os.path.join(OUT, lib))
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-mapper", "--no-cpu-baseline",
-                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", *args], env=env, capture_output=True, text=True,
+                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", "--no-nwf-leg", *args], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
                 print(lib, "FAILED", r.stderr[-2000:])
