@@ -506,6 +506,22 @@ int pin_sample_rays(const float* points, int64_t n, const float* randn_surface, 
 int pin_deskew(float* points, int64_t n, int64_t stride, const float* ts, const float* ts_minmax, const float* pose,
                float ts_mid_pose, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Marching cubes for Mesher.mc_mesh (utils/mesher.py:310-337; the reference calls
+ * skimage.measure.marching_cubes(sdf, level=0, allow_degenerate=False, mask=mc_mask)).
+ * values [nx][ny][nz] f32 (x slowest); mask [nx][ny][nz] u8 or NULL: cube (x,y,z) -- grid points
+ * x..x+1, y..y+1, z..z+1 -- is processed iff mask[x][y][z].  Triangles from the table of
+ * tools/gen_mc_table.py; one vertex per used grid edge at the linear crossing, in index space;
+ * right-hand normals point from values < level to values >= level.  Two calls: pin_mc_count
+ * writes counts[2] = {vertices, faces} (device) and leaves the vertex / face numbering in the
+ * workspace; pin_mc_emit (same arguments and workspace) writes verts [V,3] f32 and faces [F,3]
+ * int32 in cube order.  nx*ny*nz < 2^29. */
+int64_t pin_mc_workspace_bytes(int64_t nx, int64_t ny, int64_t nz);
+int pin_mc_count(const float* values, const uint8_t* mask, int64_t nx, int64_t ny, int64_t nz, float level,
+                 void* workspace, int64_t* counts, void* stream);
+int pin_mc_emit(const float* values, int64_t nx, int64_t ny, int64_t nz, float level, const void* workspace,
+                float* verts, int32_t* faces, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

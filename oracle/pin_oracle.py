@@ -778,6 +778,98 @@ def deskewing(points: np.ndarray, ts: np.ndarray, pose: np.ndarray, ts_mid_pose:
     return out
 
 
+# ---------------------------------------------------------------- marching cubes
+MC_CORNERS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (1, 1, 1), (0, 1, 1)]
+MC_EDGES = [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 6), (6, 7), (7, 4), (0, 4), (1, 5), (2, 6), (3, 7)]
+MC_FACES = [(0, 3, 2, 1), (4, 5, 6, 7), (0, 1, 5, 4), (3, 7, 6, 2), (0, 4, 7, 3), (1, 2, 6, 5)]
+
+
+def mc_case_triangles(case: int):
+    """Triangles (cube-edge triples) of one corner sign pattern (bit c: corner c below the level).
+    PARITY UNPINNED against the reference: it calls skimage.measure.marching_cubes (Lewiner),
+    which is not installed here.  Construction: per face (corners CCW seen from outside) the
+    boundary cuts off each run of inside corners (an ambiguous face separates them); the face
+    segments (from a run's exit crossing back to its entry crossing) chain into loops, each
+    fan-triangulated -- right-hand normals point from inside to outside."""
+    inside = [(case >> c) & 1 for c in range(8)]
+    edge_of = {frozenset(e): k for k, e in enumerate(MC_EDGES)}
+    nxt = {}
+    for f in MC_FACES:
+        cross = []
+        for k in range(4):
+            a, b = f[k], f[(k + 1) % 4]
+            if inside[a] != inside[b]:
+                cross.append((edge_of[frozenset((a, b))], inside[a]))   # inside[a]: leaving an inside run
+        for k, (e, leaving) in enumerate(cross):
+            if not leaving:
+                nxt[cross[(k + 1) % len(cross)][0]] = e
+    tris, seen = [], set()
+    for start in sorted(nxt):
+        if start in seen:
+            continue
+        loop, cur = [start], nxt[start]
+        seen.add(start)
+        while cur != start:
+            loop.append(cur)
+            seen.add(cur)
+            cur = nxt[cur]
+        tris += [(loop[0], loop[i + 1], loop[i]) for i in range(1, len(loop) - 1)]
+    return tris
+
+
+def marching_cubes(values: np.ndarray, mask: Optional[np.ndarray] = None, level: float = 0.0):
+    """Marching cubes with shared vertices (one per used grid edge, id order = (grid point, axis)
+    order), cubes processed iff mask at their first corner; verts in index space (f32 crossing
+    arithmetic as the kernel), faces in cube order.  Degenerate triangles are kept (the caller
+    filters)."""
+    v = values.astype(np.float32)
+    nx, ny, nz = v.shape
+    f = np.float32
+    lvl = f(level)
+    tables = [mc_case_triangles(c) for c in range(256)]
+    edge_lo = []
+    for a, b in MC_EDGES:
+        pa, pb = np.array(MC_CORNERS[a]), np.array(MC_CORNERS[b])
+        lo = np.minimum(pa, pb)
+        edge_lo.append((tuple(lo), int(np.argmax(np.abs(pb - pa)))))
+    used = {}
+    cube_tris = []
+    below = v < lvl
+    for x in range(nx - 1):
+        for y in range(ny - 1):
+            for z in range(nz - 1):
+                if mask is not None and not mask[x, y, z]:
+                    continue
+                case = 0
+                for c, (dx, dy, dz) in enumerate(MC_CORNERS):
+                    case |= int(below[x + dx, y + dy, z + dz]) << c
+                for tri in tables[case]:
+                    keys = []
+                    for e in tri:
+                        (dx, dy, dz), ax = edge_lo[e]
+                        k = (((x + dx) * ny + (y + dy)) * nz + (z + dz)) * 3 + ax
+                        used[k] = True
+                        keys.append(k)
+                    cube_tris.append(keys)
+    order = sorted(used)
+    vid = {k: i for i, k in enumerate(order)}
+    verts = np.zeros((len(order), 3), f)
+    for i, k in enumerate(order):
+        g, ax = divmod(k, 3)
+        gz, g2 = g % nz, g // nz
+        gy, gx = g2 % ny, g2 // ny
+        va = v[gx, gy, gz]
+        d = [0, 0, 0]
+        d[ax] = 1
+        vb = v[gx + d[0], gy + d[1], gz + d[2]]
+        t = (lvl - va) / (vb - va)
+        p = [f(gx), f(gy), f(gz)]
+        p[ax] = f(p[ax] + t)
+        verts[i] = p
+    faces = np.array([[vid[k] for k in tri] for tri in cube_tris], np.int64).reshape(-1, 3)
+    return verts, faces
+
+
 # ---------------------------------------------------------------- fixture helpers
 def map_from_fixture(z, prefix: str = "map_") -> MapState:
     g = lambda k: z[prefix + k]  # noqa: E731

@@ -116,6 +116,9 @@ _SIGS = {
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_mc_workspace_bytes": [i64, i64, i64],
+    "pin_mc_count": [c_void_p, c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p],
+    "pin_mc_emit": [c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_deskew": [c_void_p, i64, i64, c_void_p, c_void_p, c_void_p, f32, c_void_p],
     "pin_sample_rays": [c_void_p, i64, c_void_p, c_void_p, c_void_p, _P(PinSampleCfg), c_void_p, c_void_p, c_void_p,
                         c_void_p, c_void_p],
@@ -140,7 +143,7 @@ _SIGS = {
     "pin_map_adjust": [_P(PinMapArrays), c_void_p, i64, i32, c_void_p],
 }
 # functions whose return value is not a status code
-_RESTYPES = {"pin_map_workspace_bytes": i64}
+_RESTYPES = {"pin_map_workspace_bytes": i64, "pin_mc_workspace_bytes": i64}
 
 _lib = None
 

@@ -355,8 +355,12 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
     query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
 }
 
+#ifndef PIN_SDF_WAVES
+#define PIN_SDF_WAVES 2   // waves per SIMD the fused grid kernel is compiled for (VGPR budget)
+#endif
+
 template <bool WF, bool PGO, bool GRAD, bool FAT>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PGO ? 1 : PIN_SDF_WAVES)))
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n,
                  int nn_k, int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out,
                  int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out,

@@ -28,7 +28,7 @@ from .tracker import Tracker
 MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient",
                   "process_frame", "dynamic_filter", "_used_poses")
 TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
-MESHER_METHODS = ("query_points",)
+MESHER_METHODS = ("query_points", "mc_mesh")
 
 
 def install(neural_points=True, decoder=True, mapper=True, tracker=True, mesher=True, sampler=True):

@@ -82,3 +82,54 @@ class Mesher:
                     else:
                         mask_out[head:tail] = m.detach().cpu().numpy()
         return sdf_out, None, None, mask_out
+
+
+def marching_cubes(values: torch.Tensor, mask: torch.Tensor = None, level: float = 0.0, allow_degenerate=False):
+    """Marching cubes on the device (pin_mc_count / pin_mc_emit) over a [nx, ny, nz] grid of
+    values (x slowest); ``mask`` [nx, ny, nz] bool selects the processed cubes by their first
+    corner.  Returns (verts [V,3] f32 in index space, faces [F,3] int64) device tensors; with
+    allow_degenerate False, triangles with two coincident vertices are dropped (the reference
+    passes allow_degenerate=False to skimage, utils/mesher.py:327-328)."""
+    from . import _lib
+    _lib.require_device(values)
+    v = values.detach().to(torch.float32).contiguous()
+    nx, ny, nz = (int(s) for s in v.shape)
+    dev = v.device
+    m = None
+    if mask is not None:
+        m = mask.detach().to(device=dev, dtype=torch.uint8).contiguous()
+        if tuple(m.shape) != (nx, ny, nz):
+            raise ValueError("mask must have the grid's shape")
+    wsb = int(_lib.load().pin_mc_workspace_bytes(nx, ny, nz))
+    if wsb < 0:
+        raise ValueError(f"marching cubes grid {nx}x{ny}x{nz} outside 2..2^29 points")
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    _lib.call("pin_mc_count", _lib.ptr(v), _lib.ptr(m), nx, ny, nz, float(level), _lib.ptr(ws), _lib.ptr(counts),
+              _lib.stream())
+    nv, nf = (int(c) for c in counts.cpu())
+    verts = torch.empty((nv, 3), dtype=torch.float32, device=dev)
+    faces = torch.empty((nf, 3), dtype=torch.int32, device=dev)
+    if nf > 0:
+        _lib.call("pin_mc_emit", _lib.ptr(v), nx, ny, nz, float(level), _lib.ptr(ws), _lib.ptr(verts),
+                  _lib.ptr(faces), _lib.stream())
+    faces = faces.long()
+    if not allow_degenerate and nf > 0:
+        p = verts[faces]                                       # [F, 3 vertices, 3]
+        same = ((p[:, 0] == p[:, 1]).all(-1) | (p[:, 1] == p[:, 2]).all(-1) | (p[:, 0] == p[:, 2]).all(-1))
+        faces = faces[~same]
+    return verts, faces
+
+
+def mc_mesh(self, mc_sdf, mc_mask, voxel_size, mc_origin):
+    """utils/mesher.py:310-337 with the marching cubes on the device: mc_sdf / mc_mask as the
+    reference's assign_to_bbx leaves them (numpy or tensors), returns numpy (verts [V,3] f64 =
+    mc_origin + index verts * voxel_size, faces [F,3])."""
+    v = torch.as_tensor(mc_sdf, dtype=torch.float32, device=self.device)
+    m = None if mc_mask is None else torch.as_tensor(mc_mask, device=self.device).to(torch.bool)
+    verts, faces = marching_cubes(v, m, 0.0, allow_degenerate=False)
+    verts = np.asarray(mc_origin) + verts.cpu().numpy() * voxel_size
+    return verts, faces.cpu().numpy()
+
+
+Mesher.mc_mesh = mc_mesh

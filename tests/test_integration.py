@@ -34,7 +34,7 @@ def test_install_patches_reference_modules(monkeypatch):
             return "reference"
 
         def mc_mesh(self):
-            return "kept"
+            return "reference"
 
     mods = {"model": _fake("model"), "model.neural_points": _fake("model.neural_points", NeuralPoints=object),
             "model.decoder": _fake("model.decoder", Decoder=object), "utils": _fake("utils"),
@@ -57,5 +57,5 @@ def test_install_patches_reference_modules(monkeypatch):
     assert sys.modules["utils.mapper"].DataSampler is DataSampler
     assert sys.modules["utils.tools"].deskewing is deskewing
     assert RefTracker.tracking is P.Tracker.tracking and RefTracker.registration_step is P.Tracker.registration_step
-    assert RefMesher.query_points is P.Mesher.query_points and RefMesher().mc_mesh() == "kept"
+    assert RefMesher.query_points is P.Mesher.query_points and RefMesher.mc_mesh is P.Mesher.mc_mesh
     assert ("utils.mapper", "Mapper.mapping") in patched
