@@ -26,7 +26,7 @@ from .tools import deskewing
 from .tracker import Tracker
 
 MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient",
-                  "process_frame", "dynamic_filter", "_used_poses")
+                  "process_frame", "dynamic_filter", "_used_poses", "_pool_append")
 TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
 MESHER_METHODS = ("query_points", "mc_mesh")
 

@@ -169,22 +169,24 @@ class Mapper:
             if self.neural_points.prune_map(c.max_prune_certainty):
                 self.neural_points.recreate_hash(None, None, True, True, frame_id)
         self.neural_points.update(update_points, frame_origin, frame_orientation, frame_id)   # :177
-        self.coord_pool = torch.cat((self.coord_pool, coord), 0)                         # :185-188
-        self.weight_pool = torch.cat((self.weight_pool, weight), 0)
-        self.sdf_label_pool = torch.cat((self.sdf_label_pool, sdf_label), 0)
-        self.time_pool = torch.cat((self.time_pool, time_repeat), 0)
+        # :185-188 -- appended into growable buffers (same contents as the reference's torch.cat,
+        # without reallocating and copying the whole pool every frame)
+        self.coord_pool = self._pool_append("coord", self.coord_pool, coord)
+        self.weight_pool = self._pool_append("weight", self.weight_pool, weight)
+        self.sdf_label_pool = self._pool_append("sdf_label", self.sdf_label_pool, sdf_label)
+        self.time_pool = self._pool_append("time", self.time_pool, time_repeat)
         self.sem_label_pool = None if sem_label is None else (
-            sem_label if self.sem_label_pool is None else torch.cat((self.sem_label_pool, sem_label.to(
-                self.sem_label_pool.dtype)), 0))
+            sem_label if self.sem_label_pool is None else self._pool_append(
+                "sem", self.sem_label_pool, sem_label.to(self.sem_label_pool.dtype)))
         self.color_pool = None if color_label is None else (
-            color_label if self.color_pool is None else torch.cat((self.color_pool, color_label), 0))
+            color_label if self.color_pool is None else self._pool_append("color", self.color_pool, color_label))
         self.normal_label_pool = None
         self.used_poses = self._used_poses()                                             # :205-211
         if self.ba_done_flag:                                                            # :214-217
             self.global_coord_pool = transform_batch_torch(self.coord_pool, self.used_poses[self.time_pool])
             self.ba_done_flag = False
         else:
-            self.global_coord_pool = torch.cat((self.global_coord_pool, global_coord), 0)
+            self.global_coord_pool = self._pool_append("global_coord", self.global_coord_pool, global_coord)
         if (frame_id + 1) % int(c.pool_filter_freq) == 0:                                # :226-262
             rel = self.global_coord_pool - frame_origin.to(self.global_coord_pool)
             filter_mask = torch.sum(rel ** 2, dim=-1) < c.window_radius ** 2
@@ -194,15 +196,16 @@ class Mapper:
                 discard_count = pool_sample_count - int(c.pool_capacity)
                 discarded_index = torch.randint(0, pool_sample_count, (discard_count,), device=self.device)
                 filter_mask[true_indices[discarded_index]] = False
-            self.coord_pool = self.coord_pool[filter_mask]
-            self.global_coord_pool = self.global_coord_pool[filter_mask]
-            self.sdf_label_pool = self.sdf_label_pool[filter_mask]
-            self.weight_pool = self.weight_pool[filter_mask]
-            self.time_pool = self.time_pool[filter_mask]
+            keep = torch.nonzero(filter_mask).squeeze(1)   # one compaction index for every pool
+            self.coord_pool = self.coord_pool.index_select(0, keep)
+            self.global_coord_pool = self.global_coord_pool.index_select(0, keep)
+            self.sdf_label_pool = self.sdf_label_pool.index_select(0, keep)
+            self.weight_pool = self.weight_pool.index_select(0, keep)
+            self.time_pool = self.time_pool.index_select(0, keep)
             if sem_label is not None:
-                self.sem_label_pool = self.sem_label_pool[filter_mask]
+                self.sem_label_pool = self.sem_label_pool.index_select(0, keep)
             if color_label is not None:
-                self.color_pool = self.color_pool[filter_mask]
+                self.color_pool = self.color_pool.index_select(0, keep)
             cur_sample_filter_mask = filter_mask[-self.cur_sample_count:]
             self.cur_sample_count = int(cur_sample_filter_mask.sum().item())
             self.pool_sample_count = int(filter_mask.sum().item())
@@ -222,6 +225,22 @@ class Mapper:
             new_sample_count = self.new_idx.shape[0]
             self.train_less = bool(getattr(c, "adaptive_mode", False) and
                                    new_sample_count / max(self.cur_sample_count, 1) < c.new_sample_ratio_thre)
+
+    def _pool_append(self, name, cur, new):
+        """torch.cat((cur, new)) as a prefix view of a buffer grown by 1.5x when full; cur must
+        be the previous return value to be appended in place (anything else is copied once)."""
+        bufs = self.__dict__.setdefault("_pool_bufs", {})
+        buf = bufs.get(name)
+        n, m = cur.shape[0], new.shape[0]
+        if (buf is None or buf.dtype != cur.dtype or buf.shape[1:] != cur.shape[1:] or buf.shape[0] < n + m
+                or (n > 0 and cur.data_ptr() != buf.data_ptr())):
+            nb = torch.empty((max(int((n + m) * 1.5), 1024),) + tuple(cur.shape[1:]), dtype=cur.dtype,
+                             device=new.device)
+            nb[:n] = cur
+            buf = nb
+        buf[n:n + m] = new
+        bufs[name] = buf
+        return buf[:n + m]
 
     def set_pool(self, coord, sdf_label, ts, weight=None, global_coord=None):
         """Install a training-sample pool (the output of Mapper.process_frame, utils/mapper.py:110-321)."""

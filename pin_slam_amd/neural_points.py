@@ -211,17 +211,38 @@ class NeuralPoints(nn.Module):
         self.memory_footprint.append(cur_memory)
 
     # ------------------------------------------------------------------ neighbourhood
+    _NBHD_FIELDS = ("neighbor_dx", "neighbor_K", "max_valid_dist2", "neighbor_window", "_cells_host", "_cells",
+                    "_offsets", "_num_columns", "_grid_exact")
+
     def set_search_neighborhood(self, num_nei_cells: int = 1, search_alpha: float = 1.0):
-        """model/neural_points.py:430-457."""
-        self.neighbor_dx = neighbor_offsets(num_nei_cells, search_alpha, device=self.primes.device)
-        self.neighbor_K = self.neighbor_dx.shape[0]
+        """model/neural_points.py:430-457.  Each neighbourhood's tables are built once and kept:
+        Mapper.process_frame switches to the 1-cell neighbourhood and back every frame."""
+        self._save_neighborhood()
+        key = (int(num_nei_cells), float(search_alpha))
+        self._nbhd_key = key
+        hit = self.__dict__.setdefault("_nbhd_cache", {}).get(key)
+        if hit is not None:
+            for k, v in hit.items():
+                setattr(self, k, v)
+            return
+        dx = neighbor_offsets(num_nei_cells, search_alpha)          # host, then one copy
+        self.neighbor_dx = dx.to(self.primes.device)
+        self.neighbor_K = dx.shape[0]
         self.max_valid_dist2 = 3 * ((num_nei_cells + 1) * self.resolution) ** 2
-        dx_host = np.ascontiguousarray(self.neighbor_dx.cpu().numpy().astype(np.int32))
+        dx_host = np.ascontiguousarray(dx.numpy().astype(np.int32))
         self.neighbor_window = int(np.abs(dx_host).max()) if dx_host.size else 0
         self._cells_host = dx_host
         self._cells = None  # device tables built lazily (need the HIP runtime)
         self._offsets = None
+        self._num_columns = 0
         self._grid_exact = grid_window_collision_free(self.buffer_size, num_nei_cells)
+        self._save_neighborhood()
+
+    def _save_neighborhood(self):
+        key = self.__dict__.get("_nbhd_key")
+        if key is not None:
+            self.__dict__.setdefault("_nbhd_cache", {})[key] = {k: getattr(self, k) for k in self._NBHD_FIELDS
+                                                                 if hasattr(self, k)}
 
     def _cell_table(self):
         if self._cells is None:
@@ -230,6 +251,7 @@ class NeuralPoints(nn.Module):
             _lib.call("pin_neighbor_cells", self._cells_host.ctypes.data_as(_lib.c_void_p), int(self.neighbor_K),
                       self.buffer_size, _lib.ptr(cells), _lib.stream())
             self._cells = cells
+            self._save_neighborhood()
         return self._cells
 
     def _offset_table(self):
@@ -245,6 +267,7 @@ class NeuralPoints(nn.Module):
             if cols is not None:
                 pad = np.concatenate([pad, np.asarray(cols, dtype=np.int64).astype(np.int32)])
             self._offsets = torch.from_numpy(pad).to(self.device)
+            self._save_neighborhood()
         return self._offsets
 
     # ------------------------------------------------------------------ derived-state cache
