@@ -218,7 +218,7 @@ def test_mapper_dropin_backward(golden, dev, backend, case):
     loss = torch.nn.functional.binary_cross_entropy_with_logits(sdf / sigma, torch.sigmoid(label / sigma)) + \
         float(z["weight_e"]) * ((g.norm(2, dim=-1) - 1.0) ** 2).mean()
     loss.backward()
-    assert float(loss) == pytest.approx(float(z["it0_loss"]), rel=1e-5)
+    assert float(loss.detach()) == pytest.approx(float(z["it0_loss"]), rel=1e-5)
     np.testing.assert_allclose(_np(sdf), z["it0_sdf"], atol=SDF_ATOL)
     np.testing.assert_allclose(_np(nm.local_geo_features.grad), z["it0_feat_grad"], rtol=1e-4, atol=1e-8)
     for key, prm in zip(["W1", "b1", "W2", "b2"], dec.parameters()):
