@@ -12,7 +12,7 @@
 //                             (device totals written to counts[2] = {vertices, faces})
 //  pin_mc_emit   k_mc_verts   per flagged edge: its vertex
 //                k_mc_faces   per cube: its triangles as vertex-id triples
-// Workspace (pin_mc_workspace_bytes): 3 N + N_cubes int32 + rocPRIM scan scratch.
+// Workspace (pin_mc_workspace_bytes): 3 N + N_cubes int32, N_cubes int64 face offsets + rocPRIM scan scratch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -104,26 +104,26 @@ k_mc_verts(const float* __restrict__ v, McDims d, int64_t nedges, const int32_t*
 }
 
 __global__ void __launch_bounds__(kMcBlock)
-k_mc_faces(const float* __restrict__ v, McDims d, int64_t ncubes, const int32_t* __restrict__ tri_incl,
+k_mc_faces(const float* __restrict__ v, McDims d, int64_t ncubes, const int64_t* __restrict__ tri_incl,
            const int32_t* __restrict__ vid_incl, int32_t* __restrict__ faces) {
     const int64_t c = (int64_t)blockIdx.x * kMcBlock + threadIdx.x;
     if (c >= ncubes) return;
-    const int32_t end = tri_incl[c], beg = c ? tri_incl[c - 1] : 0;
+    const int64_t end = tri_incl[c], beg = c ? tri_incl[c - 1] : 0;
     if (end == beg) return;
     int64_t x, y, z;
     cube_of(d, c, x, y, z);
     const signed char* t = c_tris[cube_case(v, d, x, y, z)];
-    for (int n = 0; n < end - beg; ++n) {
+    for (int n = 0; n < (int)(end - beg); ++n) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int e = t[3 * n + k];
             const int64_t g = gidx(d, x + c_edge[e][0], y + c_edge[e][1], z + c_edge[e][2]);
-            faces[3 * (int64_t)(beg + n) + k] = vid_incl[3 * g + c_edge[e][3]] - 1;
+            faces[3 * (beg + n) + k] = vid_incl[3 * g + c_edge[e][3]] - 1;
         }
     }
 }
 
-__global__ void k_mc_totals(const int32_t* __restrict__ vid_incl, int64_t nedges, const int32_t* __restrict__ tri_incl,
+__global__ void k_mc_totals(const int32_t* __restrict__ vid_incl, int64_t nedges, const int64_t* __restrict__ tri_incl,
                             int64_t ncubes, int64_t* __restrict__ counts) {
     counts[0] = nedges ? vid_incl[nedges - 1] : 0;
     counts[1] = ncubes ? tri_incl[ncubes - 1] : 0;
@@ -133,7 +133,8 @@ struct McLayout {
     int64_t n, ncubes, nedges;
     size_t scan_bytes;
     int32_t* edge;
-    int32_t* tri;
+    int32_t* tri;     // triangles per cube
+    int64_t* tri64;   // their inclusive scan: up to 5 per cube, so int64 (2^29 cubes x 5 > 2^31)
     void* scan;
 };
 
@@ -141,12 +142,15 @@ bool mc_dims_ok(int64_t nx, int64_t ny, int64_t nz) {
     return nx >= 2 && ny >= 2 && nz >= 2 && nx * ny * nz < (1ll << 29);   // 3 N edge ids fit int32
 }
 
-size_t mc_scan_bytes(int64_t n) {
-    size_t b = 0;
-    if (rocprim::inclusive_scan(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)std::max<int64_t>(n, 1),
-                                rocprim::plus<int32_t>()) != hipSuccess)
+size_t mc_scan_bytes(int64_t nedges, int64_t ncubes) {
+    size_t b = 0, b64 = 0;
+    if (rocprim::inclusive_scan(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                (size_t)std::max<int64_t>(nedges, 1), rocprim::plus<int32_t>()) != hipSuccess)
         return 0;
-    return b;
+    if (rocprim::inclusive_scan(nullptr, b64, (const int32_t*)nullptr, (int64_t*)nullptr,
+                                (size_t)std::max<int64_t>(ncubes, 1), rocprim::plus<int64_t>()) != hipSuccess)
+        return 0;
+    return std::max(b, b64);
 }
 
 McLayout mc_layout(int64_t nx, int64_t ny, int64_t nz, void* ws) {
@@ -154,12 +158,14 @@ McLayout mc_layout(int64_t nx, int64_t ny, int64_t nz, void* ws) {
     L.n = nx * ny * nz;
     L.ncubes = (nx - 1) * (ny - 1) * (nz - 1);
     L.nedges = 3 * L.n;
-    L.scan_bytes = mc_scan_bytes(L.nedges);
+    L.scan_bytes = mc_scan_bytes(L.nedges, L.ncubes);
     char* p = (char*)ws;
     L.edge = (int32_t*)p;
     p += ((L.nedges * 4 + 255) / 256) * 256;
     L.tri = (int32_t*)p;
     p += ((L.ncubes * 4 + 255) / 256) * 256;
+    L.tri64 = (int64_t*)p;
+    p += ((L.ncubes * 8 + 255) / 256) * 256;
     L.scan = p;
     return L;
 }
@@ -171,7 +177,8 @@ extern "C" {
 int64_t pin_mc_workspace_bytes(int64_t nx, int64_t ny, int64_t nz) {
     if (!mc_dims_ok(nx, ny, nz)) return -1;
     const int64_t n = nx * ny * nz, nc = (nx - 1) * (ny - 1) * (nz - 1);
-    return ((3 * n * 4 + 255) / 256) * 256 + ((nc * 4 + 255) / 256) * 256 + (int64_t)mc_scan_bytes(3 * n) + 256;
+    return ((3 * n * 4 + 255) / 256) * 256 + ((nc * 4 + 255) / 256) * 256 + ((nc * 8 + 255) / 256) * 256 +
+           (int64_t)mc_scan_bytes(3 * n, nc) + 256;
 }
 
 int pin_mc_count(const float* values, const uint8_t* mask, int64_t nx, int64_t ny, int64_t nz, float level,
@@ -187,9 +194,9 @@ int pin_mc_count(const float* values, const uint8_t* mask, int64_t nx, int64_t n
     if (rocprim::inclusive_scan(L.scan, b, L.edge, L.edge, (size_t)L.nedges, rocprim::plus<int32_t>(), s) != hipSuccess)
         return PIN_ERR_HIP;
     b = L.scan_bytes;
-    if (rocprim::inclusive_scan(L.scan, b, L.tri, L.tri, (size_t)L.ncubes, rocprim::plus<int32_t>(), s) != hipSuccess)
+    if (rocprim::inclusive_scan(L.scan, b, L.tri, L.tri64, (size_t)L.ncubes, rocprim::plus<int64_t>(), s) != hipSuccess)
         return PIN_ERR_HIP;
-    hipLaunchKernelGGL(k_mc_totals, dim3(1), dim3(1), 0, s, L.edge, L.nedges, L.tri, L.ncubes, counts);
+    hipLaunchKernelGGL(k_mc_totals, dim3(1), dim3(1), 0, s, L.edge, L.nedges, L.tri64, L.ncubes, counts);
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 
@@ -202,7 +209,7 @@ int pin_mc_emit(const float* values, int64_t nx, int64_t ny, int64_t nz, float l
     hipLaunchKernelGGL(k_mc_verts, dim3((unsigned)((L.nedges + kMcBlock - 1) / kMcBlock)), dim3(kMcBlock), 0, s,
                        values, d, L.nedges, L.edge, verts);
     hipLaunchKernelGGL(k_mc_faces, dim3((unsigned)((L.ncubes + kMcBlock - 1) / kMcBlock)), dim3(kMcBlock), 0, s,
-                       values, d, L.ncubes, L.tri, L.edge, faces);
+                       values, d, L.ncubes, L.tri64, L.edge, faces);
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

@@ -144,6 +144,11 @@ def install_map_state(nm, st, params, device):
         if p is not None:
             setattr(nm, k, torch.nn.Parameter(p.detach().to(device)))
     nm._cache = {}
+    # resolution / buffer_size may come from the file: the neighbourhood tables derived from the
+    # constructor's values (max_valid_dist2, slot offsets, grid exactness) are rebuilt
+    nm._nbhd_cache = {}
+    nm._nbhd_key = None
+    nm.set_search_neighborhood(num_nei_cells=nm.config.num_nei_cells, search_alpha=nm.config.search_alpha)
     return nm
 
 

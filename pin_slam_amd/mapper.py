@@ -230,16 +230,20 @@ class Mapper:
         """torch.cat((cur, new)) as a prefix view of a buffer grown by 1.5x when full; cur must
         be the previous return value to be appended in place (anything else is copied once)."""
         bufs = self.__dict__.setdefault("_pool_bufs", {})
-        buf = bufs.get(name)
+        buf, last = bufs.get(name, (None, -1))
         n, m = cur.shape[0], new.shape[0]
-        if (buf is None or buf.dtype != cur.dtype or buf.shape[1:] != cur.shape[1:] or buf.shape[0] < n + m
-                or (n > 0 and cur.data_ptr() != buf.data_ptr())):
-            nb = torch.empty((max(int((n + m) * 1.5), 1024),) + tuple(cur.shape[1:]), dtype=cur.dtype,
-                             device=new.device)
+        dt = torch.promote_types(cur.dtype, new.dtype)    # torch.cat's type promotion
+        # in place only when cur IS the view returned last time: a shorter prefix view (a
+        # truncated pool) still references the rows past it, so it gets a fresh buffer
+        in_place = (buf is not None and n == last and buf.dtype == dt and buf.shape[1:] == cur.shape[1:]
+                    and buf.shape[0] >= n + m and (n == 0 or cur.data_ptr() == buf.data_ptr())
+                    and cur.is_contiguous())
+        if not in_place:
+            nb = torch.empty((max(int((n + m) * 1.5), 1024),) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
             nb[:n] = cur
             buf = nb
         buf[n:n + m] = new
-        bufs[name] = buf
+        bufs[name] = (buf, n + m)
         return buf[:n + m]
 
     def set_pool(self, coord, sdf_label, ts, weight=None, global_coord=None):
@@ -293,6 +297,11 @@ class Mapper:
                 raise NotImplementedError("fused mapping implements ekional_add_to 'all'")
         if getattr(c, "loss_weight_on", False):
             raise NotImplementedError("fused mapping implements the unweighted BCE (loss_weight_on False)")
+        # utils/tools.py:89-116: the fused step is Adam without L2 (the reference's defaults)
+        if not getattr(c, "opt_adam", True):
+            raise NotImplementedError("fused mapping implements the Adam optimizer only (opt_adam True)")
+        if float(getattr(c, "weight_decay", 0.0)) != 0.0:
+            raise NotImplementedError("fused mapping implements Adam with weight_decay 0")
 
     def _world(self):
         group = getattr(self, "group", None)
@@ -391,6 +400,8 @@ class Mapper:
                       ctypes.byref(cfg), ctypes.byref(st), s)
         _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
                   _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
+        # the forward's side effects went through raw pointers: invalidate caches built on them
+        nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if ts64 is not None else None)
         if world > 1:
             allreduce_gradients([grad_features, mlp_grad], getattr(self, "group", None))
         self.last_loss = b.loss
@@ -405,6 +416,8 @@ class Mapper:
         s = _lib.stream()
         _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
                   ctypes.byref(st), s)
+        feats = self.neural_points.local_geo_features
+        self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
         if m_grad is not None:
             off = 0
             for p in mlp_params:

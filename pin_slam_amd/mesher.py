@@ -127,7 +127,13 @@ def mc_mesh(self, mc_sdf, mc_mask, voxel_size, mc_origin):
     mc_origin + index verts * voxel_size, faces [F,3])."""
     v = torch.as_tensor(mc_sdf, dtype=torch.float32, device=self.device)
     m = None if mc_mask is None else torch.as_tensor(mc_mask, device=self.device).to(torch.bool)
-    verts, faces = marching_cubes(v, m, 0.0, allow_degenerate=False)
+    try:
+        verts, faces = marching_cubes(v, m, 0.0, allow_degenerate=False)
+    except ValueError:
+        # the reference wraps skimage in a bare try/except and returns an empty mesh
+        # (utils/mesher.py:324-333); a grid outside 2..2^29 points lands here (the reference's
+        # get_query_from_bbx already refuses more than 5e8 voxels, mesher.py:163)
+        return np.asarray(mc_origin) + np.zeros((0, 3)) * voxel_size, np.zeros((0, 3))
     verts = np.asarray(mc_origin) + verts.cpu().numpy() * voxel_size
     return verts, faces.cpu().numpy()
 

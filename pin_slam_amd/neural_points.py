@@ -218,7 +218,10 @@ class NeuralPoints(nn.Module):
         """model/neural_points.py:430-457.  Each neighbourhood's tables are built once and kept:
         Mapper.process_frame switches to the 1-cell neighbourhood and back every frame."""
         self._save_neighborhood()
-        key = (int(num_nei_cells), float(search_alpha))
+        # the tables also depend on the resolution (max_valid_dist2), the table size (slot offsets,
+        # grid exactness) and the device they live on
+        key = (int(num_nei_cells), float(search_alpha), float(self.resolution), int(self.buffer_size),
+               str(self.primes.device))
         self._nbhd_key = key
         hit = self.__dict__.setdefault("_nbhd_cache", {}).get(key)
         if hit is not None:
@@ -550,6 +553,15 @@ class NeuralPoints(nn.Module):
         ts = (self.neural_points, self.local_neural_points, self.point_orientations, self.local_point_orientations)
         return tuple((weakref.ref(t), t._version) for t in ts)
 
+    @staticmethod
+    def mark_modified(*tensors):
+        """Bump the version of tensors a kernel wrote through raw pointers (features by Adam,
+        certainty / ts side effects), so the derived caches keyed on ``_version`` (the fat compact
+        records) are rebuilt before the next query reads them."""
+        for t in tensors:
+            if t is not None and t.numel():
+                torch.autograd.graph.increment_version(t)
+
     def _unchanged_since_reset(self, idx):
         snap = getattr(self, "_local_snapshot", None)
         if snap is None:
@@ -735,6 +747,7 @@ class NeuralPoints(nn.Module):
                 qts = query_ts.to(device=ids.device, dtype=torch.int64).contiguous()
             _lib.call("pin_train_scatter", _lib.ptr(ids), _lib.ptr(weights.detach()), ids.shape[0], nn_k,
                       _lib.ptr(qts), _lib.ptr(cert_t), _lib.ptr(ts_t), _lib.stream())
+            self.mark_modified(cert_t, ts_t)
         return geo_vec, None, weights.unsqueeze(-1), nn_counts, certainty
 
     def get_map_o3d_bbx(self):

@@ -191,3 +191,26 @@ def test_adam_matches_torch(dev):
         _lib.call("pin_adam_step", _lib.ptr(mine), _lib.ptr(gbuf), _lib.ptr(m), _lib.ptr(v), mine.numel(),
                   ctypes.byref(adam_scalars(0.01, t, 1e-15)), _lib.stream())
         np.testing.assert_allclose(_np(mine), _np(ref), rtol=1e-6, atol=1e-7)
+
+
+def test_fat_cache_sees_training_writes(dev):
+    """Local inference queries read cached copies of the local features and certainties (fat
+    compact records).  mapping() writes those through raw pointers (Adam, certainty / ts side
+    effects); the cache must be rebuilt, so a query after mapping() equals one on a fresh cache."""
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    nm, dec, pts = surface_map(200, device=dev, buffer_size=1 << 22, query_backend="grid")
+    for p in dec.parameters():
+        p.requires_grad_(False)
+    q = surface_pool(pts, 5000, seed=3, device=dev)[0]
+    coord, label, ts = surface_pool(pts, 20000, seed=4, device=dev)
+    before = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True, want_certainty=True)
+    mapper = P.Mapper(nm.config, None, nm, dec)
+    mapper.set_pool(coord, label, ts)
+    mapper.mapping(2)
+    after = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True, want_certainty=True)
+    nm._cache = {}
+    fresh = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True, want_certainty=True)
+    assert not torch.equal(before[0], fresh[0])          # training moved the SDF
+    for a, b in zip(after, fresh):
+        if a is not None:
+            assert torch.equal(a, b)

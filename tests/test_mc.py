@@ -121,3 +121,9 @@ def test_kernel_edge_cases(dev):
     assert faces.shape[0] == 8 and verts.shape[0] == 6
     with pytest.raises(ValueError):
         marching_cubes(torch.ones((1, 4, 4), device=dev))
+    # the drop-in mc_mesh returns an empty mesh instead (the reference's try/except,
+    # utils/mesher.py:324-333)
+    import pin_slam_amd as P
+    m = P.Mesher(P.Config(device=dev), None, None)
+    wv, wf = m.mc_mesh(np.ones((1, 4, 4), np.float32), None, 0.1, np.array([1.0, 2.0, 3.0]))
+    assert wv.shape == (0, 3) and wf.shape == (0, 3)

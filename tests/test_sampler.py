@@ -166,3 +166,22 @@ def test_deskew_kernel_matches_oracle(dev):
                         torch.as_tensor(T, device=dev))
         np.testing.assert_allclose(got.cpu().numpy()[:, :3], want[:, :3], rtol=0, atol=2e-5)
         np.testing.assert_array_equal(got.cpu().numpy()[:, 3], p[:, 3])
+
+
+def test_pool_append_prefix_view_copies():
+    """_pool_append appends in place only onto the view it returned last time: a truncated
+    prefix view gets a fresh buffer (the rows past it are not overwritten), and the result
+    type-promotes like torch.cat."""
+    import torch
+    from pin_slam_amd.mapper import Mapper
+    m = Mapper.__new__(Mapper)
+    a = m._pool_append("x", torch.empty((0, 3)), torch.arange(30.).view(10, 3))
+    b = m._pool_append("x", a, torch.full((2, 3), -1.0))
+    assert b.data_ptr() == a.data_ptr() and b.shape[0] == 12          # in place
+    head = b[:5]
+    tail_before = b[5:12].clone()
+    c = m._pool_append("x", head, torch.full((4, 3), 7.0))
+    assert torch.equal(b[5:12], tail_before)                          # older view untouched
+    assert torch.equal(c, torch.cat((head, torch.full((4, 3), 7.0))))
+    d = m._pool_append("y", torch.zeros(3, dtype=torch.float32), torch.ones(2, dtype=torch.float64))
+    assert d.dtype == torch.float64
