@@ -153,16 +153,23 @@ struct HashSource {
 // Payload = compact record index.  FAT: features / certainty come from the compact record
 // (one line per candidate); otherwise from the live PinPoints arrays.
 // one of 8 registers by a per-lane 3-bit index, as a select tree (no scratch)
+__device__ __forceinline__ uint32_t sel4v(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int k);
 __device__ __forceinline__ uint32_t sel8(const uint32_t (&w)[8], int k) {
-    const uint32_t a0 = (k & 1) ? w[1] : w[0], a1 = (k & 1) ? w[3] : w[2];
-    const uint32_t a2 = (k & 1) ? w[5] : w[4], a3 = (k & 1) ? w[7] : w[6];
-    const uint32_t b0 = (k & 2) ? a1 : a0, b1 = (k & 2) ? a3 : a2;
-    return (k & 4) ? b1 : b0;
+    const uint32_t lo = sel4v(w[0], w[1], w[2], w[3], k), hi = sel4v(w[4], w[5], w[6], w[7], k);
+    return (k & 4) ? hi : lo;
 }
 
 // one of 4 registers by a per-lane 2-bit index
 __device__ __forceinline__ uint32_t sel4(const uint32_t* w, int k) {
     const uint32_t a0 = (k & 1) ? w[1] : w[0], a1 = (k & 1) ? w[3] : w[2];
+    return (k & 2) ? a1 : a0;
+}
+
+// The same on four values.  Callers that pick between two register quads must select the
+// VALUES (sel4v of each quad, then a select): a pointer select (w vs w + 4) makes the compiler
+// spill the array to scratch and index it there -- a vector-memory round trip per lookup.
+__device__ __forceinline__ uint32_t sel4v(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int k) {
+    const uint32_t a0 = (k & 1) ? w1 : w0, a1 = (k & 1) ? w3 : w2;
     return (k & 2) ? a1 : a0;
 }
 
@@ -242,8 +249,12 @@ struct GridSource {
                 const int cx = lx + ((col & 255) - 128);
                 const int cy = ly + (((col >> 8) & 255) - 128);
                 const int kxy = ((cx >> 2) - bx0) | (((cy >> 2) - by0) << 1);
-                const uint32_t lo0 = sel4(wl, kxy), hi0 = sel4(wh, kxy);
-                const uint32_t lo1 = sel4(wl + 4, kxy), hi1 = sel4(wh + 4, kxy);
+                const uint32_t lo0 = sel4v(wl[0], wl[1], wl[2], wl[3], kxy);
+                const uint32_t hi0 = sel4v(wh[0], wh[1], wh[2], wh[3], kxy);
+                const uint32_t lo1 = sel4v(wl[4], wl[5], wl[6], wl[7], kxy);
+                const uint32_t hi1 = sel4v(wh[4], wh[5], wh[6], wh[7], kxy);
+                const uint32_t pre0 = sel4v(wp[0], wp[1], wp[2], wp[3], kxy);
+                const uint32_t pre1 = sel4v(wp[4], wp[5], wp[6], wp[7], kxy);
                 const int sh = ((cx & 3) << 4) | ((cy & 3) << 2);
                 const uint32_t n0 = (uint32_t)((((uint64_t)hi0 << 32) | lo0) >> sh) & 15u;
                 const uint32_t n1 = (uint32_t)((((uint64_t)hi1 << 32) | lo1) >> sh) & 15u;
@@ -254,7 +265,7 @@ struct GridSource {
                     run &= run - 1u;
                     const bool up = z >= 4;
                     const uint64_t bits = up ? (((uint64_t)hi1 << 32) | lo1) : (((uint64_t)hi0 << 32) | lo0);
-                    const uint32_t pre = up ? sel4(wp + 4, kxy) : sel4(wp, kxy);
+                    const uint32_t pre = up ? pre1 : pre0;
                     const int bit = sh | (z & 3);
                     s_list[cnt][tid] = (int)(pre + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
                     ++cnt;

@@ -338,6 +338,17 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 1
+    // profiling variant: candidate scan only (the top-k kept live through one output)
+    if (i >= 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < kK; ++j) s += tk.d[j] + (float)tk.g[j];
+        sdf_out[i] = s;
+        nn_out[i] = nn;
+    }
+    return;
+#endif
     query_sdf_epilogue<WF, PGO, GRAD>(src, p, m, qx, qy, qz, tk, nn, i, nn_k, zero_empty, sdf_out, grad_out, nn_out,
                                       cert_out, std_out);
 }

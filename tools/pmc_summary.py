@@ -9,7 +9,7 @@ import sys
 
 def main(root, match=""):
     agg = collections.defaultdict(list)
-    for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
             if match and match not in name:
