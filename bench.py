@@ -5,8 +5,8 @@ Workload (BASELINE.json configs[1]): synthetic 1M-point
 surface map (1000 x 1000 voxels of 0.3 m, hash table B = 5e7), 262,144 queries
 per step = map points + N(0, 0.25^2), Kc = 33 cells (num_nei_cells 2, alpha 0.2),
 k = 8, F = 8, decoder 11 -> 64 -> 1, weighted_first, fp32, query_locally=False.
-One step = Tracker/Mesher's fused query over the batch (pin_query_order: a tile-grouped
-processing order, then one pin_query_sdf_grid launch), inputs resident in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
+One step = Tracker/Mesher's fused query over the batch (pin_query_sort: the queries
+counting-sorted into spatial tiles, then one pin_query_sdf_grid_sorted launch), inputs resident in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
 batch against its replica of the map ("weak" scaling, no data-path collective);
 the barrier + max-over-ranks timing is the only collective.
 
@@ -19,7 +19,7 @@ RCCL when N > 1).
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
 mean duration of the SDF+grad kernel alone (HIP events on the launch stream around
-pin_query_sdf_grid with the order precomputed); the ordering pass is reported beside it.  cpu_baseline: the numpy oracle
+pin_query_sdf_grid_sorted with the sort precomputed); the ordering pass is reported beside it.  cpu_baseline: the numpy oracle
 (oracle/pin_oracle.py, single thread) on one full batch, rank 0 at N=1 only.
 """
 import argparse
@@ -120,10 +120,10 @@ def cpu_baseline(nm, dec, q, wf):
 def time_kernel(nm, dec, q, wf, backend, steps):
     """Mean duration (ms) of the headline kernel alone -- HIP events on the launch stream around
     each pin_query_sdf(_grid) launch, with the tile order precomputed -- and of the ordering pass
-    (pin_query_order) that each step also runs."""
+    (pin_query_sort) that each step also runs."""
     import ctypes  # noqa: F401
     from pin_slam_amd import _lib
-    from pin_slam_amd.query import mlp_view, query_order
+    from pin_slam_amd.query import mlp_view, query_sort
     n = q.shape[0]
     hv, pv = nm._views("global", False)
     mv = mlp_view(dec)
@@ -133,15 +133,14 @@ def time_kernel(nm, dec, q, wf, backend, steps):
     std = None if wf else torch.empty(n, device=q.device)
     if backend == "grid":
         gv = nm.grid_view("global", True)
-        order = query_order(gv, q)
+        q4 = query_sort(gv, q)
 
         def launch():
-            _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0,
-                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.ptr(order),
-                      _lib.stream())
+            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, 8, int(wf), 0,
+                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
 
         def order_pass():
-            query_order(gv, q)
+            query_sort(gv, q, out=q4)
     else:
         def launch():
             _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0, _lib.ptr(sdf),

@@ -245,18 +245,31 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
                   const float* features, const float* certainties, float* crec, float* cfeat, float* ccert,
                   int32_t* cgid, void* stream);
 
-/* Workspace bytes of pin_query_order for n queries. */
+/* Workspace of pin_query_order / pin_query_sort: PIN_ORDER_STATE_BYTES of state (per-tile
+ * totals and a done counter) that must be ZERO before the first call on a workspace and that
+ * every call leaves zero again (calls sharing one workspace must be ordered on one stream), then
+ * 8 bytes per query. */
+#define PIN_ORDER_STATE_BYTES 4352
 static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
-    return 4 * 1024 * ((n + 1023) / 1024 + 1);
+    return PIN_ORDER_STATE_BYTES + 8 * n;
 }
 
 /*
  * pin_query_order -- a processing order for a random query batch: order[0..n) is a permutation
- * of the query indices grouped into <= 1024 spatial tiles of the grid box (one radix pass, two
- * launches, no global atomics).  Feeding it to pin_query_sdf_grid gives better line sharing
- * and per-XCD L2 locality; results do not depend on the order.
+ * of the query indices grouped into <= 1024 spatial tiles of the grid box (a counting sort:
+ * two launches, one returning global atomic per (block, tile)).  Feeding it to
+ * pin_query_sdf_grid gives better line sharing and per-XCD L2 locality; results do not depend
+ * on the order (the order inside a tile is not deterministic).
  */
 int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* order, void* workspace, void* stream);
+
+/*
+ * pin_query_sort -- the same tile sort, writing the queries themselves in tile order:
+ * q4[4 * pos .. 4 * pos + 3] = {x, y, z, bits(i)} (int32 index i in the last float's bits);
+ * order (may be NULL) as pin_query_order.  Input of pin_query_sdf_grid_sorted.
+ */
+int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
+                   void* stream);
 
 /*
  * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  order (n ints,
@@ -266,6 +279,14 @@ int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* ord
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
                        int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
                        int32_t* nn_count, float* certainty, float* sdf_std, const int32_t* order, void* stream);
+
+/*
+ * pin_query_sdf_grid_sorted -- pin_query_sdf_grid over queries pre-sorted by pin_query_sort
+ * (q4 [n,4]: coordinates + original index); outputs go to each query's original index.
+ */
+int pin_query_sdf_grid_sorted(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
+                              int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                              float* grad, int32_t* nn_count, float* certainty, float* sdf_std, void* stream);
 
 /* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
  * (features always read live from pts->features; gids from grid->cgid). */

@@ -116,6 +116,9 @@ _SIGS = {
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_query_sort": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_sdf_grid_sorted": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_mc_workspace_bytes": [i64, i64, i64],
     "pin_mc_count": [c_void_p, c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p],
     "pin_mc_emit": [c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -191,7 +194,23 @@ def ptr(t):
     return c_void_p(t.data_ptr())
 
 
+try:
+    _raw_stream = torch._C._cuda_getCurrentRawStream   # no Stream object per call (~0.2 vs ~3 us)
+except AttributeError:   # pragma: no cover
+    _raw_stream = None
+
+
 def stream(device=None):
+    """The current HIP stream of ``device`` (default: the current device) as a c_void_p."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = torch.device(device).index
+            idx = torch.cuda.current_device() if idx is None else idx
+        return c_void_p(_raw_stream(idx))
     return c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -141,11 +141,22 @@ struct NbInput {
 template <bool PGO, bool CERT, class Src>
 __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints& p, int pay, bool valid, float qx,
                                                  float qy, float qz, NbInput& o) {
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 2
+    // profiling variant: no record re-gather (wrong positions, same instruction stream otherwise)
+    const float4 r = make_float4(qx + 0.1f, qy - 0.1f, qz + 0.05f * (float)(pay & 7), __int_as_float(pay));
+#else
     const float4 r = src.record(pay);
+#endif
     const int raw = __float_as_int(r.w);
     const int64_t id = valid ? (raw & kIdMask) : 0;
     float4 f0, f1;
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 3
+    // profiling variant: no feature gathers
+    f0 = make_float4(r.x * 0.01f, r.y * 0.01f, r.z * 0.01f, 0.02f);
+    f1 = make_float4(r.y * 0.02f, r.z * 0.02f, r.x * 0.03f, -0.02f);
+#else
     src.features(pay, id, f0, f1);
+#endif
     o.pg[0] = qx - r.x;
     o.pg[1] = qy - r.y;
     o.pg[2] = qz - r.z;
@@ -237,7 +248,14 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
             }
         }
         float gx[kD];
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 4
+        // profiling variant: no decoder (a linear stand-in with the same outputs' shapes)
+        sdf = 0.f;
+#pragma unroll
+        for (int d = 0; d < kD; ++d) { gx[d] = 0.01f * (float)(d + 1); sdf = fmaf(x[d], gx[d], sdf); }
+#else
         sdf = mlp_sdf<GRAD, 0, kD>(m, x, gx);
+#endif
         if (nn == 0 && zero_empty) sdf = 0.f;
         if (GRAD && nn > 0) {
             float abar = 0.f;
@@ -328,13 +346,12 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
 }
 
 template <bool WF, bool PGO, bool GRAD, class Src>
-__device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const MlpW& m,
-                                               const float* __restrict__ q, int64_t i, int nn_k, int zero_empty,
+__device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& p, const MlpW& m, float qx, float qy,
+                                               float qz, int64_t i, int nn_k, int zero_empty,
                                                float* __restrict__ sdf_out, float* __restrict__ grad_out,
                                                int* __restrict__ nn_out, float* __restrict__ cert_out,
                                                float* __restrict__ std_out) {
-    const int64_t iq = i >= 0 ? i : 0;   // i < 0: no query (the lane only completes its wave)
-    const float qx = q[3 * iq], qy = q[3 * iq + 1], qz = q[3 * iq + 2];
+    // i < 0: no query (the lane only completes its wave); nothing is written for it
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
@@ -363,19 +380,23 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const HashSource src(h, p);
-    query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+    query_sdf_body<WF, PGO, GRAD>(src, p, mw, q[3 * i], q[3 * i + 1], q[3 * i + 2], i, nn_k, zero_empty, sdf_out,
+                                  grad_out, nn_out, cert_out, std_out);
 }
 
 #ifndef PIN_SDF_WAVES
 #define PIN_SDF_WAVES 2   // waves per SIMD the fused grid kernel is compiled for (VGPR budget)
 #endif
 
+// q4 != NULL: the queries pre-sorted by pin_query_sort, {x, y, z, bits(original index)} each
+// (one coalesced 16-B load, no order -> coordinate dependency); otherwise q [n,3] processed in
+// `order` (or input order).
 template <bool WF, bool PGO, bool GRAD, bool FAT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PGO ? 1 : PIN_SDF_WAVES)))
-k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q, int64_t n,
-                 int nn_k, int zero_empty, float* __restrict__ sdf_out, float* __restrict__ grad_out,
-                 int* __restrict__ nn_out, float* __restrict__ cert_out, float* __restrict__ std_out,
-                 const int* __restrict__ order) {
+k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q,
+                 const float4* __restrict__ q4, int64_t n, int nn_k, int zero_empty, float* __restrict__ sdf_out,
+                 float* __restrict__ grad_out, int* __restrict__ nn_out, float* __restrict__ cert_out,
+                 float* __restrict__ std_out, const int* __restrict__ order) {
     __shared__ float s_mlp[kWSize];
     MlpW mw = stage_mlp(m, s_mlp);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
@@ -390,25 +411,39 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
 #else
     if (t >= n) return;
 #endif
-    const int64_t i = t < n ? (order ? order[t] : t) : -1;
+    const int64_t tt = t < n ? t : 0;
+    float qx, qy, qz;
+    int64_t i;
+    if (q4) {
+        const float4 v = q4[tt];
+        qx = v.x; qy = v.y; qz = v.z;
+        const int iw = __float_as_int(v.w);
+        i = (t < n && iw >= 0 && iw < n) ? iw : -1;
+    } else {
+        i = t < n ? (order ? order[t] : t) : -1;
+        const int64_t iq = i >= 0 ? i : 0;
+        qx = q[3 * iq]; qy = q[3 * iq + 1]; qz = q[3 * iq + 2];
+    }
     const GridSource<FAT> src(g, p);
-    query_sdf_body<WF, PGO, GRAD>(src, p, mw, q, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out, std_out);
+    query_sdf_body<WF, PGO, GRAD>(src, p, mw, qx, qy, qz, i, nn_k, zero_empty, sdf_out, grad_out, nn_out, cert_out,
+                                  std_out);
 }
 
-// Query tiling: one radix-partition pass of the queries into <= 1024 spatial tiles of the grid
-// box (cubes of 2^shift cells; the host picks the smallest shift >= 3 with <= 1024 tiles).
-// Random batches are then processed tile by tile: a block's gathers share lines and, with
-// xcd_block(), each XCD's L2 holds one region of the map (random 262K-query batch on a 1M map:
-// 104 -> 65 us for the SDF+grad kernel).  Order inside a tile is arbitrary; every query's
-// outputs still go to its own index, so results are unchanged.
+// Query tiling: one counting-sort pass of the queries into <= 1024 spatial tiles of the grid box
+// (cubes of 2^shift cells; the host picks the smallest shift >= 3 with <= 1024 tiles).  Random
+// batches are then processed tile by tile: a block's gathers share lines and, with xcd_block(),
+// each XCD's L2 holds one region of the map.  Order inside a tile is arbitrary (it depends on
+// atomic arrival); every query's outputs still go to its own index, so results are unchanged.
+//
+//   k_tile_rank   per block: LDS tile histogram (the returning LDS atomic is the query's rank in
+//                 its tile within the block), then one returning global atomic per (block, tile)
+//                 reserves the block's run inside the tile: off = run + rank, stored per query
+//   k_tile_place  per block: exclusive scan of the 1024 tile totals -> tile bases; each query
+//                 lands at base[tile] + off.  The last block to finish zeroes the totals again.
+// Workspace state (PIN_ORDER_STATE_BYTES): tile totals + a done counter, zero before the first
+// call and zero again after each call; then n int2 (tile, off).
 constexpr int kMaxTiles = 1024;
-constexpr int kPartThreads = 1024;   // one thread per tile in the scatter's prefix step
-#ifndef PIN_PART_BATCH
-#define PIN_PART_BATCH 64                // count-matrix rows loaded per round trip in the scatter
-#endif
-#ifndef PIN_PART_ROWS
-#define PIN_PART_ROWS 64                 // max count-matrix rows (blocks) before PER doubles
-#endif
+constexpr int kPartThreads = 1024;   // one tile per thread in the atomic and scan phases
 
 struct TileMap {
     int64_t ox, oy, oz;
@@ -424,10 +459,14 @@ __device__ __forceinline__ int tile_of(float x, float y, float z, const TileMap&
     return (axis(z, t.oz, t.ntz) * t.nty + axis(y, t.oy, t.nty)) * t.ntx + axis(x, t.ox, t.ntx);
 }
 
-// the PER queries of one thread: all coordinate loads first, then the tiles
+// Both kernels issue every load of a thread before using any (one memory round trip per phase).
 template <int PER>
-__device__ __forceinline__ void load_tiles(const float* __restrict__ q, int64_t n, const TileMap& t, int (&tile)[PER]) {
-    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + threadIdx.x;
+__global__ void __launch_bounds__(kPartThreads)
+k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ tot, int2* __restrict__ tk) {
+    __shared__ int h[kMaxTiles];
+    const int k = threadIdx.x;
+    h[k] = 0;
+    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + k;
     float x[PER], y[PER], z[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -437,71 +476,76 @@ __device__ __forceinline__ void load_tiles(const float* __restrict__ q, int64_t 
         y[u] = q[3 * j + 1];
         z[u] = q[3 * j + 2];
     }
+    int tile[PER], rank[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) tile[u] = lo + (int64_t)u * kPartThreads < n ? tile_of(x[u], y[u], z[u], t) : -1;
-}
-
-// per-block tile histogram (LDS atomics) -> cnt[block][tile] (one coalesced row)
-template <int PER>
-__global__ void __launch_bounds__(kPartThreads)
-k_part_count(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ cnt) {
-    __shared__ int h[kMaxTiles];
-    for (int k = threadIdx.x; k < t.ntiles; k += kPartThreads) h[k] = 0;
-    int tile[PER];
-    load_tiles<PER>(q, n, t, tile);
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < PER; ++u)
-        if (tile[u] >= 0) atomicAdd(h + tile[u], 1);
+    for (int u = 0; u < PER; ++u) rank[u] = tile[u] >= 0 ? atomicAdd(h + tile[u], 1) : 0;
     __syncthreads();
-    for (int k = threadIdx.x; k < t.ntiles; k += kPartThreads) cnt[(int64_t)blockIdx.x * t.ntiles + k] = h[k];
+    const int c = h[k];
+    const int run = c ? atomicAdd(tot + k, c) : 0;   // this block's run inside tile k
+    __syncthreads();
+    h[k] = run;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int64_t i = lo + (int64_t)u * kPartThreads;
+        if (tile[u] >= 0) tk[i] = make_int2(tile[u], h[tile[u]] + rank[u]);
+    }
 }
 
-// Each block reads the whole count matrix: thread k sums tile k's column (all blocks, and the
-// blocks before this one), a 1024-wide scan of the column totals gives the tile bases, and the
-// block's queries are placed at base + LDS-atomic rank.  No separate scan launch.
 template <int PER>
 __global__ void __launch_bounds__(kPartThreads)
-k_part_scatter(const float* __restrict__ q, int64_t n, TileMap t, const int* __restrict__ cnt, int nblk,
-               int* __restrict__ order) {
+k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict__ tot, unsigned* __restrict__ done,
+             const int2* __restrict__ tk, float4* __restrict__ q4, int* __restrict__ order) {
     __shared__ int base[kMaxTiles];
     __shared__ int wsum[kPartThreads / 64];
-    int tile[PER];
-    load_tiles<PER>(q, n, t, tile);
+    __shared__ int last;
     const int k = threadIdx.x;
-    int pre = 0, tot = 0;
-    if (k < t.ntiles) {
-        // all rows of the column in flight, PIN_PART_BATCH at a time (nblk <= ~100)
-        for (int b = 0; b < nblk; b += PIN_PART_BATCH) {
-            int v[PIN_PART_BATCH];
+    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + k;
+    const int v = k < ntiles ? tot[k] : 0;
+    int2 e[PER];
+    float x[PER], y[PER], z[PER];
 #pragma unroll
-            for (int u = 0; u < PIN_PART_BATCH; ++u)
-                v[u] = b + u < nblk ? cnt[(int64_t)(b + u) * t.ntiles + k] : 0;
-#pragma unroll
-            for (int u = 0; u < PIN_PART_BATCH; ++u) {
-                tot += v[u];
-                pre += b + u < (int)blockIdx.x ? v[u] : 0;
-            }
+    for (int u = 0; u < PER; ++u) {
+        const int64_t i = lo + (int64_t)u * kPartThreads;
+        const int64_t j = i < n ? i : 0;
+        e[u] = tk[j];
+        if (q4) {
+            x[u] = q[3 * j];
+            y[u] = q[3 * j + 1];
+            z[u] = q[3 * j + 2];
         }
     }
-    int incl = tot;
+    // exclusive scan of the tile totals, one per thread
+    int incl = v;
     for (int o = 1; o < 64; o <<= 1) {
-        const int x = __shfl_up(incl, o);
-        if ((k & 63) >= o) incl += x;
+        const int w = __shfl_up(incl, o);
+        if ((k & 63) >= o) incl += w;
     }
     if ((k & 63) == 63) wsum[k >> 6] = incl;
     __syncthreads();
-    int tb = incl - tot;
-    for (int w = 0; w < (k >> 6); ++w) tb += wsum[w];
-    if (k < t.ntiles) base[k] = tb + pre;
+    // after the barrier every wave of the block has its total in hand: count the block as done
+    // (the returning atomic's latency overlaps the placement below; its value is used at the end)
+    unsigned ticket = 0;
+    if (k == 0) ticket = atomicInc(done, gridDim.x - 1);   // wraps back to 0 after the last block
+    int run = incl - v;
+    for (int w = 0; w < (k >> 6); ++w) run += wsum[w];
+    base[k] = run;
     __syncthreads();
-    int pos[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) pos[u] = tile[u] >= 0 ? atomicAdd(base + tile[u], 1) : -1;
-    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < PER; ++u)
-        if (pos[u] >= 0) order[pos[u]] = (int)(lo + (int64_t)u * kPartThreads);
+    for (int u = 0; u < PER; ++u) {
+        const int64_t i = lo + (int64_t)u * kPartThreads;
+        const int64_t pos = (int64_t)base[e[u].x & (kMaxTiles - 1)] + e[u].y;
+        if (i >= n || pos < 0 || pos >= n) continue;   // pos: only a workspace whose state was not zeroed
+        if (q4) q4[pos] = make_float4(x[u], y[u], z[u], __int_as_float((int)i));
+        if (order) order[pos] = (int)i;
+    }
+    // every block read the totals before its atomicInc: the last one clears them for the next call
+    if (k == 0) last = ticket == gridDim.x - 1;
+    __syncthreads();
+    if (last) tot[k] = 0;
 }
 
 // host: tile map of a grid box
@@ -528,27 +572,25 @@ TileMap tile_map(const PinGrid& g) {
     return t;
 }
 
-// order[0..n) = the queries grouped by tile; workspace = pin_query_order_workspace_bytes(n).  8 queries
-// per thread (32 blocks at 256K queries) up to 512K queries, 16 per thread beyond, so the count
-// matrix each scatter block reads stays small (~100 rows at 1.6M).
-int partition_queries(const PinGrid& g, const float* q, int64_t n, void* workspace, hipStream_t s, int*& order,
-                      int* out) {
+// the tile sort of q: q4 (may be NULL) = {x, y, z, bits(i)} in tile order, order (may be NULL) =
+// the indices in tile order; workspace = pin_query_order_workspace_bytes(n) with zeroed state.
+// 4 queries per thread up to 512K queries (64 blocks at 256K), 16 beyond (<= ~256 blocks at
+// 4M): few blocks keep the same-address atomics on the tile totals few.
+int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* order, void* workspace,
+                 hipStream_t s) {
     const TileMap t = tile_map(g);
-    order = out;
-    int* cnt = (int*)workspace;
-    // the fewest queries per thread that keep the count matrix within PIN_PART_ROWS rows
-    // (each scatter thread reads its tile's whole column)
+    char* ws = (char*)workspace;
+    int* tot = (int*)ws;
+    unsigned* done = (unsigned*)(ws + 4 * kMaxTiles);
+    int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
     auto launch = [&](auto per_tag) {
         constexpr int PER = decltype(per_tag)::value;
         const int nblk = (int)((n + PER * kPartThreads - 1) / (PER * kPartThreads));
-        hipLaunchKernelGGL(k_part_count<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt);
-        hipLaunchKernelGGL(k_part_scatter<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, cnt, nblk, order);
+        hipLaunchKernelGGL(k_tile_rank<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot, tk);
+        hipLaunchKernelGGL(k_tile_place<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot, done, tk,
+                           q4, order);
     };
-    const int64_t rows = PIN_PART_ROWS;
-    if (n <= rows * 1 * kPartThreads) launch(std::integral_constant<int, 1>());
-    else if (n <= rows * 2 * kPartThreads) launch(std::integral_constant<int, 2>());
-    else if (n <= rows * 4 * kPartThreads) launch(std::integral_constant<int, 4>());
-    else if (n <= rows * 8 * kPartThreads) launch(std::integral_constant<int, 8>());
+    if (n <= (1 << 19)) launch(std::integral_constant<int, 4>());
     else launch(std::integral_constant<int, 16>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
@@ -896,13 +938,20 @@ static bool grid_ok(const PinGrid* g) {
 int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* order, void* workspace, void* stream) {
     if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !order || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
-    int* o = nullptr;
-    return partition_queries(*grid, q, n, workspace, as_stream(stream), o, (int*)order);
+    return sort_queries(*grid, q, n, nullptr, (int*)order, workspace, as_stream(stream));
 }
 
-int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
-                       int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
-                       int32_t* nn_count, float* certainty, float* sdf_std, const int32_t* order, void* stream) {
+int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
+                   void* stream) {
+    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !q4 || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
+}
+
+static int query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                          const float* q4, int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty,
+                          float* sdf, float* grad, int32_t* nn_count, float* certainty, float* sdf_std,
+                          const int32_t* order, void* stream) {
     if (!grid_ok(grid) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
         return PIN_ERR_ARG;
     const bool fat = grid->fat != 0;
@@ -910,13 +959,14 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
         return PIN_ERR_ARG;
     if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
     if (n == 0) return PIN_OK;
-    if (!q || n > INT32_MAX) return PIN_ERR_ARG;
+    if ((!q && !q4) || n > INT32_MAX) return PIN_ERR_ARG;
     const bool g = grad != nullptr;
     const bool pgo = pts->after_pgo != 0;
     auto s = as_stream(stream);
 #define PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT)                                                                     \
     hipLaunchKernelGGL((k_query_sdf_grid<WF, PGO, GRAD, FAT>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, *mlp, \
-                       q, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std, (const int*)order)
+                       q, (const float4*)q4, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std,        \
+                       (const int*)order)
 #define PIN_SDFG_FAT(WF, PGO, GRAD) \
     do { if (fat) PIN_LAUNCH_SDFG(WF, PGO, GRAD, true); else PIN_LAUNCH_SDFG(WF, PGO, GRAD, false); } while (0)
     if (weighted_first) {
@@ -929,6 +979,22 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
 #undef PIN_SDFG_FAT
 #undef PIN_LAUNCH_SDFG
     return launch_status();
+}
+
+int pin_query_sdf_grid_sorted(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
+                              int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                              float* grad, int32_t* nn_count, float* certainty, float* sdf_std, void* stream) {
+    if (n > 0 && !q4) return PIN_ERR_ARG;
+    return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                          certainty, sdf_std, nullptr, stream);
+}
+
+int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,
+                       int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf, float* grad,
+                       int32_t* nn_count, float* certainty, float* sdf_std, const int32_t* order, void* stream) {
+    if (n > 0 && !q) return PIN_ERR_ARG;
+    return query_sdf_grid(grid, pts, mlp, q, nullptr, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                          certainty, sdf_std, order, stream);
 }
 
 int pin_query_feature_fwd_grid(const PinGrid* grid, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,

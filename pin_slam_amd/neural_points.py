@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .query import QueryFeatureFn, hash_view, points_view
+from .query import QueryFeatureFn, hash_view, points_view, tensor_key
 
 PRIMES = (73856093, 19349669, 83492791)
 
@@ -404,17 +404,30 @@ class NeuralPoints(nn.Module):
         return crec, cfeat, ccert, cgid
 
     def grid_view(self, mode: str, fat: bool):
-        from .query import _View
-        bricks, dims, n_occ = self.occupancy()
-        crec, cfeat, ccert, cgid = self.compact_records(mode, fat)
+        """PinGrid view of a query mode, reused while the occupancy grid, the compact records and the
+        neighbourhood tables it points into are the same objects."""
+        occ = self.occupancy()
+        comp = self.compact_records(mode, fat)
         offs = self._offset_table()
+        key = (id(occ), id(comp), id(offs), self.neighbor_window, self._num_columns, os.environ.get("PIN_GRID_SCAN"))
+        hit = self.__dict__.setdefault("_grid_view_cache", {}).get((mode, bool(fat)))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        v = self._grid_view(occ, comp, offs, fat)
+        self._grid_view_cache[(mode, bool(fat))] = (key, v)
+        return v
+
+    def _grid_view(self, occ, comp, offs, fat):
+        from .query import _View
+        bricks, dims, n_occ = occ
+        crec, cfeat, ccert, cgid = comp
         g = _lib.PinGrid(bricks=bricks.data_ptr(), dims=dims, crec=crec.data_ptr(), cgid=cgid.data_ptr(),
                          n_occ=n_occ, offsets=offs.data_ptr(), resolution=float(np.float32(self.resolution)),
                          num_cells=int(self.neighbor_K), max_valid_dist2=float(np.float32(self.max_valid_dist2)),
                          cfeat=cfeat.data_ptr() if cfeat is not None else None,
                          ccert=ccert.data_ptr() if ccert is not None else None, fat=int(fat), window=99 if os.environ.get("PIN_GRID_SCAN") == "cells" else self.neighbor_window,
                          num_columns=0 if os.environ.get("PIN_GRID_SCAN") == "bricks" else self._num_columns)
-        return _View(g, (bricks, crec, cfeat, ccert, cgid, offs))
+        return _View(g, (bricks, crec, cfeat, ccert, cgid, offs, occ, comp))
 
     # ------------------------------------------------------------------ map maintenance
     def _travel_dist_dev(self, device):
@@ -693,14 +706,26 @@ class NeuralPoints(nn.Module):
 
     # ------------------------------------------------------------------ queries
     def _views(self, mode: str, query_locally: bool):
+        """(PinHash view, PinPoints view) of a query mode, reused while every tensor they are built
+        from is unchanged (tensor_key) -- a query call then costs no view rebuild."""
         rec = self.records(mode)
-        hv = hash_view(self)
         if query_locally:
-            pv = points_view(rec, self.local_geo_features.data, self.local_neural_points,
-                             self.local_point_orientations, self.local_point_certainties, self.after_pgo)
+            src = (self.local_geo_features, self.local_neural_points, self.local_point_orientations,
+                   self.local_point_certainties)
         else:
-            pv = points_view(rec, self.geo_features, self.neural_points, self.point_orientations,
-                             self.point_certainties, self.after_pgo)
+            src = (self.geo_features, self.neural_points, self.point_orientations, self.point_certainties)
+        key = (mode, bool(query_locally), bool(self.after_pgo), tensor_key((rec, self.buffer_pt_index) + src),
+               float(self.resolution), int(self.buffer_size), int(self.neighbor_K), float(self.max_valid_dist2),
+               id(self._cells))
+        hit = self.__dict__.setdefault("_view_cache", {}).get((mode, bool(query_locally)))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        hv = hash_view(self)
+        f = src[0].data if isinstance(src[0], nn.Parameter) else src[0]
+        pv = points_view(rec, f, src[1], src[2], src[3], self.after_pgo)
+        # the key is taken after hash_view, which may build the cell table
+        key = key[:-1] + (id(self._cells),)
+        self._view_cache[(mode, bool(query_locally))] = (key, (hv, pv))
         return hv, pv
 
     def radius_neighborhood_search(self, points: torch.Tensor, time_filtering: bool = False):

@@ -2,6 +2,7 @@
 Function behind ``NeuralPoints.query_feature`` and the fused SDF(+gradient) call
 used by the tracker and mesher paths."""
 import ctypes
+from ctypes import c_void_p
 import os
 
 import numpy as np
@@ -56,8 +57,32 @@ def points_view(records, features, positions, orientations, certainties, after_p
     return v
 
 
+def tensor_key(ts):
+    """Identity, storage pointer and version of each tensor (None kept): a derived view built from
+    them is reusable while this tuple compares equal (in-place writes bump _version; the kernels'
+    raw-pointer writes bump it through NeuralPoints.mark_modified)."""
+    return tuple((id(t), t.data_ptr(), t._version) if t is not None else None for t in ts)
+
+
 def mlp_view(decoder) -> _View:
-    """PinMlp over a hidden_level=1, out_dim=1 geo decoder (model/decoder.py:16-57)."""
+    """PinMlp over a hidden_level=1, out_dim=1 geo decoder (model/decoder.py:16-57); cached on the
+    decoder until a parameter is replaced or modified."""
+    try:
+        ps = (decoder.layers[0].weight, decoder.layers[0].bias, decoder.lout.weight, decoder.lout.bias)
+    except (AttributeError, IndexError):
+        ps = None
+    if ps is not None and len(decoder.layers) == 1:
+        key = (tensor_key(ps), float(decoder.sdf_scale))
+        hit = decoder.__dict__.get("_pin_mlp_view")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        v = _mlp_view(decoder)
+        decoder.__dict__["_pin_mlp_view"] = (key, v)
+        return v
+    return _mlp_view(decoder)
+
+
+def _mlp_view(decoder) -> _View:
     if len(decoder.layers) != 1 or decoder.out_dim != 1 or decoder.layers[0].bias is None:
         raise NotImplementedError("fused SDF kernels implement geo_mlp_level=1, out_dim=1, bias on")
     W1 = _f32(decoder.layers[0].weight)
@@ -123,22 +148,49 @@ class QueryFeatureFn(torch.autograd.Function):
         return grad_q, grad_f, None, None, None, None, None
 
 
+ORDER_STATE_BYTES = 4352   # PIN_ORDER_STATE_BYTES
+_order_ws = {}
+
+
+def order_workspace(n, device, stream_handle=None):
+    """Workspace of pin_query_order / pin_query_sort: its state bytes must be zero before the
+    first call and every call leaves them zero, so one zero-initialised buffer per (device,
+    stream) is kept and grown (calls on one stream are ordered)."""
+    key = (str(device), _lib.stream(device).value if stream_handle is None else stream_handle)
+    need = ORDER_STATE_BYTES + 8 * max(n, 1)
+    ws = _order_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros((max(need, 2 * (ws.numel() if ws is not None else 0)),), dtype=torch.uint8, device=device)
+        _order_ws[key] = ws
+    return ws
+
+
 def query_order(gv, q):
     """pin_query_order: a tile-grouped processing order for the queries q [N,3] (device int32)."""
     n = q.shape[0]
     order = torch.empty((n,), dtype=torch.int32, device=q.device)
-    ws = torch.empty((1024 * ((n + 1023) // 1024 + 1),), dtype=torch.int32, device=q.device)  # pin_query_order_workspace_bytes / 4
+    ws = order_workspace(n, q.device)
     _lib.call("pin_query_order", gv.ref(), _lib.ptr(q), n, _lib.ptr(order), _lib.ptr(ws), _lib.stream())
     return order
 
 
+def query_sort(gv, q, out=None):
+    """pin_query_sort: the queries q [N,3] in tile order as [N,4] f32 rows {x, y, z, bits(index)}."""
+    n = q.shape[0]
+    q4 = out if out is not None else torch.empty((n, 4), dtype=torch.float32, device=q.device)
+    ws = order_workspace(n, q.device)
+    _lib.call("pin_query_sort", gv.ref(), _lib.ptr(q), n, _lib.ptr(q4), None, _lib.ptr(ws), _lib.stream(q.device))
+    return q4
+
+
 def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
-              want_certainty=True, nn_k=None, weighted_first=None):
+              want_certainty=True, nn_k=None, weighted_first=None, sorted_rows=None):
     """Fused query_feature + Decoder.sdf (+ analytic dSDF/dq) in one kernel.
 
     Returns (sdf [N], grad [N,3] or None, nn_count [N] int32, certainty [N] or None,
     sdf_std [N] or None).  Semantics: utils/tracker.py:176-260 (query_locally=True) and
-    utils/mesher.py:41-136 (query_locally=False, zero_empty=True)."""
+    utils/mesher.py:41-136 (query_locally=False, zero_empty=True).  sorted_rows: q already sorted
+    by query_sort."""
     _lib.require_device(points)
     q = points.detach().to(torch.float32).contiguous()
     n = q.shape[0]
@@ -155,10 +207,15 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
     if nm.backend() == "grid":
         gv = nm.grid_view(mode, True)
-        order = query_order(gv, q) if (_TILE_QUERIES and n >= _TILE_MIN) else None
-        _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
-                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.ptr(order),
-                  _lib.stream())
+        if sorted_rows is not None or (_TILE_QUERIES and n >= _TILE_MIN):
+            q4 = sorted_rows if sorted_rows is not None else query_sort(gv, q)
+            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, nn_k, int(wf),
+                      int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
+                      _lib.ptr(std), _lib.stream())
+        else:
+            _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
+                      int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
+                      _lib.ptr(std), None, _lib.stream())
     else:
         _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
                   _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())

@@ -250,28 +250,53 @@ def test_random_map_vs_oracle(dev, wf, backend):
 
 @pytest.mark.parametrize("wf", [True, False])
 def test_query_order_is_a_permutation_and_invisible(dev, wf):
-    """pin_query_order groups a random batch by spatial tile; pin_query_sdf_grid's outputs are
-    bitwise identical with and without it (the order only changes which lane runs a query)."""
+    """pin_query_order / pin_query_sort group a random batch by spatial tile (a counting sort whose
+    workspace state is left zero by every call, so repeated calls stay valid); the SDF kernel's
+    outputs are bitwise identical in input order, in `order` and over the sorted float4 rows
+    (the order only changes which lane runs a query)."""
     from pin_slam_amd import _lib
-    from pin_slam_amd.query import mlp_view, query_order
+    from pin_slam_amd.query import mlp_view, query_order, query_sort
     nm, dec, pts = H.surface_map(300, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend="grid")
     q = H.surface_queries(pts, 70001, device=dev)
     gv = nm.grid_view("global", True)
-    order = query_order(gv, q)
-    assert torch.equal(torch.sort(order.long())[0], torch.arange(q.shape[0], device=dev))
+    for _ in range(3):
+        order = query_order(gv, q)
+        assert torch.equal(torch.sort(order.long())[0], torch.arange(q.shape[0], device=dev))
+    q4 = query_sort(gv, q)
+    idx = q4[:, 3].contiguous().view(torch.int32).long()
+    assert torch.equal(torch.sort(idx)[0], torch.arange(q.shape[0], device=dev))
+    assert torch.equal(q4[:, :3], q[idx])
+    # tile grouping: the tile id along the sorted rows never returns to an earlier tile
+    d = gv.struct.dims
+    inv = 1.0 / torch.tensor(np.float32(nm.resolution), dtype=torch.float32, device=dev)   # the kernel's rule
+    cell = torch.floor(q4[:, :3] * inv).long() - torch.tensor([d.ox, d.oy, d.oz], device=dev)
+    ext = torch.tensor([4 * d.nbx, 4 * d.nby, 4 * d.nbz], device=dev)
+    sh = 3
+    while int(torch.prod((ext + (1 << sh) - 1) >> sh)) > 1024:
+        sh += 1
+    nt = (ext + (1 << sh) - 1) >> sh
+    tc = torch.minimum(torch.clamp(cell >> sh, min=0), nt - 1)
+    tile = (tc[:, 2] * nt[1] + tc[:, 1]) * nt[0] + tc[:, 0]
+    starts = torch.nonzero(tile[1:] != tile[:-1]).numel() + 1
+    assert starts == torch.unique(tile).numel()
     hv, pv = nm._views("global", False)
     mv = mlp_view(dec)
     outs = []
-    for o in (None, order):
+    for o in (None, order, "sorted"):
         sdf = torch.empty(q.shape[0], device=dev)
         grad = torch.empty((q.shape[0], 3), device=dev)
         nn = torch.empty(q.shape[0], dtype=torch.int32, device=dev)
         std = torch.empty(q.shape[0], device=dev)
-        _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), q.shape[0], 8, int(wf), 0,
-                  _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.ptr(o), _lib.stream())
+        if isinstance(o, str):
+            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), q.shape[0], 8, int(wf),
+                      0, _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
+        else:
+            _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), q.shape[0], 8, int(wf), 0,
+                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.ptr(o), _lib.stream())
         outs.append((sdf, grad, nn, std))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def test_backend_selection(golden, dev):
@@ -343,3 +368,4 @@ def test_tracking_loop_fixture(golden, dev, case):
         assert abs(cnt - int(z["tracking_valid_count"][i])) <= 3
     assert bool(valid) == bool(z["tracking_valid"])
     np.testing.assert_allclose(_np(T), z["tracking_T"], atol=1e-4)
+
