@@ -249,14 +249,14 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
  * totals and a done counter) that must be ZERO before the first call on a workspace and that
  * every call leaves zero again (calls sharing one workspace must be ordered on one stream), then
  * 8 bytes per query. */
-#define PIN_ORDER_STATE_BYTES 4352
+#define PIN_ORDER_STATE_BYTES 16640
 static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
     return PIN_ORDER_STATE_BYTES + 8 * n;
 }
 
 /*
  * pin_query_order -- a processing order for a random query batch: order[0..n) is a permutation
- * of the query indices grouped into <= 1024 spatial tiles of the grid box (a counting sort:
+ * of the query indices grouped into <= 4096 spatial tiles of the grid box (a counting sort:
  * two launches, one returning global atomic per (block, tile)).  Feeding it to
  * pin_query_sdf_grid gives better line sharing and per-XCD L2 locality; results do not depend
  * on the order (the order inside a tile is not deterministic).
@@ -287,6 +287,16 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
 int pin_query_sdf_grid_sorted(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
                               int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
                               float* grad, int32_t* nn_count, float* certainty, float* sdf_std, void* stream);
+
+/*
+ * pin_query_sdf_grid_tiled -- pin_query_sort into q4 ([n,4] f32 scratch) followed by
+ * pin_query_sdf_grid_sorted, in one call (the launches leave the host back to back);
+ * workspace as pin_query_order.  Outputs go to each query's own index.
+ */
+int pin_query_sdf_grid_tiled(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                             int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                             float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
+                             void* workspace, void* stream);
 
 /* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
  * (features always read live from pts->features; gids from grid->cgid). */

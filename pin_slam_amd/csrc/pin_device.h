@@ -543,15 +543,29 @@ struct MlpW {
     float* xs;        // per-wave LDS scratch (64 x 12 floats) of the MFMA decoder, or nullptr
 };
 
+#ifndef PIN_MLP_ROWS
+#define PIN_MLP_ROWS 0   // 1: W1 staged row-major and decoded one hidden unit at a time (mlp_sdf_rows)
+#endif
+
 // W1[c][i] in the staged layout
-__device__ __forceinline__ int w1_at(int c, int i) { return (c >> 1) * kWPair + 2 * i + (c & 1); }
+__device__ __forceinline__ int w1_at(int c, int i) {
+    return PIN_MLP_ROWS ? c * kWRow + i : (c >> 1) * kWPair + 2 * i + (c & 1);
+}
 
 // all threads of the block must call this (it ends with a barrier)
 __device__ __forceinline__ MlpW stage_mlp(const PinMlp& m, float* s_w) {
     for (int e = threadIdx.x; e < kWSize; e += blockDim.x) {
         float v = 0.f;
         if (e < kWB1) {
-            const int pr = e / kWPair, r = e - pr * kWPair, i = r >> 1, c = 2 * pr + (r & 1);
+            int c, i;
+            if (PIN_MLP_ROWS) {
+                c = e / kWRow;
+                i = e - c * kWRow;
+            } else {
+                const int pr = e / kWPair, r = e - pr * kWPair;
+                i = r >> 1;
+                c = 2 * pr + (r & 1);
+            }
             v = i < kD ? m.W1[c * kD + i] : 0.f;
         } else if (e < kWW2) {
             v = m.b1[e - kWB1];
@@ -578,7 +592,7 @@ __device__ __forceinline__ void load_row(const float* __restrict__ w, int c, flo
 //   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
 // One pass over the hidden units, two at a time with packed FMAs (v_pk_fma_f32).
 template <bool GRAD, int OFF, int NOUT>
-__device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+__device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
     f32x2 out2 = {0.f, 0.f};
     f32x2 g2[NOUT];
 #pragma unroll
@@ -607,6 +621,46 @@ __device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], fl
         for (int i = 0; i < NOUT; ++i) gx[i] = (g2[i].x + g2[i].y) * m.sdf_scale;
     }
     return ((out2.x + out2.y) + m.w[kWB2]) * m.sdf_scale;
+}
+
+// The same decoder one hidden unit at a time with plain FMAs (v_fma_f32 issues in 2 cycles per
+// wave64 on a SIMD-32, so packing buys no FLOP rate on gfx950): the W1 row comes from LDS as
+// three 16-B broadcast reads, and only x, the gradient accumulators and one row are live --
+// about 40 VGPRs instead of the packed form's ~90, which is what lets the fused SDF+gradient
+// kernel fit 128 VGPRs (4 waves per SIMD).
+template <bool GRAD, int OFF, int NOUT>
+__device__ __forceinline__ float mlp_sdf_rows(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+    float out = 0.f;
+    float g[NOUT];
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) g[i] = 0.f;
+#pragma unroll PIN_MLP_UNROLL
+    for (int c = 0; c < kH; ++c) {
+        const float* __restrict__ wr = m.w + c * kWRow;   // row-major staging (PIN_MLP_ROWS)
+        const float4 w0 = *(const float4*)(wr), w1 = *(const float4*)(wr + 4), w2 = *(const float4*)(wr + 8);
+        const float w[kWRow] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w};
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kD; ++i) acc = fmaf(w[i], x[i], acc);
+        const float pre = acc + m.w[kWB1 + c];
+        const float a = pre > 0.f ? m.w[kWW2 + c] : 0.f;
+        out = fmaf(a, pre, out);
+        if (GRAD) {
+#pragma unroll
+            for (int i = 0; i < NOUT; ++i) g[i] = fmaf(a, w[OFF + i], g[i]);
+        }
+    }
+    if (GRAD) {
+#pragma unroll
+        for (int i = 0; i < NOUT; ++i) gx[i] = g[i] * m.sdf_scale;
+    }
+    return (out + m.w[kWB2]) * m.sdf_scale;
+}
+
+template <bool GRAD, int OFF, int NOUT>
+__device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+    if constexpr (PIN_MLP_ROWS != 0) return mlp_sdf_rows<GRAD, OFF, NOUT>(m, x, gx);
+    else return mlp_sdf_packed<GRAD, OFF, NOUT>(m, x, gx);
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

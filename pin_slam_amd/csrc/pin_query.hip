@@ -429,8 +429,8 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
                                   std_out);
 }
 
-// Query tiling: one counting-sort pass of the queries into <= 1024 spatial tiles of the grid box
-// (cubes of 2^shift cells; the host picks the smallest shift >= 3 with <= 1024 tiles).  Random
+// Query tiling: one counting-sort pass of the queries into <= kMaxTiles spatial tiles of the grid
+// box (cubes of 2^shift cells; the host picks the smallest shift >= 3 with <= kMaxTiles tiles).  Random
 // batches are then processed tile by tile: a block's gathers share lines and, with xcd_block(),
 // each XCD's L2 holds one region of the map.  Order inside a tile is arbitrary (it depends on
 // atomic arrival); every query's outputs still go to its own index, so results are unchanged.
@@ -438,12 +438,17 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
 //   k_tile_rank   per block: LDS tile histogram (the returning LDS atomic is the query's rank in
 //                 its tile within the block), then one returning global atomic per (block, tile)
 //                 reserves the block's run inside the tile: off = run + rank, stored per query
-//   k_tile_place  per block: exclusive scan of the 1024 tile totals -> tile bases; each query
+//   k_tile_place  per block: exclusive scan of the tile totals -> tile bases; each query
 //                 lands at base[tile] + off.  The last block to finish zeroes the totals again.
 // Workspace state (PIN_ORDER_STATE_BYTES): tile totals + a done counter, zero before the first
 // call and zero again after each call; then n int2 (tile, off).
-constexpr int kMaxTiles = 1024;
-constexpr int kPartThreads = 1024;   // one tile per thread in the atomic and scan phases
+#ifndef PIN_MAX_TILES
+#define PIN_MAX_TILES 4096
+#endif
+constexpr int kMaxTiles = PIN_MAX_TILES;   // 16x16-cell columns on the 1000x1000 surface: ~one wave per tile
+constexpr int kPartThreads = 1024;
+constexpr int kTpt = kMaxTiles / kPartThreads;   // tiles per thread in the atomic and scan phases
+static_assert(kMaxTiles % kPartThreads == 0, "tile capacity must be a multiple of the block");
 
 struct TileMap {
     int64_t ox, oy, oz;
@@ -465,7 +470,8 @@ __global__ void __launch_bounds__(kPartThreads)
 k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ tot, int2* __restrict__ tk) {
     __shared__ int h[kMaxTiles];
     const int k = threadIdx.x;
-    h[k] = 0;
+#pragma unroll
+    for (int j = 0; j < kTpt; ++j) h[k + j * kPartThreads] = 0;
     const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + k;
     float x[PER], y[PER], z[PER];
 #pragma unroll
@@ -483,10 +489,15 @@ k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__
 #pragma unroll
     for (int u = 0; u < PER; ++u) rank[u] = tile[u] >= 0 ? atomicAdd(h + tile[u], 1) : 0;
     __syncthreads();
-    const int c = h[k];
-    const int run = c ? atomicAdd(tot + k, c) : 0;   // this block's run inside tile k
+    int run[kTpt];
+#pragma unroll
+    for (int j = 0; j < kTpt; ++j) {   // this block's run inside each tile (independent returning atomics)
+        const int c = h[k + j * kPartThreads];
+        run[j] = c ? atomicAdd(tot + k + j * kPartThreads, c) : 0;
+    }
     __syncthreads();
-    h[k] = run;
+#pragma unroll
+    for (int j = 0; j < kTpt; ++j) h[k + j * kPartThreads] = run[j];
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -504,7 +515,12 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
     __shared__ int last;
     const int k = threadIdx.x;
     const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + k;
-    const int v = k < ntiles ? tot[k] : 0;
+    int v[kTpt], sum = 0;   // thread k owns tiles kTpt*k .. kTpt*k + kTpt-1 (consecutive)
+#pragma unroll
+    for (int j = 0; j < kTpt; ++j) {
+        v[j] = kTpt * k + j < ntiles ? tot[kTpt * k + j] : 0;
+        sum += v[j];
+    }
     int2 e[PER];
     float x[PER], y[PER], z[PER];
 #pragma unroll
@@ -518,21 +534,25 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
             z[u] = q[3 * j + 2];
         }
     }
-    // exclusive scan of the tile totals, one per thread
-    int incl = v;
+    // exclusive scan of the tile totals
+    int incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
         const int w = __shfl_up(incl, o);
         if ((k & 63) >= o) incl += w;
     }
     if ((k & 63) == 63) wsum[k >> 6] = incl;
     __syncthreads();
-    // after the barrier every wave of the block has its total in hand: count the block as done
+    // after the barrier every wave of the block has its totals in hand: count the block as done
     // (the returning atomic's latency overlaps the placement below; its value is used at the end)
     unsigned ticket = 0;
     if (k == 0) ticket = atomicInc(done, gridDim.x - 1);   // wraps back to 0 after the last block
-    int run = incl - v;
+    int run = incl - sum;
     for (int w = 0; w < (k >> 6); ++w) run += wsum[w];
-    base[k] = run;
+#pragma unroll
+    for (int j = 0; j < kTpt; ++j) {
+        base[kTpt * k + j] = run;
+        run += v[j];
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -545,7 +565,10 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
     // every block read the totals before its atomicInc: the last one clears them for the next call
     if (k == 0) last = ticket == gridDim.x - 1;
     __syncthreads();
-    if (last) tot[k] = 0;
+    if (last) {
+#pragma unroll
+        for (int j = 0; j < kTpt; ++j) tot[k + j * kPartThreads] = 0;
+    }
 }
 
 // host: tile map of a grid box
@@ -582,6 +605,7 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     char* ws = (char*)workspace;
     int* tot = (int*)ws;
     unsigned* done = (unsigned*)(ws + 4 * kMaxTiles);
+    static_assert(4 * kMaxTiles + 64 <= PIN_ORDER_STATE_BYTES, "order workspace state too small");
     int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
     auto launch = [&](auto per_tag) {
         constexpr int PER = decltype(per_tag)::value;
@@ -985,6 +1009,20 @@ int pin_query_sdf_grid_sorted(const PinGrid* grid, const PinPoints* pts, const P
                               int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
                               float* grad, int32_t* nn_count, float* certainty, float* sdf_std, void* stream) {
     if (n > 0 && !q4) return PIN_ERR_ARG;
+    return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                          certainty, sdf_std, nullptr, stream);
+}
+
+int pin_query_sdf_grid_tiled(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                             int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                             float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
+                             void* workspace, void* stream) {
+    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !q4 || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    // the three launches leave the host back to back: the query kernel is queued before the
+    // sort has finished, so the GPU does not wait for the host between them
+    const int rc = sort_queries(*grid, q, n, (float4*)q4, nullptr, workspace, as_stream(stream));
+    if (rc != PIN_OK) return rc;
     return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
                           certainty, sdf_std, nullptr, stream);
 }

@@ -148,7 +148,7 @@ class QueryFeatureFn(torch.autograd.Function):
         return grad_q, grad_f, None, None, None, None, None
 
 
-ORDER_STATE_BYTES = 4352   # PIN_ORDER_STATE_BYTES
+ORDER_STATE_BYTES = 16640   # PIN_ORDER_STATE_BYTES
 _order_ws = {}
 
 
@@ -207,11 +207,17 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
     if nm.backend() == "grid":
         gv = nm.grid_view(mode, True)
-        if sorted_rows is not None or (_TILE_QUERIES and n >= _TILE_MIN):
-            q4 = sorted_rows if sorted_rows is not None else query_sort(gv, q)
-            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, nn_k, int(wf),
+        if sorted_rows is not None:
+            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(sorted_rows), n, nn_k,
+                      int(wf), int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
+                      _lib.ptr(std), _lib.stream(dev))
+        elif _TILE_QUERIES and n >= _TILE_MIN:
+            # tile sort + sorted query in one call (pin_query_sdf_grid_tiled)
+            q4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
+            ws = order_workspace(n, dev)
+            _lib.call("pin_query_sdf_grid_tiled", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
                       int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
-                      _lib.ptr(std), _lib.stream())
+                      _lib.ptr(std), _lib.ptr(q4), _lib.ptr(ws), _lib.stream(dev))
         else:
             _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
                       int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),

@@ -272,7 +272,7 @@ def test_query_order_is_a_permutation_and_invisible(dev, wf):
     cell = torch.floor(q4[:, :3] * inv).long() - torch.tensor([d.ox, d.oy, d.oz], device=dev)
     ext = torch.tensor([4 * d.nbx, 4 * d.nby, 4 * d.nbz], device=dev)
     sh = 3
-    while int(torch.prod((ext + (1 << sh) - 1) >> sh)) > 1024:
+    while int(torch.prod((ext + (1 << sh) - 1) >> sh)) > 4096:
         sh += 1
     nt = (ext + (1 << sh) - 1) >> sh
     tc = torch.minimum(torch.clamp(cell >> sh, min=0), nt - 1)
