@@ -319,8 +319,11 @@ typedef struct PinTrainCfg {
     float weight_e;              /* eikonal weight (mapper.py:547) */
     float grad_scale;            /* multiplies loss and gradients: 1, or 1/world_size so that a SUM
                                     all-reduce of per-rank gradients is the gradient of the mean loss */
-    int32_t reserved;
+    int32_t flags;               /* PIN_TRAIN_ROWS: `coord` of pin_train_forward holds every row (batch and
+                                    stencil, pin_train_rows / pin_train_gather) instead of the batch */
 } PinTrainCfg;
+
+#define PIN_TRAIN_ROWS 1
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
 typedef struct PinTrainState {
@@ -351,6 +354,15 @@ typedef struct PinAdamStep {
 
 /* pin_train_rows -- coordinates [rows,3] of every row of one iteration (batch + stencil). */
 int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, void* stream);
+
+/*
+ * pin_train_gather -- Mapper.get_batch's gathers (utils/mapper.py:352-356) fused with the row
+ * build: rows_out [rows,3] = every row of the iteration from coord_pool[index] (batch rows, then
+ * the stencil of every decimation-th one), label_out [n_main] = label_pool[index] and, when
+ * ts_pool is non-NULL, ts_out [n_main] = ts_pool[index].  index: [n_main] int64 pool rows.
+ */
+int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool, const int64_t* index,
+                     const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out, void* stream);
 
 /*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping

@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PIN_LIB") or os.path.join(_HERE, "libpin_slam_amd.so")
 
 PIN_OK = 0
+PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 
 FEATURE_DIM = 8
@@ -70,7 +71,7 @@ class PinMlp(ctypes.Structure):
 
 class PinTrainCfg(ctypes.Structure):
     _fields_ = [("n_main", i64), ("n_stencil", i64), ("decimation", i32), ("nn_k", i32), ("weighted_first", i32),
-                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("reserved", i32)]
+                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("flags", i32)]
 
 
 class PinTrainState(ctypes.Structure):
@@ -130,6 +131,8 @@ _SIGS = {
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_rows": [c_void_p, _P(PinTrainCfg), c_void_p, c_void_p],
+    "pin_train_gather": [c_void_p, c_void_p, c_void_p, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p, c_void_p,
+                         c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,

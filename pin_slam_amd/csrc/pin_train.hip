@@ -28,7 +28,7 @@ inline int launch_status() { return hipGetLastError() == hipSuccess ? PIN_OK : P
 // row r of the iteration: a main query or a stencil query (x+,x-,y+,y-,z+,z- blocks)
 __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const PinTrainCfg& c, int64_t r, float& qx,
                                           float& qy, float& qz) {
-    if (r < c.n_main) {
+    if (r < c.n_main || (c.flags & PIN_TRAIN_ROWS)) {   // a batch row, or every row materialized
         qx = coord[3 * r];
         qy = coord[3 * r + 1];
         qz = coord[3 * r + 2];
@@ -54,7 +54,7 @@ template <bool WF, class Src>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
-                                                   float (&cw)[kK]) {
+                                                   float (&cw)[kK], int64_t& qts_out) {
     // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
     const int64_t r = st.order ? st.order[t] : t;
     float qx, qy, qz;
@@ -75,6 +75,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     for (int d = 0; d < kD; ++d) x[d] = 0.f;
     float sdf = 0.f;
     const int64_t qts = (ts && r < c.n_main) ? ts[r] : -1;
+    qts_out = qts;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
@@ -99,15 +100,15 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         }
         cid[j] = valid ? id : -1;
         cw[j] = w;
+#if !PIN_CERT_T8
         if (valid) {
             // training side effects (neural_points.py:640, :644); ts: read first, the max is
             // usually a no-op
-#if !PIN_CERT_T8
             if (st.certainties) atomicAdd(st.certainties + id, w);
-#endif
             if (qts >= 0 && st.ts_update && st.ts_update[id] < qts)
                 atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
         }
+#endif
         if (WF) {
 #pragma unroll
             for (int d = 0; d < kD; ++d) x[d] = x[d] + (valid ? xj[d] : 0.f) * w;
@@ -133,27 +134,49 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     st.sdf[r] = sdf;
 }
 
-// The certainty side effect is a float atomic add per (row, neighbour): memory-side, and with
-// one lane per row every wave-instruction hits 64 unrelated 64-B segments (the slow shape,
-// MI355X_MICROARCH.md Global float atomics).  Flushed transposed instead -- through LDS, 8 lanes
-// per row, 8 rows per instruction -- a row's neighbours (adjacent cells) share segments.
-__device__ __forceinline__ void flush_certainty(float* __restrict__ cert, const int (&cid)[kK], const float (&cw)[kK]) {
+// The training side effects (neural_points.py:640 certainty scatter_add, :644 ts amax) are one
+// memory-side atomic per (row, neighbour); with one lane per row every wave-instruction would hit
+// 64 unrelated 64-B segments (the slow shape, MI355X_MICROARCH.md Global float atomics).  Both are
+// flushed transposed instead -- through LDS, 8 lanes per row, 8 rows per instruction: a row's
+// neighbours (adjacent cells) share segments, and the ts reads (the max is usually a no-op) are
+// issued together instead of one dependent read per neighbour inside the streaming loop.
+__device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int64_t* __restrict__ ts_update,
+                                                   const int (&cid)[kK], const float (&cw)[kK], int64_t qts) {
 #if PIN_CERT_T8
     __shared__ int s_id[kBlock * kK];
     __shared__ float s_w[kBlock * kK];
+    __shared__ int64_t s_ts[kBlock];
     const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         s_id[tid * kK + j] = cid[j];
         s_w[tid * kK + j] = cw[j];
     }
+    s_ts[tid] = qts;
     __syncthreads();
     const int base = (tid & ~63) * kK, lane = tid & 63;
+    if (cert) {
 #pragma unroll
-    for (int u = 0; u < kK; ++u) {
-        const int e = base + u * 64 + lane;
-        const int id = s_id[e];
-        if (id >= 0) atomicAdd(cert + id, s_w[e]);
+        for (int u = 0; u < kK; ++u) {
+            const int e = base + u * 64 + lane;
+            const int id = s_id[e];
+            if (id >= 0) atomicAdd(cert + id, s_w[e]);
+        }
+    }
+    if (ts_update) {
+        int64_t cur[kK];
+#pragma unroll
+        for (int u = 0; u < kK; ++u) {
+            const int e = base + u * 64 + lane;
+            const int id = s_id[e];
+            cur[u] = (id >= 0 && s_ts[e / kK] >= 0) ? ts_update[id] : INT64_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < kK; ++u) {
+            const int e = base + u * 64 + lane;
+            const int64_t q = s_ts[e / kK];
+            if (cur[u] < q) atomicMax((unsigned long long*)(ts_update + s_id[e]), (unsigned long long)q);
+        }
     }
 #endif
 }
@@ -167,13 +190,14 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
     int cid[kK];
     float cw[kK];
+    int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (t < c.n_main + 6 * c.n_stencil) {
         const HashSource src(h, p);
-        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw);
+        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts);
     }
-    if (st.certainties) flush_certainty(st.certainties, cid, cw);
+    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
 }
 
 template <bool WF>
@@ -185,14 +209,15 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
     int cid[kK];
     float cw[kK];
+    int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (t < c.n_main + 6 * c.n_stencil) {
         const GridSource<false> src(g, p);
-        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw);
+        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts);
     }
 #ifndef PIN_CERT_SKIP
-    if (st.certainties) flush_certainty(st.certainties, cid, cw);
+    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
 #endif
 }
 
@@ -200,7 +225,42 @@ __global__ void __launch_bounds__(kBlock)
 k_train_rows(const float* __restrict__ coord, PinTrainCfg c, float* __restrict__ out) {
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main + 6 * c.n_stencil) return;
+    c.flags &= ~PIN_TRAIN_ROWS;
     row_coord(coord, c, r, out[3 * r], out[3 * r + 1], out[3 * r + 2]);
+}
+
+// one thread per batch row: the row, its label and ts gathered from the pool and, for every
+// decimation-th row, its six stencil rows pool[index[k*dec]] +- eps e_a (mapper.py:697-702) --
+// the pool is read once per batch row
+__global__ void __launch_bounds__(kBlock)
+k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool, const int64_t* __restrict__ tpool,
+               const int64_t* __restrict__ index, PinTrainCfg c, float* __restrict__ rows, float* __restrict__ label,
+               int64_t* __restrict__ ts) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= c.n_main) return;
+    const int64_t i = index[r];
+    const float qx = cpool[3 * i], qy = cpool[3 * i + 1], qz = cpool[3 * i + 2];
+    const float lb = lpool[i];
+    const int64_t tv = tpool ? tpool[i] : 0;
+    rows[3 * r] = qx;
+    rows[3 * r + 1] = qy;
+    rows[3 * r + 2] = qz;
+    label[r] = lb;
+    if (tpool) ts[r] = tv;
+    if (c.n_stencil > 0 && r % c.decimation == 0 && r / c.decimation < c.n_stencil) {
+        const int64_t k = r / c.decimation;
+#pragma unroll
+        for (int blk = 0; blk < 6; ++blk) {
+            float x = qx, y = qy, z = qz;
+            if ((blk >> 1) == 0) x = (blk & 1) ? x - c.eps : x + c.eps;
+            else if ((blk >> 1) == 1) y = (blk & 1) ? y - c.eps : y + c.eps;
+            else z = (blk & 1) ? z - c.eps : z + c.eps;
+            float* o = rows + 3 * (c.n_main + blk * c.n_stencil + k);
+            o[0] = x;
+            o[1] = y;
+            o[2] = z;
+        }
+    }
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
@@ -356,18 +416,27 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     if (!grad_features) return;
     // scatter: element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour)
     // pairs x 32 contiguous bytes, one memory-side request each -- the cheapest atomic shape
-    // measured (LDS pre-aggregation per block, and 64-B rows carrying the certainty, were slower)
+    // measured (LDS pre-aggregation per block, and 64-B rows carrying the certainty, were slower).
+    // The block's ids (and WF weights) are staged in LDS first with coalesced loads, so the
+    // scatter loop issues its atomics back to back instead of waiting on a load per element.
+    __shared__ int s_ids[kBlock * kK];
+    __shared__ float s_wt[WF ? kBlock * kK : 1];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int total = kBlock * nn_k * kF;
+    const int nrow_blk = (int)(nrows - row0 < kBlock ? nrows - row0 : kBlock);
+    const int npair = nrow_blk * nn_k;
+    for (int e = threadIdx.x; e < npair; e += kBlock) {
+        s_ids[e] = st.ids[row0 * nn_k + e];
+        if (WF) s_wt[e] = st.weights[row0 * nn_k + e];
+    }
+    __syncthreads();
+    const int total = npair * kF;
     for (int e = threadIdx.x; e < total; e += kBlock) {
         const int d = e & (kF - 1);
         const int rj = e >> 3;
-        const int lr = rj / nn_k, j = rj - lr * nn_k;
-        const int64_t rr = row0 + lr;
-        if (rr >= nrows) break;
-        const int id = st.ids[rr * nn_k + j];
+        const int id = s_ids[rj];
         if (id < 0) continue;
-        const float g = WF ? st.weights[rr * nn_k + j] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        const int lr = rj / nn_k, j = rj - lr * nn_k;
+        const float g = WF ? s_wt[rj] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
         atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }
@@ -448,6 +517,18 @@ int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, 
     if (rows == 0) return PIN_OK;
     if (!coord || !rows_out) return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_train_rows, grid_for(rows), dim3(kBlock), 0, as_stream(stream), coord, *cfg, rows_out);
+    return launch_status();
+}
+
+int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool, const int64_t* index,
+                     const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out, void* stream) {
+    if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
+    if (cfg->n_stencil > 0 && (cfg->n_stencil - 1) * (int64_t)cfg->decimation >= cfg->n_main) return PIN_ERR_ARG;
+    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    if (rows == 0) return PIN_OK;
+    if (!coord_pool || !label_pool || !index || !rows_out || !label_out || (ts_pool && !ts_out)) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_train_gather, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream), coord_pool,
+                       label_pool, ts_pool, index, *cfg, rows_out, label_out, ts_out);
     return launch_status();
 }
 

@@ -52,6 +52,9 @@ class _TrainBuffers:
             self.weights = torch.empty((rows, nn_k), dtype=torch.float32, device=device)
             self.x = torch.empty((rows, D) if wf else (rows, nn_k, 3), dtype=torch.float32, device=device)
             self.sdf = torch.empty((rows,), dtype=torch.float32, device=device)
+            self.rows = torch.empty((rows, 3), dtype=torch.float32, device=device)
+            self.label = torch.empty((rows,), dtype=torch.float32, device=device)
+            self.ts = torch.empty((rows,), dtype=torch.int64, device=device)
             nblk = (rows + 255) // 256
             self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_GRAD_SIZE * 4,), dtype=torch.uint8,
                                          device=device)
@@ -255,8 +258,8 @@ class Mapper:
         self.weight_pool = torch.ones_like(sdf_label) if weight is None else weight
         self.pool_sample_count = int(sdf_label.shape[0])
 
-    def get_batch(self, global_coord=False):
-        """utils/mapper.py:323-361."""
+    def _batch_index(self):
+        """The pool rows of one batch: get_batch's sampling (utils/mapper.py:323-350), same draws."""
         stop = getattr(self.dataset, "stop_status", False) if self.dataset is not None else False
         bs = int(self.config.bs)
         bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
@@ -267,11 +270,13 @@ class Mapper:
                 bs_history = bs - bs_new
                 index_history = torch.randint(0, self.pool_sample_count, (bs_history,), device=self.device)
                 index_new_batch = torch.randint(0, new_idx_count, (bs_new,), device=self.device)
-                index = torch.cat((index_history, self.new_idx[index_new_batch]), dim=0)
-            else:
-                index = torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
-        else:
-            index = torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+                return torch.cat((index_history, self.new_idx[index_new_batch]), dim=0)
+            return torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+        return torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+
+    def get_batch(self, global_coord=False):
+        """utils/mapper.py:323-361."""
+        index = self._batch_index()
         coord = self.global_coord_pool[index, :] if global_coord else self.coord_pool[index, :]
         sdf_label = self.sdf_label_pool[index]
         ts = self.time_pool[index]
@@ -335,11 +340,18 @@ class Mapper:
             m_v = torch.zeros_like(m_grad)
         cert_before = nm.local_point_certainties.clone() if world > 1 else None
         self._adam_t = 0
+        # get_batch's gathers fused into the row build (pin_train_gather) when the pools allow it;
+        # a get_batch replaced on the instance (tests, callers) is honoured
+        fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
         for _ in range(iter_count):
-            coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
-            if self.ba_done_flag:
-                coord = transform_batch_torch(coord, self.used_poses[ts])
-            self.train_step(coord, sdf_label, ts, f_grad, m_grad, world)
+            if fused:
+                self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad, world,
+                                index=self._batch_index())
+            else:
+                coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
+                if self.ba_done_flag:
+                    coord = transform_batch_torch(coord, self.used_poses[ts])
+                self.train_step(coord, sdf_label, ts, f_grad, m_grad, world)
             self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
             self.total_iter += 1
         if world > 1:
@@ -349,16 +361,30 @@ class Mapper:
             cert.copy_(cert_before + cert_delta)
         nm.assign_local_to_global()
 
-    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1):
+    def _pools_fusable(self):
+        c, l, t = self.global_coord_pool, self.sdf_label_pool, self.time_pool
+        return (c is not None and c.is_cuda and c.dtype == torch.float32 and c.is_contiguous() and c.dim() == 2
+                and l is not None and l.dtype == torch.float32 and l.is_contiguous()
+                and (t is None or (t.dtype == torch.int64 and t.is_contiguous())))
+
+    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None):
         """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
-        SUM all-reduced over the group when world > 1.  Returns the device loss tensor."""
+        SUM all-reduced over the group when world > 1.  Returns the device loss tensor.
+        index ([N] int64): coord / sdf_label / ts are then the sample pools and the batch is their
+        rows `index` (get_batch's gathers done by pin_train_gather)."""
         c = self.config
         nm = self.neural_points
-        q = coord.detach().to(torch.float32).contiguous()
-        _lib.require_device(q)
-        label = sdf_label.detach().to(torch.float32).contiguous()
-        ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
-        n = q.shape[0]
+        if index is None:
+            q = coord.detach().to(torch.float32).contiguous()
+            _lib.require_device(q)
+            label = sdf_label.detach().to(torch.float32).contiguous()
+            ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
+            n = q.shape[0]
+        else:
+            q = coord
+            _lib.require_device(q)
+            index = index.to(device=q.device, dtype=torch.int64).contiguous()
+            n = index.shape[0]
         if grad_features is not None and (grad_features.shape[1] != 8 or not grad_features.is_contiguous()):
             raise ValueError("grad_features must be a contiguous [L+1, 8] float32 tensor")
         dec = int(c.gradient_decimation)
@@ -373,16 +399,26 @@ class Mapper:
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
                                sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
-                               grad_scale=float(np.float32(1.0 / world)), reserved=0)
+                               grad_scale=float(np.float32(1.0 / world)), flags=0)
         hv, pv = nm._views("local", True)
         s = _lib.stream()
         grid = nm.backend() == "grid"
         gv = nm.grid_view("local", False) if grid else None
+        # every row of the iteration (batch + stencil) materialised once: the tile sort and the
+        # forward read it
+        rows_xyz = b.rows
+        if index is None:
+            _lib.call("pin_train_rows", _lib.ptr(q), ctypes.byref(cfg), _lib.ptr(rows_xyz), s)
+        else:
+            label = b.label
+            ts64 = b.ts if ts is not None else None
+            _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(index),
+                      ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), s)
+        cfg.flags = _lib.PIN_TRAIN_ROWS
+        q = rows_xyz
         order = None
         if grid and _TILE_QUERIES and rows >= _TILE_MIN:
             # process the rows tile by tile (pin_query_order over the batch + stencil coordinates)
-            rows_xyz = torch.empty((rows, 3), dtype=torch.float32, device=q.device)
-            _lib.call("pin_train_rows", _lib.ptr(q), ctypes.byref(cfg), _lib.ptr(rows_xyz), s)
             order = query_order(gv, rows_xyz)
         self._order = order
         st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),

@@ -214,3 +214,31 @@ def test_fat_cache_sees_training_writes(dev):
     for a, b in zip(after, fresh):
         if a is not None:
             assert torch.equal(a, b)
+
+
+def test_fused_gather_path_matches_get_batch(dev):
+    """mapping() with get_batch's gathers fused into pin_train_gather gives the same features,
+    certainties and ts as mapping() through get_batch (same draws: the batch index is drawn by
+    the same code), up to float-atomic reordering of the gradient sums."""
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    outs = []
+    for fused in (True, False):
+        nm, dec, pts = surface_map(300, device=dev, buffer_size=1 << 22, query_backend="grid", bs=70000)
+        for p in dec.parameters():
+            p.requires_grad_(False)
+        coord, label, ts = surface_pool(pts, 200000, seed=5, device=dev)
+        ts = torch.randint(0, 4, ts.shape, device=dev)
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        mapper.set_pool(coord, label, ts)
+        if not fused:
+            mapper.get_batch = lambda global_coord=False, m=mapper: P.Mapper.get_batch(m, global_coord)
+        torch.manual_seed(77)
+        mapper.mapping(3)
+        outs.append((nm.geo_features.clone(), nm.point_certainties.clone(), nm.point_ts_update.clone(),
+                     float(mapper.last_loss)))
+    (f0, c0, t0, l0), (f1, c1, t1, l1) = outs
+    assert torch.equal(t0, t1)
+    assert l0 == pytest.approx(l1, rel=1e-6)
+    off = ~torch.isclose(f0, f1, rtol=1e-5, atol=1e-6)
+    assert float(off.float().mean()) <= 1e-3
+    np.testing.assert_allclose(_np(c0), _np(c1), rtol=1e-5, atol=1e-5)

@@ -47,7 +47,7 @@ def main():
         b = mapper._buf.get(rows, 8, wf, coord.device)
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=10, nn_k=8, weighted_first=int(wf),
                                eps=float(np.float32(0.06)), sigma=float(np.float32(0.055)), weight_e=0.5,
-                               grad_scale=1.0, reserved=0)
+                               grad_scale=1.0, flags=0)
         hv, pv = nm._views("local", True)
         mv = mlp_view(dec)
         res = {}
