@@ -335,6 +335,9 @@ typedef struct PinTrainState {
     int64_t* ts_update;          /* [L] amax with the main rows' ts (neural_points.py:644), may be NULL */
     const int32_t* order;        /* [rows] processing order (pin_query_order over pin_train_rows), may be
                                     NULL; ids/weights/x are stored per processing slot, sdf per row */
+    const float* sorted_rows;    /* [rows,4] the rows in processing order as {x, y, z, bits(row)}
+                                    (pin_query_sort over the rows), may be NULL; takes precedence over
+                                    order and saves the order -> coordinate dependent load */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */

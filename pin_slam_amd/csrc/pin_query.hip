@@ -607,12 +607,16 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     unsigned* done = (unsigned*)(ws + 4 * kMaxTiles);
     static_assert(4 * kMaxTiles + 64 <= PIN_ORDER_STATE_BYTES, "order workspace state too small");
     int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
+    // the placement does not depend on the ranking's blocks: it runs 2 queries per thread (more
+    // blocks in flight for its scattered 16-B stores)
+    constexpr int kPlacePer = 2;
+    const int nplace = (int)((n + kPlacePer * kPartThreads - 1) / (kPlacePer * kPartThreads));
     auto launch = [&](auto per_tag) {
         constexpr int PER = decltype(per_tag)::value;
         const int nblk = (int)((n + PER * kPartThreads - 1) / (PER * kPartThreads));
         hipLaunchKernelGGL(k_tile_rank<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot, tk);
-        hipLaunchKernelGGL(k_tile_place<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot, done, tk,
-                           q4, order);
+        hipLaunchKernelGGL(k_tile_place<kPlacePer>, dim3(nplace), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot, done,
+                           tk, q4, order);
     };
     if (n <= (1 << 19)) launch(std::integral_constant<int, 4>());
     else launch(std::integral_constant<int, 16>());

@@ -56,9 +56,16 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
                                                    float (&cw)[kK], int64_t& qts_out) {
     // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
-    const int64_t r = st.order ? st.order[t] : t;
+    int64_t r;
     float qx, qy, qz;
-    row_coord(coord, c, r, qx, qy, qz);
+    if (st.sorted_rows) {
+        const float4 v = ((const float4*)st.sorted_rows)[t];
+        qx = v.x; qy = v.y; qz = v.z;
+        r = __float_as_int(v.w);
+    } else {
+        r = st.order ? st.order[t] : t;
+        row_coord(coord, c, r, qx, qy, qz);
+    }
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
@@ -352,7 +359,9 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
-    const int64_t row = live && st.order ? st.order[r] : r;          // the row it holds (sdf, label)
+    // the row it holds (sdf, label)
+    const int64_t row = !live ? r : st.sorted_rows ? (int64_t)__float_as_int(((const float4*)st.sorted_rows)[r].w)
+                                  : st.order ? st.order[r] : r;
     const int nn_k = c.nn_k;
     const int wave = threadIdx.x >> 6;
     double loss = 0.0;

@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .data_sampler import DataSampler
-from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_order, query_sdf
+from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
 
 
 def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -53,6 +53,7 @@ class _TrainBuffers:
             self.x = torch.empty((rows, D) if wf else (rows, nn_k, 3), dtype=torch.float32, device=device)
             self.sdf = torch.empty((rows,), dtype=torch.float32, device=device)
             self.rows = torch.empty((rows, 3), dtype=torch.float32, device=device)
+            self.rows4 = torch.empty((rows, 4), dtype=torch.float32, device=device)
             self.label = torch.empty((rows,), dtype=torch.float32, device=device)
             self.ts = torch.empty((rows,), dtype=torch.int64, device=device)
             nblk = (rows + 255) // 256
@@ -416,15 +417,15 @@ class Mapper:
                       ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), s)
         cfg.flags = _lib.PIN_TRAIN_ROWS
         q = rows_xyz
-        order = None
+        sorted_rows = None
         if grid and _TILE_QUERIES and rows >= _TILE_MIN:
-            # process the rows tile by tile (pin_query_order over the batch + stencil coordinates)
-            order = query_order(gv, rows_xyz)
-        self._order = order
+            # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates)
+            sorted_rows = query_sort(gv, rows_xyz, out=b.rows4)
+        self._order = sorted_rows
         st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                 ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
-                                order=order.data_ptr() if order is not None else None)
+                                order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None)
         mv = mlp_view(self.geo_mlp)
         if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
             raise RuntimeError("local_geo_features must be a contiguous float32 tensor")

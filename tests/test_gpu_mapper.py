@@ -127,7 +127,7 @@ def test_mapping_call_fixture(golden, dev, backend, case, monkeypatch):
 
 @pytest.mark.parametrize("wf", [True, False])
 def test_train_step_tile_order_invisible(dev, wf, monkeypatch):
-    """Large batches are processed in tile order (pin_train_rows + pin_query_order): per-row sdf
+    """Large batches are processed in tile order (pin_train_rows + pin_query_sort): per-row sdf
     and ts are bitwise those of input order, gradients / certainties / loss agree to float-atomic
     reordering."""
     import pin_slam_amd.mapper as M
