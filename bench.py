@@ -90,6 +90,9 @@ def parse():
     ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
     ap.add_argument("--no-nwf-leg", action="store_true", help="skip the per-neighbour-decoding leg")
     ap.add_argument("--mapper-steps", type=int, default=10)
+    ap.add_argument("--mapper-shard", default="space", choices=["space", "dense"],
+                    help="N > 1 mapper data parallelism: owner-partitioned slabs with halo exchange (space) or "
+                         "the dense all-reduce of the feature gradient")
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per launch (from profiles/), reported as roofline.traffic")
@@ -454,18 +457,33 @@ def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
                       f"({t_fb:.2f} s, scaled x{n / sample:.0f}) + dense Adam over the map ({t_adam:.2f} s)"}
 
 
+def _shard_info(mapper):
+    """Owned / halo rows of this rank's slab and the halo exchange bytes per iteration."""
+    p = getattr(mapper, "_partition", None)
+    if p is None:
+        return None
+    halo = int(p.halo.numel())
+    sent = sum(int(r.numel()) for r in p.send_rows.values())
+    return {"mode": "space (owner-partitioned slabs, halo exchange)", "owned_rows": int(p.owned.numel()),
+            "halo_rows": halo, "exchange_bytes_per_iter": 2 * 32 * (halo + sent)}
+
+
 def mapper_leg(args, dev, world, rank):
     """configs[3]: Mapper.mapping on a 4M-point map, 1M sampled queries per iteration per GPU
     (+ 6 x 100K numerical-gradient stencil rows), BCE + 0.5 eikonal, Adam on the features
-    (decoder frozen, the steady state after freeze_after_frame).  W > 1: per-rank batches,
-    feature gradients SUM all-reduced over RCCL every iteration (weak scaling)."""
+    (decoder frozen, the steady state after freeze_after_frame).  W > 1 (weak scaling, 1M queries
+    per rank): --mapper-shard space (default) -- every rank owns a slab of the map, samples its
+    batches there and exchanges only halo gradient / feature rows with the neighbouring slabs
+    (pin_slam_amd.sharding); dense -- every rank samples the whole map and the [L+1,8] feature
+    gradient is SUM all-reduced over RCCL every iteration."""
     wf = not args.nwf
     nm, dec, pts = surface_map(MAPPER_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf,
                                query_backend=args.backend, bs=MAPPER_BS)
     for p in dec.parameters():
         p.requires_grad_(False)
     coord, label, ts = surface_pool(pts, MAPPER_POOL, seed=11 + rank, device=dev)
-    mapper = P.Mapper(nm.config, None, nm, dec, group=dist.group.WORLD if world > 1 else None)
+    shard = args.mapper_shard if world > 1 else "dense"
+    mapper = P.Mapper(nm.config, None, nm, dec, group=dist.group.WORLD if world > 1 else None, shard=shard)
     L = int(nm.local_neural_points.shape[0])
     mapper.set_pool(coord, label, ts)
     torch.manual_seed(1234 + rank)
@@ -493,7 +511,9 @@ def mapper_leg(args, dev, world, rank):
                                   "stencil (configs[3])", "map_points": int(pts.shape[0]),
                       "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",
                       "grad_allreduce": (f"{dist.get_backend()} all_reduce SUM of the [L+1,8] f32 gradient "
-                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter)") if world > 1 else None,
+                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter)") if world > 1 and shard == "dense"
+                      else None,
+                      "shard": (_shard_info(mapper) if world > 1 and shard == "space" else None),
                       "candidate_backend": backend, "timed": "mapping(K): K iterations + Adam state init + "
                                                              "assign_local_to_global"},
            "roofline": {"bound": "hbm", "achieved": bpi / (ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,

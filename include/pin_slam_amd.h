@@ -399,6 +399,12 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
                   void* stream);
 
+/* pin_adam_rows -- the same Adam update on the listed rows only of [rows, 8] contiguous arrays
+ * (param, grad, exp_avg, exp_avg_sq; grad_stride must be 8); those rows' gradients are zeroed
+ * when a->zero_grad.  The owned rows of a spatially sharded mapping step (mapper.py shard="space"). */
+int pin_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* rows, int64_t nrows,
+                  const PinAdamStep* a, void* stream);
+
 /* ======================================================================================
  * Map maintenance: insert, local-map selection, prune, pose
  * adjustment and re-hash of NeuralPoints, model/neural_points.py:205-428, with the voxel

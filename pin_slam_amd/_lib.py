@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("PIN_LIB") or os.path.join(_HERE, "libpin_slam_amd.so"
 
 PIN_OK = 0
 PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
+PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 
 FEATURE_DIM = 8
@@ -138,6 +139,7 @@ _SIGS = {
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
+    "pin_adam_rows": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_map_workspace_bytes": [i64],
     "pin_voxel_down_sample": [c_void_p, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_map_insert": [c_void_p, c_void_p, i64, f32, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, i64, f32, f32,

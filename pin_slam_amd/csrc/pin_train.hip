@@ -516,9 +516,39 @@ k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_
     }
 }
 
+// Adam on listed rows of a [rows, 8] parameter (the owned rows of a spatially sharded mapper):
+// one thread per (row, half row), the same arithmetic as k_adam; the rows' gradients are zeroed
+__global__ void __launch_bounds__(kBlock)
+k_adam_rows(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_,
+            const int64_t* __restrict__ rows, int64_t nrows, PinAdamStep a) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 2 * nrows) return;
+    const int64_t i0 = rows[t >> 1] * kF + 4 * (t & 1);
+    float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + i0), m = *(float4*)(m_ + i0), v = *(float4*)(v_ + i0);
+    adam_one(p.x, g.x, m.x, v.x, a);
+    adam_one(p.y, g.y, m.y, v.y, a);
+    adam_one(p.z, g.z, m.z, v.z, a);
+    adam_one(p.w, g.w, m.w, v.w, a);
+    *(float4*)(prm + i0) = p;
+    *(float4*)(m_ + i0) = m;
+    *(float4*)(v_ + i0) = v;
+    if (a.zero_grad) *(float4*)(grad + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 }  // namespace
 
 extern "C" {
+
+int pin_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* rows, int64_t nrows,
+                  const PinAdamStep* a, void* stream) {
+    if (!a || nrows < 0 || (nrows > 0 && (!param || !grad || !exp_avg || !exp_avg_sq || !rows))) return PIN_ERR_ARG;
+    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
+    if (nrows == 0) return PIN_OK;
+    if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_adam_rows, grid_for(2 * nrows), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg,
+                       exp_avg_sq, rows, nrows, *a);
+    return launch_status();
+}
 
 int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, void* stream) {
     if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;

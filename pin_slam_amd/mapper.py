@@ -67,7 +67,8 @@ class _TrainBuffers:
 class Mapper:
     """utils/mapper.py:Mapper -- constructor signature, pools and training entry points."""
 
-    def __init__(self, config, dataset, neural_points, geo_mlp, sem_mlp=None, color_mlp=None, group=None):
+    def __init__(self, config, dataset, neural_points, geo_mlp, sem_mlp=None, color_mlp=None, group=None,
+                 shard="dense"):
         self.config = config
         self.silence = config.silence
         self.dataset = dataset
@@ -105,6 +106,12 @@ class Mapper:
         self.time_pool = torch.empty((0,), device=dev, dtype=torch.long)
         self.pool_sample_count = 0
         self.group = group
+        # data-parallel mode with a group of W > 1: "dense" (every rank samples the whole pool,
+        # SUM all-reduce of the [L+1,8] gradient) or "space" (owner-partitioned slabs, halo
+        # exchange only: pin_slam_amd.sharding)
+        if shard not in ("dense", "space"):
+            raise ValueError("shard must be 'dense' or 'space'")
+        self.shard = shard
         self.last_loss = None        # device f64 tensor: loss of the last iteration
         self._buf = _TrainBuffers()
         self._adam_t = 0
@@ -259,21 +266,26 @@ class Mapper:
         self.weight_pool = torch.ones_like(sdf_label) if weight is None else weight
         self.pool_sample_count = int(sdf_label.shape[0])
 
-    def _batch_index(self):
-        """The pool rows of one batch: get_batch's sampling (utils/mapper.py:323-350), same draws."""
+    def _batch_index(self, rows=None, new_idx=None):
+        """The pool rows of one batch: get_batch's sampling (utils/mapper.py:323-350), same draws.
+        rows / new_idx: the pool rows (and new samples) to draw from instead of the whole pool
+        (a spatially sharded rank's slab)."""
         stop = getattr(self.dataset, "stop_status", False) if self.dataset is not None else False
         bs = int(self.config.bs)
         bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
-        if bs_new_sample > 0 and self.new_idx is not None and not self.lose_track and not stop:
-            new_idx_count = self.new_idx.shape[0]
+        count = self.pool_sample_count if rows is None else rows.shape[0]
+        pick = (lambda i: i) if rows is None else (lambda i: rows[i])   # noqa: E731
+        new_idx = self.new_idx if rows is None else new_idx
+        if bs_new_sample > 0 and new_idx is not None and not self.lose_track and not stop:
+            new_idx_count = new_idx.shape[0]
             if new_idx_count > 0:
                 bs_new = min(new_idx_count, bs_new_sample)
                 bs_history = bs - bs_new
-                index_history = torch.randint(0, self.pool_sample_count, (bs_history,), device=self.device)
+                index_history = pick(torch.randint(0, count, (bs_history,), device=self.device))
                 index_new_batch = torch.randint(0, new_idx_count, (bs_new,), device=self.device)
-                return torch.cat((index_history, self.new_idx[index_new_batch]), dim=0)
-            return torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
-        return torch.randint(0, self.pool_sample_count, (bs,), device=self.device)
+                return torch.cat((index_history, new_idx[index_new_batch]), dim=0)
+            return pick(torch.randint(0, count, (bs,), device=self.device))
+        return pick(torch.randint(0, count, (bs,), device=self.device))
 
     def get_batch(self, global_coord=False):
         """utils/mapper.py:323-361."""
@@ -344,23 +356,55 @@ class Mapper:
         # get_batch's gathers fused into the row build (pin_train_gather) when the pools allow it;
         # a get_batch replaced on the instance (tests, callers) is honoured
         fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
+        part = slab_rows = slab_new = None
+        if world > 1 and getattr(self, "shard", "dense") == "space" and self._slab_exact():
+            if not fused:
+                raise NotImplementedError("shard='space' samples device pools through the fused batch path")
+            from .sharding import SlabPartition, query_reach
+            group = getattr(self, "group", None)
+            part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group)
+            mask = part.sample_mask(self.global_coord_pool[: self.pool_sample_count])
+            slab_rows = torch.nonzero(mask).flatten()
+            if self.new_idx is not None:
+                slab_new = self.new_idx[mask[self.new_idx]]
+            self._partition = part
         for _ in range(iter_count):
             if fused:
+                index = self._batch_index() if part is None else self._batch_index(slab_rows, slab_new)
                 self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad, world,
-                                index=self._batch_index())
+                                index=index, reduce=part is None)
             else:
                 coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
                 if self.ba_done_flag:
                     coord = transform_batch_torch(coord, self.used_poses[ts])
                 self.train_step(coord, sdf_label, ts, f_grad, m_grad, world)
-            self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
+            if part is not None:
+                part.exchange_gradients(f_grad)                   # halo rows -> owners
+                if m_grad is not None:
+                    dist.all_reduce(m_grad, op=dist.ReduceOp.SUM, group=getattr(self, "group", None))
+            self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, partition=part)
+            if part is not None:
+                part.exchange_features(fdata)                     # owners -> halo copies
             self.total_iter += 1
-        if world > 1:
+        if part is not None:
+            part.reconcile_side_effects(cert_before, nm.local_point_certainties, nm.local_point_ts_update)
+            part.gather_owned(fdata, nm.local_point_certainties, nm.local_point_ts_update)
+            nm.mark_modified(feats, nm.local_point_certainties, nm.local_point_ts_update)
+        elif world > 1:
             cert = nm.local_point_certainties
             cert_delta = cert - cert_before
             sync_side_effects(cert_delta, nm.local_point_ts_update, getattr(self, "group", None))
             cert.copy_(cert_before + cert_delta)
         nm.assign_local_to_global()
+
+    def _slab_exact(self):
+        """Slab sharding is exact when every candidate a query can reach is a local point at its own
+        position: the reference's global2local fill quirk (a non-local point passing the travel
+        filter reads local row 1, neural_points.py:290-300) would route gradients to a far-away
+        row.  Such records carry PIN_RECORD_UNFAITHFUL; with any of them the dense path is used."""
+        rec = self.neural_points.records("local")
+        flags = rec[:, 3].contiguous().view(torch.int32) & _lib.PIN_RECORD_UNFAITHFUL
+        return not bool((flags != 0).any())
 
     def _pools_fusable(self):
         c, l, t = self.global_coord_pool, self.sdf_label_pool, self.time_pool
@@ -368,7 +412,7 @@ class Mapper:
                 and l is not None and l.dtype == torch.float32 and l.is_contiguous()
                 and (t is None or (t.dtype == torch.int64 and t.is_contiguous())))
 
-    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None):
+    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None, reduce=True):
         """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
         SUM all-reduced over the group when world > 1.  Returns the device loss tensor.
         index ([N] int64): coord / sdf_label / ts are then the sample pools and the batch is their
@@ -439,20 +483,26 @@ class Mapper:
                   _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
         # the forward's side effects went through raw pointers: invalidate caches built on them
         nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if ts64 is not None else None)
-        if world > 1:
+        if world > 1 and reduce:
             allreduce_gradients([grad_features, mlp_grad], getattr(self, "group", None))
         self.last_loss = b.loss
         self.last_sdf = b.sdf[:n]
         return b.loss
 
-    def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None):
-        """torch.optim.Adam(betas=(0.9, 0.99), eps=adam_eps) step (utils/tools.py:111-112)."""
+    def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None, partition=None):
+        """torch.optim.Adam(betas=(0.9, 0.99), eps=adam_eps) step (utils/tools.py:111-112); with a
+        slab partition only the owned feature rows (their halo copies are refreshed after)."""
         c = self.config
         self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
-        _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
-                  ctypes.byref(st), s)
+        if partition is None:
+            _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
+                      fdata.numel(), ctypes.byref(st), s)
+        else:
+            _lib.call("pin_adam_rows", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
+                      _lib.ptr(partition.owned), partition.owned.numel(), ctypes.byref(st), s)
+            partition.zero_halo(f_grad)
         feats = self.neural_points.local_geo_features
         self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
         if m_grad is not None:

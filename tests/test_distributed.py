@@ -97,3 +97,113 @@ def test_data_parallel_mapping_equals_single_process(case):
     np.testing.assert_array_equal(ts, ts1)
     assert loss == pytest.approx(loss1, rel=1e-9)
     assert tmax == 2.0
+
+
+# ------------------------------------------------------------------ spatially sharded mapping
+def _shard_setup():
+    """A small all-local oracle map (surface grid), the mapper fixture's decoder and two seeded
+    batches: surface points + N(0, 0.25^2) along z, label = -offset."""
+    z = np.load(os.path.join(GOLDEN, "mapper_wf.npz"))
+    mlp = O.mlp_from_fixture(z)
+    res = 0.3
+    nx, ny = 120, 40
+    xs, ys = np.meshgrid((np.arange(nx) + 0.5) * res, (np.arange(ny) + 0.5) * res, indexing="ij")
+    pts = np.stack([xs.ravel(), ys.ravel(), 0.5 * np.sin(xs.ravel() / 7) * np.cos(ys.ravel() / 5) + 0.15], -1)
+    st = O.empty_map(res, 1 << 20, np.zeros(1, np.float32), 1e9)
+    O.map_update(st, pts.astype(np.float32), 0)
+    O.reset_local_map(st, np.array([18.0, 6.0, 0.0]), 0, 1e6)
+    rng = np.random.default_rng(3)
+    st.local_features[:-1] = rng.normal(0, 0.05, st.local_features[:-1].shape).astype(np.float32)
+    batches = []
+    for it in range(2):
+        idx = rng.integers(0, st.points.shape[0], 1600)
+        off = rng.normal(0, 0.25, 1600).astype(np.float32)
+        coord = st.points[idx].copy()
+        coord[:, 2] += off
+        batches.append((coord, -off, np.zeros(1600, np.int64)))
+    cfg = dict(nn_k=8, neighbor_dx=O.neighbor_offsets(2, 0.2), maxd2=float(3 * (3 * res) ** 2),
+               weighted_first=True, sigma=float(z["sigma"]), weight_e=0.5, decimation=10, eps=0.06, lr=0.01)
+    return st, mlp, batches, cfg
+
+
+def _rank_grad(st, mlp, batch, mask, cfg, n_total):
+    """Oracle forward/backward of one rank's rows (st mutated: its side effects), scaled so that the
+    ranks' gradients add up to the gradient of the sum of their means weighted by rows."""
+    coord, label, ts = batch
+    out = O.mapper_forward_backward(st, mlp, coord[mask], label[mask], ts[mask], cfg["nn_k"], cfg["neighbor_dx"],
+                                    cfg["maxd2"], cfg["weighted_first"], cfg["sigma"], cfg["weight_e"],
+                                    cfg["decimation"], cfg["eps"])
+    return out["feat_grad"].astype(np.float32) * np.float32(mask.sum() / n_total)
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pin_slam_amd.sharding import SlabPartition
+        st, mlp, batches, cfg = _shard_setup()
+        reach = float(np.sqrt(cfg["maxd2"])) * 1.001 + cfg["eps"] + 1e-3
+        part = SlabPartition(torch.from_numpy(st.local_points), reach)
+        feats = torch.from_numpy(st.local_features)        # shares memory with the oracle state
+        m, v = torch.zeros_like(feats), torch.zeros_like(feats)
+        cert_before = torch.from_numpy(st.local_certainties.copy())
+        owned = part.owned.numpy()
+        masks = []
+        for it, batch in enumerate(batches):
+            mask = part.sample_mask(torch.from_numpy(batch[0])).numpy()
+            masks.append(mask)
+            g = torch.from_numpy(_rank_grad(st, mlp, batch, mask, cfg, batch[0].shape[0]))
+            part.exchange_gradients(g)
+            p_o, g_o, m_o, v_o = (t.numpy()[owned].copy() for t in (feats, g, m, v))
+            O.adam_step(p_o, g_o, m_o, v_o, it + 1, cfg["lr"])
+            for t, val in ((feats, p_o), (m, m_o), (v, v_o)):
+                t.numpy()[owned] = val
+            part.exchange_features(feats)
+        cert = torch.from_numpy(st.local_certainties)
+        ts = torch.from_numpy(st.local_ts_update)
+        part.reconcile_side_effects(cert_before, cert, ts)
+        part.gather_owned(feats, cert, ts)
+        q.put((rank, feats.numpy().copy(), cert.numpy().copy(), ts.numpy().copy(), masks,
+               int(part.owned.numel()), int(part.halo.numel())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_slab_sharded_mapping_equals_dense_data_parallel():
+    """shard='space' (pin_slam_amd.sharding): halo gradients to owners, Adam on owned rows, halo
+    features refreshed, side effects reconciled, owned rows all-gathered -- equals the dense
+    data-parallel step on the same per-rank batches (sum of the ranks' gradients, Adam on every
+    row, summed certainty deltas, max ts) on every replica, over two iterations."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    st, mlp, batches, cfg = _shard_setup()
+    L = st.local_points.shape[0]
+    assert sum(r[5] for r in res) == L and all(0 < r[6] < L // 4 for r in res)   # owners partition; small halos
+    m, v = np.zeros_like(st.local_features), np.zeros_like(st.local_features)
+    cert0 = st.local_certainties.copy()
+    cert_delta = np.zeros_like(cert0)
+    ts = st.local_ts_update.copy()
+    for it, batch in enumerate(batches):
+        g = np.zeros_like(st.local_features)
+        for r in range(world):
+            sr = st.copy()
+            sr.local_certainties[:] = 0
+            g += _rank_grad(sr, mlp, batch, res[r][4][it], cfg, batch[0].shape[0])
+            cert_delta += sr.local_certainties
+            ts = np.maximum(ts, sr.local_ts_update)
+        O.adam_step(st.local_features, g, m, v, it + 1, cfg["lr"])
+    for r in range(world):
+        np.testing.assert_allclose(res[r][1], st.local_features, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(res[r][2], cert0 + cert_delta, rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(res[r][3], ts)

@@ -242,3 +242,32 @@ def test_fused_gather_path_matches_get_batch(dev):
     off = ~torch.isclose(f0, f1, rtol=1e-5, atol=1e-6)
     assert float(off.float().mean()) <= 1e-3
     np.testing.assert_allclose(_np(c0), _np(c1), rtol=1e-5, atol=1e-5)
+
+
+def test_adam_rows_matches_dense_adam_on_those_rows(dev):
+    """pin_adam_rows (the owned rows of a slab-sharded mapper) equals pin_adam_step on those rows
+    and leaves every other row, its moments and its gradient untouched."""
+    import ctypes
+    from pin_slam_amd.mapper import adam_scalars
+    g = torch.Generator(device="cpu").manual_seed(1)
+    L = 5001
+    p0 = torch.randn((L, 8), generator=g).to(dev)
+    rows = torch.randperm(L, generator=g)[:1700].sort()[0].to(dev)
+    pa, pb = p0.clone(), p0.clone()
+    ma, va, mb, vb = (torch.zeros_like(p0) for _ in range(4))
+    for t in range(1, 4):
+        grad = torch.randn((L, 8), generator=g).to(dev)
+        ga, gb = grad.clone(), grad.clone()
+        st = adam_scalars(0.01, t, 1e-15)
+        _lib.call("pin_adam_rows", _lib.ptr(pa), _lib.ptr(ga), _lib.ptr(ma), _lib.ptr(va), _lib.ptr(rows), rows.numel(),
+                  ctypes.byref(st), _lib.stream())
+        _lib.call("pin_adam_step", _lib.ptr(pb), _lib.ptr(gb), _lib.ptr(mb), _lib.ptr(vb), pb.numel(),
+                  ctypes.byref(st), _lib.stream())
+        assert torch.equal(pa[rows], pb[rows]) and torch.equal(ma[rows], mb[rows]) and torch.equal(va[rows], vb[rows])
+        other = torch.ones(L, dtype=torch.bool, device=dev)
+        other[rows] = False
+        assert torch.equal(pa[other], p0[other]) and torch.equal(ga[other], grad[other])
+        assert float(ga[rows].abs().max()) == 0.0
+        pb[other] = p0[other]
+        mb[other] = 0
+        vb[other] = 0

@@ -5,5 +5,5 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 --mapper-steps 3 --mapper-warmup 1 \
-    --dist-backend gloo > gpurun_out/multi.json 2> gpurun_out/multi.err
+    --dist-backend gloo ${BENCH_ARGS:-} > gpurun_out/multi.json 2> gpurun_out/multi.err
 rc=$?; echo "rc=$rc"; cat gpurun_out/multi.json; tail -5 gpurun_out/multi.err; exit $rc
