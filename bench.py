@@ -129,7 +129,7 @@ def time_kernel(nm, dec, q, wf, backend, steps):
     from pin_slam_amd.query import mlp_view, query_sort
     n = q.shape[0]
     hv, pv = nm._views("global", False)
-    mv = mlp_view(dec)
+    mv = mlp_view(dec, packed=True)
     sdf = torch.empty(n, device=q.device)
     grad = torch.empty((n, 3), device=q.device)
     nn = torch.empty(n, dtype=torch.int32, device=q.device)

@@ -95,7 +95,25 @@ typedef struct PinMlp {
     const float* b2;             /* [1] */
     float sdf_scale;             /* logistic_gaussian_ratio * sigma_sigmoid_m (decoder.py:51-54) */
     int32_t reserved;
+    const void* packed;          /* PIN_MLP_PACK_BYTES written by pin_mlp_pack from THESE weights, or NULL.
+                                    Set: the SDF kernels (pin_query_sdf*) decode on the f16 matrix cores
+                                    when the gradient is requested (each f32 operand split into two f16
+                                    terms, f32 accumulation); NULL or SDF only: f32 VALU */
 } PinMlp;
+
+/*
+ * pin_mlp_pack -- the decoder as MFMA operand tiles (pin_query_sdf_grid*, decoder.py:66-88):
+ *   GEMM1  P^T = [W1 | b1] [x ; 1]       64 hidden x 64 queries of a wave, K = 11 + bias
+ *   GEMM2  g^T = (W1 o w2)^T 1[P > 0]    rows 0..10: dsdf/dx_i / s, row 11: sum_c 1[P_c>0] w2_c b1_c,
+ *                                        so that sdf = s (x . g + row 11 + b2)  (= s (w2 . relu(P) + b2))
+ * Each f32 operand v is stored as v_hi + v_lo (f16, round to nearest) after a power-of-two
+ * scale per operand row (rows of W1|b1 and of W1 o w2 to [2^13, 2^14); queries scaled per
+ * lane in the kernel): products are exact in the f32 accumulators and the dropped lo*lo term
+ * is ~2^-22 relative, the f32 rounding level of the reference's own sums.  Inputs |x| < 2^29.
+ * Re-run after every decoder update (Mapper steps change W1/b1/W2/b2).
+ */
+#define PIN_MLP_PACK_BYTES 8320
+int pin_mlp_pack(const PinMlp* mlp, void* packed, void* stream);
 
 /*
  * pin_build_records -- per-point candidate records for one query mode.

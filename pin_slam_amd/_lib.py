@@ -67,7 +67,10 @@ REG_WORKSPACE_DOUBLES = 256 * REG_NACC
 
 class PinMlp(ctypes.Structure):
     _fields_ = [("W1", c_void_p), ("b1", c_void_p), ("W2", c_void_p), ("b2", c_void_p), ("sdf_scale", f32),
-                ("reserved", i32)]
+                ("reserved", i32), ("packed", c_void_p)]
+
+
+MLP_PACK_BYTES = 8320
 
 
 class PinTrainCfg(ctypes.Structure):
@@ -117,6 +120,7 @@ _SIGS = {
                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_mlp_pack": [_P(PinMlp), c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_sort": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_tiled": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,

@@ -540,7 +540,8 @@ constexpr int kWSize = kWB2 + 4;
 struct MlpW {
     const float* w;   // LDS
     float sdf_scale;
-    float* xs;        // per-wave LDS scratch (64 x 12 floats) of the MFMA decoder, or nullptr
+    float* xs;        // per-wave LDS scratch of the MFMA decoders, or nullptr
+    const unsigned char* pk = nullptr;   // LDS copy of the pin_mlp_pack image (mlp_sdf_mfma16)
 };
 
 #ifndef PIN_MLP_ROWS
@@ -757,6 +758,144 @@ __device__ __forceinline__ float mlp_sdf_wave(const MlpW& m, const float (&x)[kD
         wave_lds_sync();   // the next call's X staging reuses xs
     }
     return (out + m.w[kWB2]) * m.sdf_scale;
+}
+
+// ------------------------------------------------------------------ f16 matrix-core decoder
+// The wave's 64 decodes as two GEMMs on v_mfma_f32_16x16x32_f16 with every f32 operand split
+// into two f16 terms (pin_mlp_pack, include/pin_slam_amd.h):
+//   GEMM1  P^T[c][q]  = sum_k A1[c][k] B1[k][q]        K-slots: Wh.xh | Wl.xh | b1h.E b1l.E (16x16x32)
+//                                                      + Wh.xl (a second 16x16x32, K-slots 11..31 zero;
+//                                                      a 16x16x16 chained onto the 16x16x32 accumulator
+//                                                      measured wrong sums in tools/mf_unit.hip)
+//   GEMM2  g^T[i][q]  = sum_c A2[i][c] 1[P[c][q] > 0]  A2 = (W1 o w2)^T split hi/lo, row 11 = w2 o b1
+//   sdf = s (x . g + g_11 + b2),  dsdf/dx_i = s g_i
+// B1 column q is query q's inputs scaled by E = 2^e_q (max|x| to [2^13, 2^14)), so D1 = 2^(e_c+e_q)
+// P and only its sign is used; the GEMM2 B operand is the 0/1 mask, exact in f16, taken from
+// the GEMM1 accumulators as they stand (K-slot s of lane group g <-> hidden 4g+s / 16+4g+s-4).
+// Per lane: ~55 VALU for the split, 64 x 2.5 for the masks, ~40 to read g back -- against
+// ~830 packed-FMA instructions for the VALU decoder -- and 48 MFMAs per wave.
+constexpr int kPkA1 = 0;                    // [4 mt][64 lanes] f16x8   GEMM1 K-slots 8g..8g+7
+constexpr int kPkA2 = kPkA1 + 4 * 64 * 16;  // [2 ch][2 term][64 lanes] f16x8
+constexpr int kPkScale = kPkA2 + 4 * 64 * 16;   // [16] f32: 2^-f_i of GEMM2 row i
+constexpr int kPkB2 = kPkScale + 16 * 4;        // f32 b2
+constexpr int kPkBytes = 8320;
+static_assert(kPkB2 + 4 <= kPkBytes && kPkBytes == PIN_MLP_PACK_BYTES && kPkBytes % 16 == 0, "pack layout");
+constexpr int kXsStride = 20;               // floats per query row of the decoder scratch (80 B: conflict-free)
+constexpr int kXsWave = 64 * kXsStride;     // floats of scratch per wave
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pack_f16x2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, (f16x2){(_Float16)a, (_Float16)b});
+}
+
+// 1.0h in each half whose accumulator is > 0 (relu' with torch's convention at 0 and NaN)
+__device__ __forceinline__ uint32_t mask_f16x2(float a, float b) {
+    return (a > 0.f ? 0x3C00u : 0u) | (b > 0.f ? 0x3C000000u : 0u);
+}
+
+// All 64 lanes of the wave must call this together (lanes without a query pass zeros).
+// Returns sdf; gx = the NOUT input gradients from input OFF on (GRAD).
+template <bool GRAD, int OFF, int NOUT>
+__device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+    static_assert(OFF + NOUT <= kD, "decoder input range");
+    float* xs = m.xs;
+    const unsigned char* pk = m.pk;
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15, grp = lane >> 4;
+    // ---- this lane's query as B1 column: scale, split, one 80-B LDS row
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < kD; ++i) mx = fmaxf(mx, fabsf(x[i]));
+    const int eb = (__float_as_int(mx) >> 23) & 0xff;
+    const int e = min(max(140 - eb, -14), 15);            // 2^e a normal f16
+    const float sc = __int_as_float((e + 127) << 23);
+    float xh[kD], xl[kD];
+#pragma unroll
+    for (int i = 0; i < kD; ++i) {
+        const float v = x[i] * sc;
+        xh[i] = __int_as_float(__float_as_int(v) & (int)0xFFFFE000u);   // 11 significant bits: exact f16
+        xl[i] = v - xh[i];
+    }
+    {
+        uint4* row = (uint4*)(xs + lane * kXsStride);
+        row[0] = make_uint4(pack_f16x2(xh[0], xh[1]), pack_f16x2(xh[2], xh[3]), pack_f16x2(xh[4], xh[5]),
+                            pack_f16x2(xh[6], xh[7]));
+        row[1] = make_uint4(pack_f16x2(xh[8], xh[9]), pack_f16x2(xh[10], xh[0]), pack_f16x2(xh[1], xh[2]),
+                            pack_f16x2(xh[3], xh[4]));
+        row[2] = make_uint4(pack_f16x2(xh[5], xh[6]), pack_f16x2(xh[7], xh[8]), pack_f16x2(xh[9], xh[10]),
+                            pack_f16x2(sc, sc));
+        row[3] = make_uint4(pack_f16x2(xl[0], xl[1]), pack_f16x2(xl[2], xl[3]), pack_f16x2(xl[4], xl[5]),
+                            pack_f16x2(xl[6], xl[7]));
+        row[4] = make_uint4(pack_f16x2(xl[8], xl[9]), pack_f16x2(xl[10], 0.f), 0u, 0u);
+    }
+    wave_lds_sync();
+    // B operands of the four query tiles (lane group 3 reads lo-row halves; its A slots are 0)
+    f16x8 bh[4];
+    f16x8 bl[4];   // x-lo rows: groups 2, 3 re-read group 1's slots (their A slots are 0)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const float* r = xs + (16 * nt + col) * kXsStride;
+        bh[nt] = *(const f16x8*)(r + 4 * grp);
+        bl[nt] = *(const f16x8*)(r + 12 + 4 * min(grp, 1));
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        uint32_t mk[4][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int mt = 2 * ch + h;
+            const f16x8 a = ((const f16x8*)(pk + kPkA1))[mt * 64 + lane];
+            // Wh.xl: its K-slots 0..10 are A1's own slots 0..10 (lane groups 0 and 1), the rest 0
+            const uint4 au = __builtin_bit_cast(uint4, a);
+            const f16x8 al = __builtin_bit_cast(
+                f16x8, make_uint4(grp < 2 ? au.x : 0u, grp == 0 ? au.y : (grp == 1 ? (au.y & 0xFFFFu) : 0u),
+                                  grp == 0 ? au.z : 0u, grp == 0 ? au.w : 0u));
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh[nt], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bl[nt], d, 0, 0, 0);
+                mk[nt][2 * h] = mask_f16x2(d[0], d[1]);
+                mk[nt][2 * h + 1] = mask_f16x2(d[2], d[3]);
+            }
+        }
+        const f16x8 a2h = ((const f16x8*)(pk + kPkA2))[(2 * ch) * 64 + lane];
+        const f16x8 a2l = ((const f16x8*)(pk + kPkA2))[(2 * ch + 1) * 64 + lane];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const f16x8 b = __builtin_bit_cast(f16x8, make_uint4(mk[nt][0], mk[nt][1], mk[nt][2], mk[nt][3]));
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h, b, acc[nt], 0, 0, 0);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l, b, acc[nt], 0, 0, 0);
+        }
+    }
+    // ---- g back to the query's lane: lane (col, grp) holds rows 4grp..4grp+3 of query 16nt+col
+    wave_lds_sync();   // every lane has read its B operands
+    if (grp < 3) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
+    }
+    wave_lds_sync();
+    const f32x4* r = (const f32x4*)(xs + lane * kXsStride);
+    const f32x4 g0 = r[0], g1 = r[1], g2 = r[2];
+    const f32x4* us = (const f32x4*)(pk + kPkScale);
+    const f32x4 u0 = us[0], u1 = us[1], u2 = us[2];
+    const float g[12] = {g0[0] * u0[0], g0[1] * u0[1], g0[2] * u0[2], g0[3] * u0[3],
+                         g1[0] * u1[0], g1[1] * u1[1], g1[2] * u1[2], g1[3] * u1[3],
+                         g2[0] * u2[0], g2[1] * u2[1], g2[2] * u2[2], g2[3] * u2[3]};
+    wave_lds_sync();   // the next call's staging reuses xs
+    float out = g[11] + *(const float*)(pk + kPkB2);
+#pragma unroll
+    for (int i = 0; i < kD; ++i) out = fmaf(x[i], g[i], out);
+    if (GRAD) {
+#pragma unroll
+        for (int i = 0; i < NOUT; ++i) gx[i] = g[OFF + i] * m.sdf_scale;
+    }
+    return out * m.sdf_scale;
 }
 
 }  // namespace pin

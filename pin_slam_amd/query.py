@@ -64,9 +64,14 @@ def tensor_key(ts):
     return tuple((id(t), t.data_ptr(), t._version) if t is not None else None for t in ts)
 
 
-def mlp_view(decoder) -> _View:
+# decode on the f16 matrix cores (pin_mlp_pack image in PinMlp.packed; PIN_MLP_PACK=0: f32 VALU decoder)
+_MLP_PACK = os.environ.get("PIN_MLP_PACK", "1") != "0"
+
+
+def mlp_view(decoder, packed=False) -> _View:
     """PinMlp over a hidden_level=1, out_dim=1 geo decoder (model/decoder.py:16-57); cached on the
-    decoder until a parameter is replaced or modified."""
+    decoder until a parameter is replaced or modified.  packed: also carry the pin_mlp_pack
+    operand image (built once per decoder version) for the grid SDF kernels."""
     try:
         ps = (decoder.layers[0].weight, decoder.layers[0].bias, decoder.lout.weight, decoder.lout.bias)
     except (AttributeError, IndexError):
@@ -75,11 +80,18 @@ def mlp_view(decoder) -> _View:
         key = (tensor_key(ps), float(decoder.sdf_scale))
         hit = decoder.__dict__.get("_pin_mlp_view")
         if hit is not None and hit[0] == key:
-            return hit[1]
+            v = hit[1]
+        else:
+            v = _mlp_view(decoder)
+            decoder.__dict__["_pin_mlp_view"] = (key, v)
+    else:
         v = _mlp_view(decoder)
-        decoder.__dict__["_pin_mlp_view"] = (key, v)
-        return v
-    return _mlp_view(decoder)
+    if packed and _MLP_PACK and not v.struct.packed:
+        buf = torch.empty(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=v.keep[0].device)
+        _lib.call("pin_mlp_pack", v.ref(), _lib.ptr(buf), _lib.stream(buf.device))
+        v.struct.packed = buf.data_ptr()
+        v.keep = v.keep + (buf,)
+    return v
 
 
 def _mlp_view(decoder) -> _View:
@@ -199,7 +211,7 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     wf = bool(nm.config.weighted_first if weighted_first is None else weighted_first)
     mode = "local" if query_locally else "global"
     hv, pv = nm._views(mode, query_locally)
-    mv = mlp_view(decoder)
+    mv = mlp_view(decoder, packed=want_grad)
     sdf = torch.empty(n, dtype=torch.float32, device=dev)
     grad = torch.empty((n, 3), dtype=torch.float32, device=dev) if want_grad else None
     nn_count = torch.empty(n, dtype=torch.int32, device=dev)

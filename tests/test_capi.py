@@ -61,6 +61,14 @@ def test_struct_layouts_match_header(tmp_path):
     assert sorted(re.findall(r"^} (Pin\w+);", hdr, re.M)) == sorted(STRUCTS)
 
 
+def test_header_constants_match_bindings():
+    from pin_slam_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "pin_slam_amd.h")).read()
+    val = lambda name: int(re.search(r"#define %s (\d+)" % name, hdr).group(1))  # noqa: E731
+    assert val("PIN_MLP_PACK_BYTES") == _lib.MLP_PACK_BYTES
+    assert val("PIN_ORDER_STATE_BYTES") == __import__("pin_slam_amd.query", fromlist=["x"]).ORDER_STATE_BYTES
+
+
 def test_neighbor_offsets_host(golden):
     from pin_slam_amd.neural_points import neighbor_offsets
     z = golden("neighborhoods")

@@ -249,6 +249,43 @@ def test_random_map_vs_oracle(dev, wf, backend):
 
 
 @pytest.mark.parametrize("wf", [True, False])
+@pytest.mark.parametrize("feature_std,wscale", [(1e-4, 1.0), (0.05, 1.0), (20.0, 1.0), (0.05, 30.0)])
+def test_matrix_core_decoder_matches_f32(dev, wf, feature_std, wscale):
+    """The f16-split MFMA decoder (pin_mlp_pack) against the f32 VALU decoder on the same
+    queries, across input and weight magnitudes (the per-row / per-query power-of-two scaling
+    keeps both f16 terms in range): SDF within 2e-6 relative to the SDF scale of the batch,
+    gradients within the parity tolerance."""
+    from pin_slam_amd import _lib
+    from pin_slam_amd.query import mlp_view
+    nm, dec, pts = H.surface_map(200, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend="grid",
+                                 feature_std=feature_std)
+    with torch.no_grad():
+        dec.layers[0].weight.mul_(wscale)
+    q = H.surface_queries(pts, 30001, device=dev)
+    gv = nm.grid_view("global", True)
+    _, pv = nm._views("global", False)
+    n = q.shape[0]
+    res = []
+    for packed in (False, True):
+        mv = mlp_view(dec, packed=packed)
+        assert bool(mv.struct.packed) == packed
+        sdf = torch.empty(n, device=dev)
+        grad = torch.empty((n, 3), device=dev)
+        nn = torch.empty(n, dtype=torch.int32, device=dev)
+        std = torch.empty(n, device=dev)
+        _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0, _lib.ptr(sdf),
+                  _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), None, _lib.stream())
+        res.append((_np(sdf), _np(grad), _np(nn), _np(std)))
+    (s0, g0, n0, d0), (s1, g1, n1, d1) = res
+    np.testing.assert_array_equal(n1, n0)
+    scale = max(1.0, float(np.abs(s0).max()))
+    np.testing.assert_allclose(s1, s0, rtol=0, atol=2e-6 * scale)
+    assert_grad_close(g1, g0, atol=2e-5 * max(1.0, float(np.abs(g0).max())))
+    if not wf:
+        np.testing.assert_allclose(d1, d0, rtol=0, atol=2e-6 * scale)
+
+
+@pytest.mark.parametrize("wf", [True, False])
 def test_query_order_is_a_permutation_and_invisible(dev, wf):
     """pin_query_order / pin_query_sort group a random batch by spatial tile (a counting sort whose
     workspace state is left zero by every call, so repeated calls stay valid); the SDF kernel's
@@ -280,7 +317,13 @@ def test_query_order_is_a_permutation_and_invisible(dev, wf):
     starts = torch.nonzero(tile[1:] != tile[:-1]).numel() + 1
     assert starts == torch.unique(tile).numel()
     hv, pv = nm._views("global", False)
-    mv = mlp_view(dec)
+    for packed in (False, True):   # f32 VALU decoder and f16 matrix-core decoder
+        _check_order_invisible(gv, pv, mlp_view(dec, packed=packed), q, q4, order, wf)
+
+
+def _check_order_invisible(gv, pv, mv, q, q4, order, wf):
+    from pin_slam_amd import _lib
+    dev = q.device
     outs = []
     for o in (None, order, "sorted"):
         sdf = torch.empty(q.shape[0], device=dev)

@@ -23,7 +23,7 @@ def main():
         n = q.shape[0]
         gv = nm.grid_view("global", True)
         hv, pv = nm._views("global", False)
-        mv = mlp_view(dec)
+        mv = mlp_view(dec, packed=True)
         q4 = query_sort(gv, q)
         sdf = torch.empty(n, device=q.device)
         grad = torch.empty((n, 3), device=q.device)
