@@ -98,7 +98,9 @@ typedef struct PinMlp {
     const void* packed;          /* PIN_MLP_PACK_BYTES written by pin_mlp_pack from THESE weights, or NULL.
                                     Set: the SDF kernels (pin_query_sdf*) decode on the f16 matrix cores
                                     when the gradient is requested (each f32 operand split into two f16
-                                    terms, f32 accumulation); NULL or SDF only: f32 VALU */
+                                    terms, f32 accumulation), as do pin_train_forward under PIN_TRAIN_DX
+                                    and pin_train_backward's per-neighbour path without mlp_grad;
+                                    NULL (or SDF only): f32 VALU */
 } PinMlp;
 
 /*
@@ -338,10 +340,15 @@ typedef struct PinTrainCfg {
     float grad_scale;            /* multiplies loss and gradients: 1, or 1/world_size so that a SUM
                                     all-reduce of per-rank gradients is the gradient of the mean loss */
     int32_t flags;               /* PIN_TRAIN_ROWS: `coord` of pin_train_forward holds every row (batch and
-                                    stencil, pin_train_rows / pin_train_gather) instead of the batch */
+                                    stencil, pin_train_rows / pin_train_gather) instead of the batch;
+                                    PIN_TRAIN_DX (weighted_first, mlp->packed set, no decoder gradient):
+                                    the forward decodes on the matrix cores and saves s dsdf/dx[0:8] in
+                                    x[:, 0:8] instead of the input, and the backward applies it without
+                                    re-evaluating the decoder */
 } PinTrainCfg;
 
 #define PIN_TRAIN_ROWS 1
+#define PIN_TRAIN_DX 2
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
 typedef struct PinTrainState {

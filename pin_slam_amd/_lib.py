@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("PIN_LIB") or os.path.join(_HERE, "libpin_slam_amd.so"
 
 PIN_OK = 0
 PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
+PIN_TRAIN_DX = 2     # PinTrainCfg.flags: forward saves s dsdf/dx (matrix-core decoder), backward applies it
 PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 

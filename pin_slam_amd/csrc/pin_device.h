@@ -898,4 +898,18 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     return out * m.sdf_scale;
 }
 
+// Block setup of the decoder (all threads; ends with a barrier): the f32 weights, or (MF) the
+// pin_mlp_pack image plus each wave's scratch rows for mlp_sdf_mfma16.
+template <bool MF>
+__device__ __forceinline__ MlpW stage_decoder(const PinMlp& m, float* s_mlp, uint4* s_pk, float* s_x16) {
+    if constexpr (MF) {
+        const uint4* src = (const uint4*)m.packed;
+        for (int e = threadIdx.x; e < kPkBytes / 16; e += blockDim.x) s_pk[e] = src[e];
+        __syncthreads();
+        return MlpW{nullptr, m.sdf_scale, s_x16 + (threadIdx.x >> 6) * kXsWave, (const unsigned char*)s_pk};
+    } else {
+        return stage_mlp(m, s_mlp);
+    }
+}
+
 }  // namespace pin

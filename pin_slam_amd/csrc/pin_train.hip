@@ -50,12 +50,15 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 #define PIN_CERT_T8 1   // certainty side effect: flush transposed, 8 lanes per row (see k_train_forward_grid)
 #endif
 
-template <bool WF, class Src>
+// MF (PIN_TRAIN_DX): whole waves call this (the matrix-core decoder); live false = a lane past
+// the last row that runs slot 0 and writes nothing.
+template <bool WF, class Src, bool MF = false>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
-                                                   float (&cw)[kK], int64_t& qts_out) {
+                                                   float (&cw)[kK], int64_t& qts_out, bool live = true) {
     // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
+    if (!live) t = 0;
     int64_t r;
     float qx, qy, qz;
     if (st.sorted_rows) {
@@ -81,7 +84,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
 #pragma unroll
     for (int d = 0; d < kD; ++d) x[d] = 0.f;
     float sdf = 0.f;
-    const int64_t qts = (ts && r < c.n_main) ? ts[r] : -1;
+    const int64_t qts = (live && ts && r < c.n_main) ? ts[r] : -1;
     qts_out = qts;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
@@ -101,11 +104,11 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         if (p.after_pgo && valid) quat_rotate_passive(((const float4*)p.orientations)[id], v0, v1, v2);
         const float w = valid && nn > 0 ? u[j] / S : 0.f;
         const float xj[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
-        if (j < nn_k) {
+        if (j < nn_k && live) {
             st.ids[t * nn_k + j] = id;
             st.weights[t * nn_k + j] = w;
         }
-        cid[j] = valid ? id : -1;
+        cid[j] = valid && live ? id : -1;
         cw[j] = w;
 #if !PIN_CERT_T8
         if (valid) {
@@ -133,12 +136,21 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         }
     }
     if (WF) {
-        float gx[kD];
-        sdf = mlp_sdf<false, 0, kD>(m, x, gx);
+        if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX)
+            float gx[kF];
+            sdf = mlp_sdf_mfma16<true, 0, kF>(m, x, gx);
+            if (live) {
 #pragma unroll
-        for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+                for (int d = 0; d < kF; ++d) st.x[t * kD + d] = gx[d];
+            }
+        } else {
+            float gx[kD];
+            sdf = mlp_sdf<false, 0, kD>(m, x, gx);
+#pragma unroll
+            for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+        }
     }
-    st.sdf[r] = sdf;
+    if (live) st.sdf[r] = sdf;
 }
 
 // The training side effects (neural_points.py:640 certainty scatter_add, :644 ts amax) are one
@@ -188,40 +200,46 @@ __device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int
 #endif
 }
 
-template <bool WF>
+template <bool WF, bool MF>
 __global__ void __launch_bounds__(kBlock)
 k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
-    __shared__ float s_mlp[kWSize];
-    const MlpW mw = stage_mlp(m, s_mlp);
+    __shared__ float s_mlp[MF ? 1 : kWSize];
+    __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
+    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
+    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
     int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if (t < c.n_main + 6 * c.n_stencil) {
+    if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const HashSource src(h, p);
-        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts);
+        train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts, t < rows);
     }
     if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
 }
 
-template <bool WF>
+template <bool WF, bool MF>
 __global__ void __launch_bounds__(kBlock)
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
-    __shared__ float s_mlp[kWSize];
-    const MlpW mw = stage_mlp(m, s_mlp);
+    __shared__ float s_mlp[MF ? 1 : kWSize];
+    __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
+    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
+    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
     int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if (t < c.n_main + 6 * c.n_stencil) {
+    if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const GridSource<false> src(g, p);
-        train_forward_body<WF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts);
+        train_forward_body<WF, GridSource<false>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts, t < rows);
     }
 #ifndef PIN_CERT_SKIP
     if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
@@ -346,16 +364,28 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
     }
 }
 
-template <bool WF, bool MLP_GRAD>
+// MF, frozen decoder (no MLP_GRAD), mlp->packed:
+//   weighted_first (PIN_TRAIN_DX): x holds s dsdf/dx[0:8] per slot from the forward; the feature
+//     terms are dL/dsdf times it, no decoder evaluation here;
+//   per-neighbour: each neighbour's input gradient from the matrix-core decoder (mlp_sdf_mfma16)
+//     instead of the f32 decoder backward.
+// (A per-block LDS pre-sum of the scatter -- hash table on the feature row, 512 tile-sorted slots,
+// ~2.7 references per row -- measured slower: 683 vs 467 us, the LDS float atomics alone 470 us.)
+template <bool WF, bool MLP_GRAD, bool MF = false>
 __global__ void __launch_bounds__(kBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
                  double* __restrict__ loss_part) {
+    static_assert(!MF || !MLP_GRAD, "matrix-core backward: frozen decoder");
+    constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
     constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
     __shared__ float gst[kBlock * kJ * kF];
     __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
-    __shared__ float s_mlp[kWSize];
-    const MlpW mlpw = stage_mlp(m, s_mlp);
+    __shared__ float s_mlp[MF ? 1 : kWSize];
+    __shared__ uint4 s_pk[kDecode ? kPkBytes / 16 : 1];
+    __shared__ float s_x16[kDecode ? kBlock / 64 * kXsWave : 1];
+    const MlpW mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk, s_x16)
+                              : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
@@ -369,7 +399,10 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     loss *= (double)c.grad_scale;
     const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
     float* mw = MLP_GRAD ? mlds[wave] : nullptr;
-    if (WF) {
+    if (WF && MF) {
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? dsdf * st.x[r * kD + d] : 0.f;
+    } else if (WF) {
         float x[kD];
 #pragma unroll
         for (int d = 0; d < kD; ++d) x[d] = live ? st.x[r * kD + d] : 0.f;
@@ -400,7 +433,16 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             float gf[kF];
 #pragma unroll
             for (int d = 0; d < kF; ++d) gf[d] = 0.f;
-            if (__any(ok) || MLP_GRAD) decoder_backward<MLP_GRAD>(mlpw, x, so * w, gf, mw, j > 0);
+            if constexpr (kDecode) {
+                if (__any(ok)) {   // wave-uniform: the whole wave decodes together
+                    float g8[kF];
+                    mlp_sdf_mfma16<true, 0, kF>(mlpw, x, g8);
+#pragma unroll
+                    for (int d = 0; d < kF; ++d) gf[d] = (dsdf * w) * g8[d];
+                }
+            } else if (__any(ok) || MLP_GRAD) {
+                decoder_backward<MLP_GRAD>(mlpw, x, so * w, gf, mw, j > 0);
+            }
 #pragma unroll
             for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
         }
@@ -578,23 +620,24 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     if ((!hash && !grid) || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    const bool dx = (cfg->flags & PIN_TRAIN_DX) != 0;
+    if (dx && (!cfg->weighted_first || !mlp->packed)) return PIN_ERR_ARG;
     if (rows == 0) return PIN_OK;
     auto s = as_stream(stream);
-    if (grid) {
-        if (cfg->weighted_first)
-            hipLaunchKernelGGL(k_train_forward_grid<true>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts, *mlp,
-                               coord, ts, *cfg, *st);
-        else
-            hipLaunchKernelGGL(k_train_forward_grid<false>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts, *mlp,
-                               coord, ts, *cfg, *st);
-    } else {
-        if (cfg->weighted_first)
-            hipLaunchKernelGGL(k_train_forward_hash<true>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts, *mlp,
-                               coord, ts, *cfg, *st);
-        else
-            hipLaunchKernelGGL(k_train_forward_hash<false>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts, *mlp,
-                               coord, ts, *cfg, *st);
-    }
+#define PIN_LAUNCH_FWD(KERNEL, SRC)                                                                             \
+    do {                                                                                                        \
+        if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp, \
+                                   coord, ts, *cfg, *st);                                                       \
+        else if (cfg->weighted_first)                                                                           \
+            hipLaunchKernelGGL((KERNEL<true, false>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp,     \
+                               coord, ts, *cfg, *st);                                                           \
+        else                                                                                                    \
+            hipLaunchKernelGGL((KERNEL<false, false>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp,    \
+                               coord, ts, *cfg, *st);                                                           \
+    } while (0)
+    if (grid) PIN_LAUNCH_FWD(k_train_forward_grid, grid);
+    else PIN_LAUNCH_FWD(k_train_forward_hash, hash);
+#undef PIN_LAUNCH_FWD
     return launch_status();
 }
 
@@ -614,10 +657,18 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 #define PIN_LAUNCH_BWD(WF, MG)                                                                               \
     hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
-    if (cfg->weighted_first) {
+    if (cfg->flags & PIN_TRAIN_DX) {
+        if (mlp_grad || !cfg->weighted_first) return PIN_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st,
+                           grad_features, mpart, lpart);
+    } else if (cfg->weighted_first) {
         if (mlp_grad) PIN_LAUNCH_BWD(true, true); else PIN_LAUNCH_BWD(true, false);
     } else {
-        if (mlp_grad) PIN_LAUNCH_BWD(false, true); else PIN_LAUNCH_BWD(false, false);
+        if (mlp_grad) PIN_LAUNCH_BWD(false, true);
+        else if (mlp->packed)
+            hipLaunchKernelGGL((k_train_backward<false, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg,
+                               *st, grad_features, mpart, lpart);
+        else PIN_LAUNCH_BWD(false, false);
     }
 #undef PIN_LAUNCH_BWD
     if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);

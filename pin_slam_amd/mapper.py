@@ -28,7 +28,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .data_sampler import DataSampler
-from .query import _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
+from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
 
 
 def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -470,7 +470,13 @@ class Mapper:
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                 ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
                                 order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None)
-        mv = mlp_view(self.geo_mlp)
+        # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
+        # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
+        dx = wf and mlp_grad is None and _MLP_PACK
+        # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores
+        mv = mlp_view(self.geo_mlp, packed=mlp_grad is None and _MLP_PACK)
+        if dx:
+            cfg.flags |= _lib.PIN_TRAIN_DX
         if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
             raise RuntimeError("local_geo_features must be a contiguous float32 tensor")
         if grid:

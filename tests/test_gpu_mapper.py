@@ -153,6 +153,38 @@ def test_train_step_tile_order_invisible(dev, wf, monkeypatch):
     np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("wf", [True, False])
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_matrix_core_train_step_matches_f32(dev, backend, wf, monkeypatch):
+    """Frozen decoder on the matrix cores -- weighted_first: the forward saves s dsdf/dx for the
+    backward (PIN_TRAIN_DX); per-neighbour: the backward's per-neighbour input gradients --
+    feature gradients, loss, sdf, certainties and ts against the f32 VALU path."""
+    import pin_slam_amd.mapper as M
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    res = []
+    for dx in (False, True):
+        monkeypatch.setattr(M, "_MLP_PACK", dx)
+        nm, dec, pts = surface_map(300, device=dev, weighted_first=wf, buffer_size=1 << 22, query_backend=backend)
+        coord, label, ts = surface_pool(pts, 70001, device=dev)
+        ts = torch.randint(0, 5, ts.shape, device=dev)
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        fg = torch.zeros_like(nm.local_geo_features.data)
+        loss = float(mapper.train_step(coord, label, ts, fg, None))
+        res.append((loss, mapper.last_sdf.clone(), fg, nm.local_point_certainties.clone(),
+                    nm.local_point_ts_update.clone()))
+    (l0, s0, f0, c0, t0), (l1, s1, f1, c1, t1) = res
+    assert torch.equal(t0, t1)
+    np.testing.assert_allclose(_np(s1), _np(s0), rtol=0, atol=1e-6)
+    assert l1 == pytest.approx(l0, rel=1e-6)
+    scale = float(f0.abs().max())
+    # per-term error ~1e-6 relative; sums of terms of both signs: absolute slack at 1e-4 of the
+    # largest; a hidden unit whose pre-activation sits at 0 can take the other ReLU branch in one
+    # of the two decoders (a gradient step of w2 W1): a few elements in 10^5 allowed off
+    off = ~np.isclose(_np(f1), _np(f0), rtol=1e-4, atol=1e-4 * scale)
+    assert off.mean() <= 1e-4, (off.sum(), off.size)
+    np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
+
+
 def test_frozen_decoder_trains_features_only(golden, dev):
     """Decoder frozen (freeze_model, utils/tools.py:186-191, after freeze_after_frame): the
     decoder parameters stay bit-identical and the features still move."""

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Timing attribution for the fused mapper iteration (GPU only): forward with / without the
-training side effects, backward, Adam, and the inference kernel on the same rows."""
+"""Timing attribution for one mapper iteration as mapping() runs it (GPU only): the forward with
+and without its training side effects, the backward with and without the feature scatter, on
+the rows of a real iteration (tile-sorted, PIN_TRAIN_DX when the decoder is frozen)."""
 import ctypes
 import os
 import sys
@@ -32,62 +33,49 @@ def timeit(fn, reps=10):
 def main():
     side = int(os.environ.get("SIDE", "2000"))
     bs = int(os.environ.get("BS", str(1 << 20)))
-    for wf in (True, False):
-        nm, dec, pts = surface_map(side, device="cuda", weighted_first=wf, bs=bs)
+    for wf in [bool(int(x)) for x in os.environ.get("WFS", "1,0").split(",")]:
+        nm, dec, pts = surface_map(side, device="cuda", weighted_first=wf, bs=bs, query_backend="grid")
         for p in dec.parameters():
             p.requires_grad_(False)
-        coord, label, ts = surface_pool(pts, bs, device="cuda")
+        coord, label, ts = surface_pool(pts, 1 << 22, device="cuda")
         mapper = P.Mapper(nm.config, None, nm, dec)
         mapper.set_pool(coord, label, ts)
-        fg = torch.zeros_like(nm.local_geo_features.data)
-        c = nm.config
+        mapper.mapping(1)
+        b = mapper._buf
         n = bs
         nd = (n + 9) // 10
         rows = n + 6 * nd
-        b = mapper._buf.get(rows, 8, wf, coord.device)
+        dx = wf
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=10, nn_k=8, weighted_first=int(wf),
                                eps=float(np.float32(0.06)), sigma=float(np.float32(0.055)), weight_e=0.5,
-                               grad_scale=1.0, flags=0)
+                               grad_scale=1.0, flags=_lib.PIN_TRAIN_ROWS | (_lib.PIN_TRAIN_DX if dx else 0))
         hv, pv = nm._views("local", True)
-        mv = mlp_view(dec)
+        gv = nm.grid_view("local", False)
+        mv = mlp_view(dec, packed=dx)
+        fg = torch.zeros_like(nm.local_geo_features.data)
         res = {}
-        for backend in ("grid", "hash"):
-            gv = nm.grid_view("local", False) if backend == "grid" else None
-            for tag, cert, tsp in (("full", nm.local_point_certainties, ts), ("no_ts", nm.local_point_certainties, None),
-                                   ("no_side", None, None)):
-                st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
-                                        sdf=b.sdf.data_ptr(), certainties=cert.data_ptr() if cert is not None else None,
-                                        ts_update=nm.local_point_ts_update.data_ptr() if tsp is not None else None)
-
-                def fwd():
-                    _lib.call("pin_train_forward", hv.ref() if gv is None else None, gv.ref() if gv else None,
-                              pv.ref(), mv.ref(), _lib.ptr(coord), _lib.ptr(tsp), ctypes.byref(cfg), ctypes.byref(st),
-                              _lib.stream())
-                res[f"fwd_{backend}_{tag}"] = timeit(fwd)
+        for tag, cert, tsp in (("full", nm.local_point_certainties, b.ts), ("no_ts", nm.local_point_certainties, None),
+                               ("no_side", None, None)):
             st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
-                                    sdf=b.sdf.data_ptr(), certainties=None, ts_update=None)
+                                    sdf=b.sdf.data_ptr(), certainties=cert.data_ptr() if cert is not None else None,
+                                    ts_update=nm.local_point_ts_update.data_ptr() if tsp is not None else None,
+                                    order=None, sorted_rows=b.rows4.data_ptr())
+
+            def fwd():
+                _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(b.rows), _lib.ptr(tsp),
+                          ctypes.byref(cfg), ctypes.byref(st), _lib.stream())
+            res[f"fwd_{tag}"] = timeit(fwd)
 
         def bwd():
-            _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
-                      _lib.ptr(fg), None, _lib.ptr(b.workspace), _lib.ptr(b.loss), _lib.stream())
+            _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(b.label), ctypes.byref(cfg),
+                      ctypes.byref(st), _lib.ptr(fg), None, _lib.ptr(b.workspace), _lib.ptr(b.loss), _lib.stream())
         res["bwd"] = timeit(bwd)
 
         def bwd_nofeat():
-            _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
-                      None, None, _lib.ptr(b.workspace), _lib.ptr(b.loss), _lib.stream())
+            _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(b.label), ctypes.byref(cfg),
+                      ctypes.byref(st), None, None, _lib.ptr(b.workspace), _lib.ptr(b.loss), _lib.stream())
         res["bwd_no_scatter"] = timeit(bwd_nofeat)
-        m, v = torch.zeros_like(fg), torch.zeros_like(fg)
-        from pin_slam_amd.mapper import adam_scalars
-        a = adam_scalars(0.01, 1, 1e-15)
-        res["adam"] = timeit(lambda: _lib.call("pin_adam_step", _lib.ptr(nm.local_geo_features.data), _lib.ptr(fg),
-                                               _lib.ptr(m), _lib.ptr(v), fg.numel(), ctypes.byref(a), _lib.stream()))
-        allrows = torch.cat([coord] + [coord[::10] + 0.06 * torch.tensor(e, device="cuda") for e in
-                                       ([1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1])])
-        res["infer_grid_fat_nograd"] = timeit(lambda: P.query_sdf(nm, dec, allrows, want_grad=False,
-                                                                  want_certainty=False))
-        res["mapping_iter"] = timeit(lambda: mapper.mapping(1), reps=5)
-        print(f"wf={wf} rows={rows} map={pts.shape[0]}:", {k: round(v_, 1) for k, v_ in res.items()}, flush=True)
-        del nm, dec, pts, mapper
+        print(f"wf={int(wf)} rows={rows} " + "  ".join(f"{k} {v:.1f}" for k, v in res.items()), flush=True)
 
 
 if __name__ == "__main__":
