@@ -72,6 +72,34 @@ def measured_traffic(kernel_prefix):
     return None
 
 
+MFMA_FILE = os.path.join(ROOT, "profiles", "mfma.json")
+F16_DENSE_PEAK = 2.5e15   # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense
+ENGINE_CLOCK = 2.4e9
+
+
+def mfma_evidence(kernel, wf, kern_ms):
+    """The headline decoder's matrix-core work: F16 FLOPs per launch (48 v_mfma_f32_16x16x32_f16
+    per 64-query wave per decode, weighted_first one decode per query, else 8) against the dense
+    F16 peak at the live kernel time, plus the busy fraction from the committed PMC pass
+    (tools/mfma_pmc.sh: SQ_VALU_MFMA_BUSY_CYCLES per launch over kernel cycles x 1024 SIMDs)."""
+    waves = (N_QUERY + 63) // 64
+    flop = waves * 48 * (16 * 16 * 32 * 2) * (1 if wf else 8)
+    res = {"dtype": "f16 operands (f32 values split hi/lo), f32 accumulate", "instr": "v_mfma_f32_16x16x32_f16",
+           "flop_per_launch": flop, "achieved_tflops": flop / (kern_ms * 1e-3) / 1e12,
+           "peak_tflops": F16_DENSE_PEAK / 1e12, "frac": flop / (kern_ms * 1e-3) / F16_DENSE_PEAK,
+           "busy_frac": None, "pmc_flop_per_launch": None, "source": "profiles/mfma.json"}
+    try:
+        with open(MFMA_FILE) as f:
+            for k in json.load(f).get("kernels", []):
+                if k["name"].startswith(kernel):
+                    res["pmc_flop_per_launch"] = k.get("f16_flop")
+                    if k.get("mfma_busy_cycles"):
+                        res["busy_frac"] = k["mfma_busy_cycles"] / (kern_ms * 1e-3 * ENGINE_CLOCK * 1024)
+    except (OSError, ValueError):
+        pass
+    return res
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -583,6 +611,12 @@ def main():
     total_q = N_QUERY * args.steps * world
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
+    # the launched instance: <WF, PGO, GRAD, FAT, MF> (grid) / <WF, PGO, GRAD, MF> (hash)
+    from pin_slam_amd.query import _MLP_PACK
+    mf = str(bool(_MLP_PACK)).lower()
+    kernel_name = "k_query_sdf_grid" if backend == "grid" else "k_query_sdf"
+    kernel_tpl = (f"{str(wf).lower()}, false, true, true, {mf}>" if backend == "grid"
+                  else f"{str(wf).lower()}, false, true, {mf}>")
     out = {
         "metric": "SDF+grad queries/sec over 1M-point map",
         "value": value,
@@ -604,13 +638,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": (args.traffic_bytes if args.traffic_bytes is not None
-                                 else measured_traffic(f"k_query_sdf_grid<{str(wf).lower()}, false, true, true>"
-                                                       if backend == "grid" else "k_query_sdf<")),
+                                 else measured_traffic(f"{kernel_name}<" + kernel_tpl)),
                      "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
                                        "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
-                     "kernel": "k_query_sdf_grid" if backend == "grid" else "k_query_sdf", "kernel_ms": kern_ms,
+                     "kernel": kernel_name, "kernel_ms": kern_ms,
                      "order_pass_ms": order_ms,
                      "algorithmic_bytes_per_query": BYTES_PER_QUERY},
+        "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
