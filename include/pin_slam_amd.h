@@ -114,7 +114,7 @@ typedef struct PinMlp {
  * is ~2^-22 relative, the f32 rounding level of the reference's own sums.  Inputs |x| < 2^29.
  * Re-run after every decoder update (Mapper steps change W1/b1/W2/b2).
  */
-#define PIN_MLP_PACK_BYTES 8320
+#define PIN_MLP_PACK_BYTES 8288
 int pin_mlp_pack(const PinMlp* mlp, void* packed, void* stream);
 
 /*

@@ -71,7 +71,7 @@ class PinMlp(ctypes.Structure):
                 ("reserved", i32), ("packed", c_void_p)]
 
 
-MLP_PACK_BYTES = 8320
+MLP_PACK_BYTES = 8288
 
 
 class PinTrainCfg(ctypes.Structure):

@@ -17,6 +17,9 @@
 #ifndef PIN_NB_GROUP
 #define PIN_NB_GROUP 4       // neighbours gathered per streaming group
 #endif
+#ifndef PIN_PRED_GATHER
+#define PIN_PRED_GATHER 0    // 1: gathers of finished / invalid lanes masked off instead of clamped to entry 0
+#endif
 #ifndef PIN_GRID_CHUNK
 #define PIN_GRID_CHUNK 4     // candidate records fetched per round trip (grid source; 4 measured best)
 #endif
@@ -173,10 +176,22 @@ __device__ __forceinline__ uint32_t sel4v(uint32_t w0, uint32_t w1, uint32_t w2,
     return (k & 2) ? a1 : a0;
 }
 
+// Per-wave LDS list of the grid scan, [slot][lane] (one column per lane: conflict-free, no
+// barrier).  The matrix-core decoder takes the wave's slice as its scratch once the wave's scan
+// is over (mlp_sdf_mfma16), so the two share 32 KB per block.
+#ifndef PIN_LIST_SEG
+#define PIN_LIST_SEG 32
+#endif
+constexpr int kListSeg = PIN_LIST_SEG;   // offsets per list segment
+__device__ __forceinline__ int* wave_list() {
+    __shared__ int s_list[kBlock / 64][kListSeg * 64];
+    return s_list[threadIdx.x >> 6];
+}
+
 template <bool FAT>
 struct GridSource {
     static constexpr int kChunk = PIN_GRID_CHUNK;
-    static constexpr int kSeg = 32;   // offsets per list segment: 32 KB of LDS per block
+    static constexpr int kSeg = kListSeg;
     const PinGrid& gr;
     const PinPoints& p;
     __device__ GridSource(const PinGrid& g_, const PinPoints& p_) : gr(g_), p(p_) {}
@@ -201,7 +216,7 @@ struct GridSource {
     // cells only, CH per round trip.
     template <int CH>
     __device__ __forceinline__ int scan_window(float qx, float qy, float qz, TopK& tk) const {
-        __shared__ int s_list[kSeg][kBlock];
+        int* const s_list = wave_list();
         const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
         const float4* __restrict__ crec = (const float4*)gr.crec;
         const int32_t* __restrict__ offs = gr.offsets;
@@ -228,7 +243,7 @@ struct GridSource {
                 wp[k] = w[k].z;
             }
         }
-        const int tid = threadIdx.x;
+        const int lane = threadIdx.x & 63;
         const int Kc = gr.num_cells;
         int nn = 0;
         if (gr.num_columns > 0) {
@@ -267,7 +282,7 @@ struct GridSource {
                     const uint64_t bits = up ? (((uint64_t)hi1 << 32) | lo1) : (((uint64_t)hi0 << 32) | lo0);
                     const uint32_t pre = up ? pre1 : pre0;
                     const int bit = sh | (z & 3);
-                    s_list[cnt][tid] = (int)(pre + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
+                    s_list[cnt * 64 + lane] = (int)(pre + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
                     ++cnt;
                 }
             }
@@ -286,7 +301,7 @@ struct GridSource {
                 const uint64_t bits = ((uint64_t)sel8(wh, k) << 32) | sel8(wl, k);
                 const int bit = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
                 if ((bits >> bit) & 1ull) {
-                    s_list[cnt][tid] = (int)(sel8(wp, k) + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
+                    s_list[cnt * 64 + lane] = (int)(sel8(wp, k) + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
                     ++cnt;
                 }
             }
@@ -299,20 +314,28 @@ struct GridSource {
     // longest list among the ACTIVE lanes (__any ignores lanes that returned early in a partial
     // last wave).
     template <int CH>
-    __device__ __forceinline__ static void records_from_list(const int (*s_list)[kBlock], int cnt,
+    __device__ __forceinline__ static void records_from_list(const int* s_list, int cnt,
                                                              const float4* __restrict__ crec, float qx, float qy,
                                                              float qz, float maxd2, TopK& tk, int& nn) {
-        const int tid = threadIdx.x;
+        const int lane = threadIdx.x & 63;
         for (int j0 = 0; __any(j0 < cnt); j0 += CH) {
             int ci[CH];
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
-                const int v = s_list[j0 + u < kSeg ? j0 + u : kSeg - 1][tid];   // stale slots are masked
+                const int v = s_list[(j0 + u < kSeg ? j0 + u : kSeg - 1) * 64 + lane];   // stale slots are masked
                 ci[u] = (j0 + u < cnt) ? v : -1;
             }
             float4 r[CH];
 #pragma unroll
-            for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
+            for (int u = 0; u < CH; ++u) {
+#if PIN_PRED_GATHER
+                // lanes whose list is done issue nothing (no L1 access / TA-TD work for them)
+                r[u] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                if (ci[u] >= 0) r[u] = crec[ci[u]];
+#else
+                r[u] = crec[ci[u] > 0 ? ci[u] : 0];
+#endif
+            }
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int id = __float_as_int(r[u].w);
@@ -778,8 +801,11 @@ constexpr int kPkA1 = 0;                    // [4 mt][64 lanes] f16x8   GEMM1 K-
 constexpr int kPkA2 = kPkA1 + 4 * 64 * 16;  // [2 ch][2 term][64 lanes] f16x8
 constexpr int kPkScale = kPkA2 + 4 * 64 * 16;   // [16] f32: 2^-f_i of GEMM2 row i
 constexpr int kPkB2 = kPkScale + 16 * 4;        // f32 b2
-constexpr int kPkBytes = 8320;
+constexpr int kPkBytes = 8288;
 static_assert(kPkB2 + 4 <= kPkBytes && kPkBytes == PIN_MLP_PACK_BYTES && kPkBytes % 16 == 0, "pack layout");
+#ifndef PIN_MF_NT_OUTER
+#define PIN_MF_NT_OUTER 0   // 1: query tile as the outer GEMM loop (fewer live VGPRs, A re-read per tile)
+#endif
 constexpr int kXsStride = 20;               // floats per query row of the decoder scratch (80 B: conflict-free)
 constexpr int kXsWave = 64 * kXsStride;     // floats of scratch per wave
 
@@ -805,6 +831,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     const unsigned char* pk = m.pk;
     const int lane = threadIdx.x & 63;
     const int col = lane & 15, grp = lane >> 4;
+    wave_lds_sync();   // xs aliases the wave's scan list: every lane is past its scan reads
     // ---- this lane's query as B1 column: scale, split, one 80-B LDS row
     float mx = 0.f;
 #pragma unroll
@@ -833,6 +860,42 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     }
     wave_lds_sync();
     // B operands of the four query tiles (lane group 3 reads lo-row halves; its A slots are 0)
+#if PIN_MF_NT_OUTER
+    // query tile outer: one tile's B operands, masks and GEMM2 accumulator live at a time (the A
+    // tiles are re-read from LDS per tile); g of tile nt is written over its own, consumed B rows
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const float* rb = xs + (16 * nt + col) * kXsStride;
+        const f16x8 bh = *(const f16x8*)(rb + 4 * grp);
+        const f16x8 bl = *(const f16x8*)(rb + 12 + 4 * min(grp, 1));
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            uint32_t mk[4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int mt = 2 * ch + h;
+                const f16x8 a = ((const f16x8*)(pk + kPkA1))[mt * 64 + lane];
+                const uint4 au = __builtin_bit_cast(uint4, a);
+                const f16x8 al = __builtin_bit_cast(
+                    f16x8, make_uint4(grp < 2 ? au.x : 0u, grp == 0 ? au.y : (grp == 1 ? (au.y & 0xFFFFu) : 0u),
+                                      grp == 0 ? au.z : 0u, grp == 0 ? au.w : 0u));
+                f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bl, d, 0, 0, 0);
+                mk[2 * h] = mask_f16x2(d[0], d[1]);
+                mk[2 * h + 1] = mask_f16x2(d[2], d[3]);
+            }
+            const f16x8 a2h = ((const f16x8*)(pk + kPkA2))[(2 * ch) * 64 + lane];
+            const f16x8 a2l = ((const f16x8*)(pk + kPkA2))[(2 * ch + 1) * 64 + lane];
+            const f16x8 b = __builtin_bit_cast(f16x8, make_uint4(mk[0], mk[1], mk[2], mk[3]));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h, b, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l, b, acc, 0, 0, 0);
+        }
+        wave_lds_sync();   // every lane has read tile nt's B rows
+        if (grp < 3) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc;
+    }
+    wave_lds_sync();
+#else
     f16x8 bh[4];
     f16x8 bl[4];   // x-lo rows: groups 2, 3 re-read group 1's slots (their A slots are 0)
 #pragma unroll
@@ -880,6 +943,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
         for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
     }
     wave_lds_sync();
+#endif
     const f32x4* r = (const f32x4*)(xs + lane * kXsStride);
     const f32x4 g0 = r[0], g1 = r[1], g2 = r[2];
     const f32x4* us = (const f32x4*)(pk + kPkScale);
@@ -899,14 +963,16 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
 }
 
 // Block setup of the decoder (all threads; ends with a barrier): the f32 weights, or (MF) the
-// pin_mlp_pack image plus each wave's scratch rows for mlp_sdf_mfma16.
+// pin_mlp_pack image, with each wave's scan list as the scratch of mlp_sdf_mfma16.
+static_assert(kXsWave <= kListSeg * 64, "decoder scratch must fit the wave's scan list");
+
 template <bool MF>
-__device__ __forceinline__ MlpW stage_decoder(const PinMlp& m, float* s_mlp, uint4* s_pk, float* s_x16) {
+__device__ __forceinline__ MlpW stage_decoder(const PinMlp& m, float* s_mlp, uint4* s_pk) {
     if constexpr (MF) {
         const uint4* src = (const uint4*)m.packed;
         for (int e = threadIdx.x; e < kPkBytes / 16; e += blockDim.x) s_pk[e] = src[e];
         __syncthreads();
-        return MlpW{nullptr, m.sdf_scale, s_x16 + (threadIdx.x >> 6) * kXsWave, (const unsigned char*)s_pk};
+        return MlpW{nullptr, m.sdf_scale, (float*)wave_list(), (const unsigned char*)s_pk};
     } else {
         return stage_mlp(m, s_mlp);
     }

@@ -144,6 +144,9 @@ __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints
 #if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 2
     // profiling variant: no record re-gather (wrong positions, same instruction stream otherwise)
     const float4 r = make_float4(qx + 0.1f, qy - 0.1f, qz + 0.05f * (float)(pay & 7), __int_as_float(pay));
+#elif PIN_PRED_GATHER
+    float4 r = make_float4(qx, qy, qz, __int_as_float(-1));
+    if (valid) r = src.record(pay);
 #else
     const float4 r = src.record(pay);
 #endif
@@ -154,6 +157,9 @@ __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints
     // profiling variant: no feature gathers
     f0 = make_float4(r.x * 0.01f, r.y * 0.01f, r.z * 0.01f, 0.02f);
     f1 = make_float4(r.y * 0.02f, r.z * 0.02f, r.x * 0.03f, -0.02f);
+#elif PIN_PRED_GATHER
+    f0 = f1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) src.features(pay, id, f0, f1);
 #else
     src.features(pay, id, f0, f1);
 #endif
@@ -386,8 +392,7 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
             float* __restrict__ cert_out, float* __restrict__ std_out) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
-    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
-    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
+    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (MF ? (t & ~(int64_t)63) >= n : t >= n) return;
     const int64_t i = t < n ? t : -1, iq = t < n ? t : 0;
@@ -399,21 +404,24 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
 #ifndef PIN_SDF_WAVES
 #define PIN_SDF_WAVES 2   // waves per SIMD the fused grid kernel is compiled for (VGPR budget)
 #endif
+#ifndef PIN_SDF_WAVES_NWF
+#define PIN_SDF_WAVES_NWF PIN_SDF_WAVES   // the same for per-neighbour decoding
+#endif
 
 // q4 != NULL: the queries pre-sorted by pin_query_sort, {x, y, z, bits(original index)} each
 // (one coalesced 16-B load, no order -> coordinate dependency); otherwise q [n,3] processed in
 // `order` (or input order).
 // MF: decoder on the f16 matrix cores (mlp_sdf_mfma16, m.packed from pin_mlp_pack).
 template <bool WF, bool PGO, bool GRAD, bool FAT, bool MF>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PGO ? 1 : PIN_SDF_WAVES)))
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(PGO ? 1 : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES_NWF))))
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q,
                  const float4* __restrict__ q4, int64_t n, int nn_k, int zero_empty, float* __restrict__ sdf_out,
                  float* __restrict__ grad_out, int* __restrict__ nn_out, float* __restrict__ cert_out,
                  float* __restrict__ std_out, const int* __restrict__ order) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
-    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
-    MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
+    MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
 #if PIN_MLP_MFMA
     __shared__ float s_xs[kBlock / 64][64 * kWRow];

@@ -206,8 +206,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
-    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
-    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
+    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
@@ -228,8 +227,7 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
-    __shared__ float s_x16[MF ? kBlock / 64 * kXsWave : 1];
-    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk, s_x16);
+    const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
@@ -383,8 +381,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[kDecode ? kPkBytes / 16 : 1];
-    __shared__ float s_x16[kDecode ? kBlock / 64 * kXsWave : 1];
-    const MlpW mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk, s_x16)
+    const MlpW mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk)
                               : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
