@@ -17,9 +17,6 @@
 #ifndef PIN_NB_GROUP
 #define PIN_NB_GROUP 4       // neighbours gathered per streaming group
 #endif
-#ifndef PIN_PRED_GATHER
-#define PIN_PRED_GATHER 0    // 1: gathers of finished / invalid lanes masked off instead of clamped to entry 0
-#endif
 #ifndef PIN_GRID_CHUNK
 #define PIN_GRID_CHUNK 4     // candidate records fetched per round trip (grid source; 4 measured best)
 #endif
@@ -234,7 +231,12 @@ struct GridSource {
             for (int k = 0; k < 8; ++k) {
                 const int bx = bx0 + (k & 1), by = by0 + ((k >> 1) & 1), bz = bz0 + (k >> 2);
                 in[k] = (unsigned)bx < (unsigned)nbx && (unsigned)by < (unsigned)nby && (unsigned)bz < (unsigned)nbz;
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 6
+                __shared__ uint4 s_fakeb[512];   // profiling variant: bricks from LDS (wrong values)
+                w[k] = s_fakeb[(in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0) & 511];
+#else
                 w[k] = bricks[in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0];
+#endif
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -328,10 +330,11 @@ struct GridSource {
             float4 r[CH];
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
-#if PIN_PRED_GATHER
-                // lanes whose list is done issue nothing (no L1 access / TA-TD work for them)
-                r[u] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-                if (ci[u] >= 0) r[u] = crec[ci[u]];
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE >= 5
+                // profiling variant: records from an LDS table (wrong values): what a wave-staged
+                // record set would cost
+                __shared__ float4 s_fake[1024];
+                r[u] = s_fake[(ci[u] > 0 ? ci[u] : 0) & 1023];
 #else
                 r[u] = crec[ci[u] > 0 ? ci[u] : 0];
 #endif

@@ -144,9 +144,6 @@ __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints
 #if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 2
     // profiling variant: no record re-gather (wrong positions, same instruction stream otherwise)
     const float4 r = make_float4(qx + 0.1f, qy - 0.1f, qz + 0.05f * (float)(pay & 7), __int_as_float(pay));
-#elif PIN_PRED_GATHER
-    float4 r = make_float4(qx, qy, qz, __int_as_float(-1));
-    if (valid) r = src.record(pay);
 #else
     const float4 r = src.record(pay);
 #endif
@@ -157,9 +154,6 @@ __device__ __forceinline__ void stream_neighbour(const Src& src, const PinPoints
     // profiling variant: no feature gathers
     f0 = make_float4(r.x * 0.01f, r.y * 0.01f, r.z * 0.01f, 0.02f);
     f1 = make_float4(r.y * 0.02f, r.z * 0.02f, r.x * 0.03f, -0.02f);
-#elif PIN_PRED_GATHER
-    f0 = f1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) src.features(pay, id, f0, f1);
 #else
     src.features(pay, id, f0, f1);
 #endif
