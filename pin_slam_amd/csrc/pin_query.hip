@@ -626,7 +626,13 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
     // the placement does not depend on the ranking's blocks: it runs 2 queries per thread (more
     // blocks in flight for its scattered 16-B stores)
-    constexpr int kPlacePer = 2;
+#ifndef PIN_PLACE_PER
+#define PIN_PLACE_PER 2
+#endif
+#ifndef PIN_RANK_PER
+#define PIN_RANK_PER 4
+#endif
+    constexpr int kPlacePer = PIN_PLACE_PER;
     const int nplace = (int)((n + kPlacePer * kPartThreads - 1) / (kPlacePer * kPartThreads));
     auto launch = [&](auto per_tag) {
         constexpr int PER = decltype(per_tag)::value;
@@ -635,7 +641,7 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
         hipLaunchKernelGGL(k_tile_place<kPlacePer>, dim3(nplace), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot, done,
                            tk, q4, order);
     };
-    if (n <= (1 << 19)) launch(std::integral_constant<int, 4>());
+    if (n <= (1 << 19)) launch(std::integral_constant<int, PIN_RANK_PER>());
     else launch(std::integral_constant<int, 16>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }

@@ -81,6 +81,9 @@ class SlabPartition:
                 self.send_rows[s] = sr
         self.halo = torch.cat(list(self.recv_rows.values())) if self.recv_rows else \
             torch.empty(0, dtype=torch.long, device=dev)
+        # the group's first collective is then never a partial point-to-point batch (torch requires
+        # every rank in the first batch_isend_irecv of a group)
+        dist.barrier(group=group)
 
     # ------------------------------------------------------------------ samples
     def sample_mask(self, coords: torch.Tensor) -> torch.Tensor:
@@ -105,8 +108,12 @@ class SlabPartition:
                 out = out.cpu()
                 staged[s] = torch.empty(inp.shape, dtype=inp.dtype)
                 inp = staged[s]
-            ops.append(dist.P2POp(dist.isend, out, dst, g))
-            ops.append(dist.P2POp(dist.irecv, inp, dst, g))
+            # empty directions are skipped on both sides alike (the sizes pair up element by
+            # element), so no zero-byte transfer reaches the backend
+            if out.numel():
+                ops.append(dist.P2POp(dist.isend, out, dst, g))
+            if inp.numel():
+                ops.append(dist.P2POp(dist.irecv, inp, dst, g))
         # one group: with RCCL, a send and a receive to the same peer issued separately can
         # deadlock (each waits behind the other on the peer's stream)
         for q in dist.batch_isend_irecv(ops) if ops else []:
