@@ -108,3 +108,19 @@ def test_cpu_tensors_are_rejected():
         assert "ROCm device" in str(e)
     else:
         raise AssertionError("CPU tensors must not silently run a fallback")
+
+
+def test_argument_errors_before_any_device_work():
+    """Bad arguments come back as PIN_ERR_ARG / PIN_ERR_UNSUPPORTED before anything touches the
+    device (so these run without a GPU)."""
+    from pin_slam_amd import _lib
+    lib = _lib.load()
+    m = _lib.PinMlp()
+    assert lib.pin_mlp_pack(None, None, None) == -1
+    assert lib.pin_mlp_pack(ctypes.byref(m), None, None) == -1           # NULL weights
+    m.W1 = m.b1 = m.W2 = m.b2 = 16
+    assert lib.pin_mlp_pack(ctypes.byref(m), ctypes.c_void_p(8), None) == -1   # packed not 16-B aligned
+    st = _lib.PinAdamStep(grad_stride=4)
+    assert lib.pin_adam_rows(None, None, None, None, None, 0, ctypes.byref(st), None) == -3   # stride != 8
+    cfg = _lib.PinTrainCfg(n_main=-1, decimation=1)
+    assert lib.pin_train_rows(None, ctypes.byref(cfg), None, None) == -1
