@@ -21,7 +21,7 @@ mapper.set_pool(coord, label, ts)
 mapper.mapping(1)
 ids = mapper._buf.ids
 rows = ids.shape[0]
-for blk in (256, 1024):
+for blk in (64, 128, 256, 1024):
     nb = rows // blk
     x = ids[: nb * blk].reshape(nb, blk * ids.shape[1]).long()
     valid = (x >= 0).sum().item()
