@@ -231,12 +231,7 @@ struct GridSource {
             for (int k = 0; k < 8; ++k) {
                 const int bx = bx0 + (k & 1), by = by0 + ((k >> 1) & 1), bz = bz0 + (k >> 2);
                 in[k] = (unsigned)bx < (unsigned)nbx && (unsigned)by < (unsigned)nby && (unsigned)bz < (unsigned)nbz;
-#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 6
-                __shared__ uint4 s_fakeb[512];   // profiling variant: bricks from LDS (wrong values)
-                w[k] = s_fakeb[(in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0) & 511];
-#else
                 w[k] = bricks[in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0];
-#endif
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
@@ -330,8 +325,9 @@ struct GridSource {
             float4 r[CH];
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
-#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE >= 5
-                // profiling variant: records from an LDS table (wrong values): what a wave-staged
+#if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 5
+                // profiling variant: records from an LDS table (wrong values; the payloads stay
+                // valid compact indices, so later gathers stay in bounds): what a wave-staged
                 // record set would cost
                 __shared__ float4 s_fake[1024];
                 r[u] = s_fake[(ci[u] > 0 ? ci[u] : 0) & 1023];
