@@ -100,6 +100,7 @@ struct TopK {
 // Payload = global point index; records indexed by it.
 struct HashSource {
     static constexpr int kChunk = 12;
+    static constexpr bool kIdPayload = false;
     const PinHash& h;
     const PinPoints& p;
     __device__ HashSource(const PinHash& h_, const PinPoints& p_) : h(h_), p(p_) {}
@@ -185,10 +186,14 @@ __device__ __forceinline__ int* wave_list() {
     return s_list[threadIdx.x >> 6];
 }
 
-template <bool FAT>
+// IDP: the top-k payload is the record's feature-row id (flags stripped) instead of its
+// compact index -- for the training forward, which reads features and positions by id and never
+// needs the record again (one dependent round trip fewer per neighbour group).
+template <bool FAT, bool IDP = false>
 struct GridSource {
     static constexpr int kChunk = PIN_GRID_CHUNK;
     static constexpr int kSeg = kListSeg;
+    static constexpr bool kIdPayload = IDP;
     const PinGrid& gr;
     const PinPoints& p;
     __device__ GridSource(const PinGrid& g_, const PinPoints& p_) : gr(g_), p(p_) {}
@@ -341,7 +346,7 @@ struct GridSource {
                 const float d2 = dist2(r[u].x, r[u].y, r[u].z, qx, qy, qz);
                 const bool ok = ci[u] >= 0 && id != -1 && d2 <= maxd2;
                 nn += ok ? 1 : 0;
-                tk.insert(ok ? d2 : INFINITY, ci[u]);
+                tk.insert(ok ? d2 : INFINITY, IDP ? (id & kIdMask) : ci[u]);
             }
         }
     }
@@ -393,7 +398,7 @@ struct GridSource {
                 const float d2 = dist2(r[t].x, r[t].y, r[t].z, qx, qy, qz);
                 const bool ok = ci[t] >= 0 && id != -1 && d2 <= maxd2;
                 nn += ok ? 1 : 0;
-                tk.insert(ok ? d2 : INFINITY, ci[t]);
+                tk.insert(ok ? d2 : INFINITY, IDP ? (id & kIdMask) : ci[t]);
             }
         }
         return nn;

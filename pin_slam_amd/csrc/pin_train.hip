@@ -46,6 +46,9 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
     else qz = (blk & 1) ? qz - c.eps : qz + c.eps;
 }
 
+#ifndef PIN_TRAIN_IDP
+#define PIN_TRAIN_IDP 1   // training forward: top-k payload = feature-row id (GridSource IDP)
+#endif
 #ifndef PIN_CERT_T8
 #define PIN_CERT_T8 1   // certainty side effect: flush transposed, 8 lanes per row (see k_train_forward_grid)
 #endif
@@ -90,16 +93,31 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     for (int j = 0; j < kK; ++j) {
         if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
         const bool valid = u[j] > 0.f;
-        const float4 rc = src.record(tk.g[j]);
-        const int raw = __float_as_int(rc.w);
-        const int id = valid ? (raw & kIdMask) : -1;
+        int id;
         float4 f0, f1;
-        src.features(tk.g[j], id > 0 ? id : 0, f0, f1);
-        float v0 = qx - rc.x, v1 = qy - rc.y, v2 = qz - rc.z;
-        if (valid && (raw & PIN_RECORD_UNFAITHFUL)) {
-            v0 = qx - p.positions[3 * (int64_t)id];
-            v1 = qy - p.positions[3 * (int64_t)id + 1];
-            v2 = qz - p.positions[3 * (int64_t)id + 2];
+        float v0, v1, v2;
+        if constexpr (Src::kIdPayload) {
+            // payload = id: the neighbour vector reads positions[id], which is the record's position
+            // bitwise for a faithful record and what the reference reads for an unfaithful one
+            id = valid ? tk.g[j] : -1;
+            const int64_t ii = id > 0 ? id : 0;
+            src.features(0, ii, f0, f1);
+            v0 = qx - p.positions[3 * ii];
+            v1 = qy - p.positions[3 * ii + 1];
+            v2 = qz - p.positions[3 * ii + 2];
+        } else {
+            const float4 rc = src.record(tk.g[j]);
+            const int raw = __float_as_int(rc.w);
+            id = valid ? (raw & kIdMask) : -1;
+            src.features(tk.g[j], id > 0 ? id : 0, f0, f1);
+            v0 = qx - rc.x;
+            v1 = qy - rc.y;
+            v2 = qz - rc.z;
+            if (valid && (raw & PIN_RECORD_UNFAITHFUL)) {
+                v0 = qx - p.positions[3 * (int64_t)id];
+                v1 = qy - p.positions[3 * (int64_t)id + 1];
+                v2 = qz - p.positions[3 * (int64_t)id + 2];
+            }
         }
         if (p.after_pgo && valid) quat_rotate_passive(((const float4*)p.orientations)[id], v0, v1, v2);
         const float w = valid && nn > 0 ? u[j] / S : 0.f;
@@ -236,8 +254,9 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
-        const GridSource<false> src(g, p);
-        train_forward_body<WF, GridSource<false>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts, t < rows);
+        const GridSource<false, PIN_TRAIN_IDP> src(g, p);
+        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts,
+                                                                     t < rows);
     }
 #ifndef PIN_CERT_SKIP
     if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
