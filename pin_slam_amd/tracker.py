@@ -59,6 +59,24 @@ def _expmap_np(axis_angle: np.ndarray) -> np.ndarray:
     return np.eye(3) + K * np.sin(angle) + (K @ K) * (1.0 - np.cos(angle))
 
 
+_T_PIN = {}
+
+
+def _to_device(a: np.ndarray, device):
+    """A small host array to the device through a per-device pinned staging buffer, without
+    blocking the host (the caller's next _reg_accumulate read-back synchronises the stream before
+    the buffer is written again)."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return torch.from_numpy(a).to(dev)
+    key = (str(dev), a.shape, a.dtype.str)
+    buf = _T_PIN.get(key)
+    if buf is None:
+        buf = _T_PIN[key] = torch.empty(a.shape, dtype=torch.from_numpy(a).dtype, pin_memory=True)
+    buf.numpy()[...] = a
+    return buf.to(dev, non_blocking=True)
+
+
 def _solve(acc: np.ndarray, lm_lambda: float, require_cov: bool, require_eigen: bool, device):
     """Normal equations from the kernel accumulators -> (dT 4x4 f64, cov, eigenvalues).
     The weight normalisation w /= 2 mean(w) (utils/tracker.py:394) is the factor
@@ -80,7 +98,7 @@ def _solve(acc: np.ndarray, lm_lambda: float, require_cov: bool, require_eigen: 
     T_np = np.eye(4)
     T_np[:3, :3] = _expmap_np(t[:3])
     T_np[:3, 3] = t[3:]
-    T = torch.from_numpy(T_np).to(device)
+    T = _to_device(T_np, device)
     eig = None
     if require_eigen:
         eig = torch.from_numpy(np.linalg.eigvals(N_old[3:, 3:]).real.copy()).to(device)
