@@ -21,6 +21,7 @@ mapping(): nothing inside an iteration reads them.
 drop-in query_feature for callers outside the fused loop.
 """
 import ctypes
+import sys
 
 import numpy as np
 import torch
@@ -208,15 +209,15 @@ class Mapper:
                 discarded_index = torch.randint(0, pool_sample_count, (discard_count,), device=self.device)
                 filter_mask[true_indices[discarded_index]] = False
             keep = torch.nonzero(filter_mask).squeeze(1)   # one compaction index for every pool
-            self.coord_pool = self.coord_pool.index_select(0, keep)
-            self.global_coord_pool = self.global_coord_pool.index_select(0, keep)
-            self.sdf_label_pool = self.sdf_label_pool.index_select(0, keep)
-            self.weight_pool = self.weight_pool.index_select(0, keep)
-            self.time_pool = self.time_pool.index_select(0, keep)
+            self.coord_pool = self._pool_compact("coord", self.coord_pool, keep)
+            self.global_coord_pool = self._pool_compact("global_coord", self.global_coord_pool, keep)
+            self.sdf_label_pool = self._pool_compact("sdf_label", self.sdf_label_pool, keep)
+            self.weight_pool = self._pool_compact("weight", self.weight_pool, keep)
+            self.time_pool = self._pool_compact("time", self.time_pool, keep)
             if sem_label is not None:
-                self.sem_label_pool = self.sem_label_pool.index_select(0, keep)
+                self.sem_label_pool = self._pool_compact("sem", self.sem_label_pool, keep)
             if color_label is not None:
-                self.color_pool = self.color_pool.index_select(0, keep)
+                self.color_pool = self._pool_compact("color", self.color_pool, keep)
             cur_sample_filter_mask = filter_mask[-self.cur_sample_count:]
             self.cur_sample_count = int(cur_sample_filter_mask.sum().item())
             self.pool_sample_count = int(filter_mask.sum().item())
@@ -237,9 +238,19 @@ class Mapper:
             self.train_less = bool(getattr(c, "adaptive_mode", False) and
                                    new_sample_count / max(self.cur_sample_count, 1) < c.new_sample_ratio_thre)
 
+    def _pool_rows_hint(self, m):
+        """Rows a pool buffer is first sized for: the window filter keeps at most pool_capacity
+        samples and up to pool_filter_freq frames of m samples arrive between two filters, so
+        buffers of this size never grow in steady state (a few hundred MB of HBM per pool)."""
+        c = getattr(self, "config", None)
+        if c is None:
+            return 0
+        return int(getattr(c, "pool_capacity", 0)) + int(getattr(c, "pool_filter_freq", 1)) * m * 5 // 4
+
     def _pool_append(self, name, cur, new):
-        """torch.cat((cur, new)) as a prefix view of a buffer grown by 1.5x when full; cur must
-        be the previous return value to be appended in place (anything else is copied once)."""
+        """torch.cat((cur, new)) as a prefix view of a buffer sized once for the steady-state pool
+        (grown by 1.5x if ever full); cur must be the previous return value to be appended in
+        place (anything else is copied once)."""
         bufs = self.__dict__.setdefault("_pool_bufs", {})
         buf, last = bufs.get(name, (None, -1))
         n, m = cur.shape[0], new.shape[0]
@@ -250,12 +261,36 @@ class Mapper:
                     and buf.shape[0] >= n + m and (n == 0 or cur.data_ptr() == buf.data_ptr())
                     and cur.is_contiguous())
         if not in_place:
-            nb = torch.empty((max(int((n + m) * 1.5), 1024),) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
+            rows = max(int((n + m) * 1.5), 1024, self._pool_rows_hint(m))
+            nb = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
             nb[:n] = cur
             buf = nb
         buf[n:n + m] = new
         bufs[name] = (buf, n + m)
         return buf[:n + m]
+
+    def _pool_compact(self, name, cur, keep):
+        """cur.index_select(0, keep) written into the pool's spare buffer (kept per pool and
+        swapped with the live one), so the window filter allocates nothing in steady state; the
+        result is the pool's new live prefix view, which _pool_append then extends in place."""
+        bufs = self.__dict__.setdefault("_pool_bufs", {})
+        spares = self.__dict__.setdefault("_pool_spare", {})
+        k = keep.shape[0]
+        spare = spares.pop(name, None)
+        # a spare still viewed from outside (a pool tensor kept by the caller: slices hold their
+        # base) is left alone; 2 = this local + getrefcount's argument
+        if (spare is None or sys.getrefcount(spare) > 2 or spare.dtype != cur.dtype
+                or spare.shape[1:] != cur.shape[1:] or spare.shape[0] < k or spare.device != cur.device):
+            live = bufs.get(name, (None, -1))[0]
+            rows = max(k, live.shape[0] if live is not None else 0)
+            spare = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=cur.dtype, device=cur.device)
+        out = spare[:k]
+        torch.index_select(cur, 0, keep, out=out)
+        old = bufs.get(name, (None, -1))[0]
+        if old is not None and old.data_ptr() != spare.data_ptr():
+            spares[name] = old          # the previous live buffer becomes the spare
+        bufs[name] = (spare, k)
+        return out
 
     def set_pool(self, coord, sdf_label, ts, weight=None, global_coord=None):
         """Install a training-sample pool (the output of Mapper.process_frame, utils/mapper.py:110-321)."""

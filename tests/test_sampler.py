@@ -185,3 +185,29 @@ def test_pool_append_prefix_view_copies():
     assert torch.equal(c, torch.cat((head, torch.full((4, 3), 7.0))))
     d = m._pool_append("y", torch.zeros(3, dtype=torch.float32), torch.ones(2, dtype=torch.float64))
     assert d.dtype == torch.float64
+
+
+def test_pool_compact_ping_pong_keeps_held_views():
+    """The window filter's compaction (_pool_compact) writes into the pool's spare buffer and
+    swaps; appends then continue in place; a pool tensor the caller still holds is never
+    overwritten (its buffer is not reused as a spare while viewed)."""
+    import torch
+    from pin_slam_amd.mapper import Mapper
+    m = Mapper.__new__(Mapper)
+    ref = torch.empty((0, 2))
+    pool = m._pool_append("p", torch.empty((0, 2)), torch.arange(40.).view(20, 2))
+    ref = torch.cat((ref, torch.arange(40.).view(20, 2)))
+    held = None
+    for it in range(6):
+        keep = torch.arange(0, pool.shape[0], 2 if it % 2 else 3)
+        if it == 2:
+            held, held_copy = pool, pool.clone()
+        pool = m._pool_compact("p", pool, keep)
+        ref = ref.index_select(0, keep)
+        assert torch.equal(pool, ref)
+        new = torch.full((7, 2), float(it))
+        before = pool.data_ptr()
+        pool = m._pool_append("p", pool, new)
+        ref = torch.cat((ref, new))
+        assert torch.equal(pool, ref) and pool.data_ptr() == before     # appended in place
+    assert torch.equal(held, held_copy)
