@@ -251,6 +251,8 @@ def tracker_leg(nm, dec, pts, args, dev, world, rank):
         out = step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if out[4].shape[0] < TRACKER_SRC // 2:   # a registration without valid points returns early: not the workload
+        print(f"WARNING: tracker leg has only {out[4].shape[0]} valid points", file=sys.stderr)
     return {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
             "queries_per_sec": TRACKER_SRC * steps / el, "ms_per_iter": el / steps * 1e3, "steps": steps,
             "valid_points": int(out[4].shape[0]), "scaling": "replicas", "map_fit_loss": fit_loss,

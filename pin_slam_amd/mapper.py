@@ -556,6 +556,10 @@ class Mapper:
                 _lib.call("pin_adam_step", _lib.ptr(pd), _lib.ptr(m_grad[off:off + k]), _lib.ptr(m_m[off:off + k]),
                           _lib.ptr(m_v[off:off + k]), k, ctypes.byref(st), s)
                 off += k
+            # the step wrote through raw pointers: bump the versions so views built on the
+            # parameters (the matrix-core operand image of mlp_view) are rebuilt before the next use
+            for p in mlp_params:
+                torch.autograd.graph.increment_version(p)
 
 
     # ---------------------------------------------------------------- autograd helpers

@@ -248,6 +248,31 @@ def test_fat_cache_sees_training_writes(dev):
             assert torch.equal(a, b)
 
 
+def test_decoder_image_sees_training_writes(dev):
+    """With the decoder training, Adam updates its parameters through raw pointers; the gradient
+    queries decode on the matrix cores from an operand image cached per parameter version, so a
+    query after mapping() must equal one through a fresh copy of the trained decoder."""
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    nm, dec, pts = surface_map(200, device=dev, buffer_size=1 << 22, query_backend="grid")
+    for p in dec.parameters():
+        p.requires_grad_(True)
+    q = surface_pool(pts, 5000, seed=3, device=dev)[0]
+    coord, label, ts = surface_pool(pts, 20000, seed=4, device=dev)
+    before = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True)
+    w0 = [p.detach().clone() for p in dec.parameters()]
+    mapper = P.Mapper(nm.config, None, nm, dec)
+    mapper.set_pool(coord, label, ts)
+    mapper.mapping(3)
+    assert max((p - w).abs().max().item() for p, w in zip(dec.parameters(), w0)) > 0   # the decoder moved
+    after = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True)
+    copy = P.Decoder(nm.config, 64, 1, 1)
+    copy.load_state_dict(dec.state_dict())
+    fresh = P.query_sdf(nm, copy, q, query_locally=True, want_grad=True)
+    assert not torch.equal(before[0], after[0])
+    torch.testing.assert_close(after[0], fresh[0], rtol=0, atol=0)
+    torch.testing.assert_close(after[1], fresh[1], rtol=0, atol=0)
+
+
 def test_fused_gather_path_matches_get_batch(dev):
     """mapping() with get_batch's gathers fused into pin_train_gather gives the same features,
     certainties and ts as mapping() through get_batch (same draws: the batch index is drawn by
