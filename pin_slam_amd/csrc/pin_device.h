@@ -60,6 +60,10 @@ __device__ __forceinline__ float dist2(float px, float py, float pz, float qx, f
     return (dx * dx + dy * dy) + dz * dz;
 }
 
+#ifndef PIN_TOPK_MED3
+#define PIN_TOPK_MED3 1   // 0: the two-select form of the distance update (experiment switch)
+#endif
+
 // Sorted (ascending) register list of the k nearest candidates.  Ties keep candidate
 // order (cell order), matching the stable sort of the CPU reference (:561-565).
 struct TopK {
@@ -71,15 +75,21 @@ struct TopK {
     }
     // Branch-free insertion (pure selects).  x = +inf is a no-op, so callers insert every
     // candidate unconditionally with rejected ones mapped to +inf.
+    // The distances take one v_med3 each: with d ascending, the selected value
+    // c[j] ? d[j] : (c[j-1] ? x : d[j-1]) is the median of (d[j-1], x, d[j]) (equal values are
+    // interchangeable, so ties change nothing); the payloads keep the two selects.
     __device__ __forceinline__ void insert(float x, int gi) {
         bool c[kK];
 #pragma unroll
         for (int j = 0; j < kK; ++j) c[j] = d[j] <= x;
 #pragma unroll
         for (int j = kK - 1; j > 0; --j) {
-            const float dj = c[j - 1] ? x : d[j - 1];
             const int gj = c[j - 1] ? gi : g[j - 1];
-            d[j] = c[j] ? d[j] : dj;
+#if PIN_TOPK_MED3
+            d[j] = __builtin_amdgcn_fmed3f(d[j - 1], x, d[j]);
+#else
+            d[j] = c[j] ? d[j] : (c[j - 1] ? x : d[j - 1]);
+#endif
             g[j] = c[j] ? g[j] : gj;
         }
         d[0] = c[0] ? d[0] : x;
