@@ -381,7 +381,10 @@ def process_frame_leg(args, dev, world, rank):
     cfg.pool_filter_freq = 10
     cfg.track_on = True
     nsteps = max(args.steps // 2, 10)
-    nw = 3
+    # warm-up frames cover one window filter: its first run allocates the caching allocator's
+    # blocks for the filter's pool-sized temporaries (~150 ms once on a 10M-sample pool), which is
+    # not the steady state the metric describes
+    nw = int(cfg.pool_filter_freq)
     T = nw + nsteps
     nm.local_map_radius = 50.0
     nm.diff_travel_dist_local = 250.0

@@ -51,18 +51,26 @@ def main():
     nm.update = timed("update", orig_update)
     mapper.sampler.sample = timed("sample", orig_sample)
     nm.query_certainty = timed("certainty", orig_cert)
+    for name in ("_pool_append", "_pool_compact", "_used_poses"):
+        setattr(mapper, name, timed(name, getattr(mapper, name)))
+    per_frame = []
     for k in range(T):
         if k == 5:
             acc.clear()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
         mapper.process_frame(frames[k], None, pose_t[k], k)
+        torch.cuda.synchronize()
+        per_frame.append((time.perf_counter() - tf) * 1e3)
     torch.cuda.synchronize()
     tot = time.perf_counter() - t0
     n = T - 5
     print(f"total {tot / n * 1e3:.3f} ms/frame")
     for k, v in acc.items():
-        print(f"  {k:10s} {v / n * 1e3:.3f} ms/frame")
+        print(f"  {k:14s} {v / n * 1e3:.3f} ms/frame")
+    print("per frame ms:", " ".join(f"{v:.2f}" for v in per_frame))
     print("pool", mapper.pool_sample_count)
 
 
