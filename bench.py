@@ -200,19 +200,26 @@ def nwf_leg(nm, dec, q, args, world):
     for _ in range(3):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    # median of 5 timed windows of K steps: the leg is a few ms long, and a one-off host stall
+    # (allocator / garbage collection) inside a single window would otherwise set its number
+    windows = []
+    for _ in range(5):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        windows.append(time.perf_counter() - t0)
+    el = statistics.median(windows)
     t = torch.tensor([el], dtype=torch.float64, device=q.device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t[0])
     return {"metric": "SDF+grad+std queries/sec, per-neighbour decoding", "value": q.shape[0] * args.steps * world / el,
             "unit": "queries/s", "ms_per_step": el / args.steps * 1e3, "scaling": "weak",
+            "windows_ms_per_step": [w / args.steps * 1e3 for w in windows],
             "config": {"workload": "configs[1] batch and map, weighted_first False (8 decoder evaluations per query)"}}
 
 
@@ -246,11 +253,15 @@ def tracker_leg(nm, dec, pts, args, dev, world, rank):
         step()
     torch.cuda.synchronize()
     steps = max(args.steps // 2, 5)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        out = step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    windows = []   # median of 5 timed windows (see nwf_leg)
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step()
+        torch.cuda.synchronize()
+        windows.append(time.perf_counter() - t0)
+    el = statistics.median(windows)
     if out[4].shape[0] < TRACKER_SRC // 2:   # a registration without valid points returns early: not the workload
         print(f"WARNING: tracker leg has only {out[4].shape[0]} valid points", file=sys.stderr)
     return {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
