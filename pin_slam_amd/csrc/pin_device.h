@@ -18,7 +18,7 @@
 #define PIN_NB_GROUP 4       // neighbours gathered per streaming group
 #endif
 #ifndef PIN_GRID_CHUNK
-#define PIN_GRID_CHUNK 4     // candidate records fetched per round trip (grid source; 4 measured best)
+#define PIN_GRID_CHUNK 8     // candidate records fetched per round trip (grid source; 8 measured best, see DESIGN)
 #endif
 
 namespace pin {
