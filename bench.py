@@ -331,6 +331,32 @@ def mesher_leg(nm, dec, pts, args, dev, world, rank):
                                    "z-slabs per rank (configs[4])"}}
 
 
+_FRAME_TIMING = ("each frame timed on its own (synchronised before and after; the frame's own host syncs "
+                 "already serialise it): median frame time x frames, max over ranks; the mean is reported "
+                 "beside it (one-off caching-allocator growth of the growing map / pool shows there)")
+
+
+def _frame_times(run, frames):
+    """Wall time of each call run(k), k in frames, each bracketed by device synchronisation."""
+    out = []
+    for k in frames:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(k)
+        torch.cuda.synchronize()
+        out.append(time.perf_counter() - t0)
+    return out
+
+
+def _frames_el(per_frame, nsteps, world, dev):
+    """(median frame time x nsteps, mean frame time), each the max over ranks."""
+    t = torch.tensor([statistics.median(per_frame) * nsteps, statistics.mean(per_frame)], dtype=torch.float64,
+                     device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1])
+
+
 def map_leg(args, dev, world, rank):
     """NeuralPoints.update per frame (voxel down-sample, hash probe +
     insert, reset_local_map over the whole map + local gathers) of a 131,072-point scan
@@ -355,17 +381,11 @@ def map_leg(args, dev, world, rank):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(nw, T):
-        nm.update(frames[k], sensors[k], None, k)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t[0])
+    per_frame = _frame_times(lambda k: nm.update(frames[k], sensors[k], None, k), range(nw, T))
+    el, mean = _frames_el(per_frame, nsteps, world, dev)
     res = {"metric": "map update frames/sec", "value": nsteps * world / el, "unit": "frames/s",
-           "points_per_sec": MAP_FRAME * nsteps * world / el, "ms_per_frame": el / nsteps * 1e3, "steps": nsteps,
+           "points_per_sec": MAP_FRAME * nsteps * world / el, "ms_per_frame": el / nsteps * 1e3,
+           "mean_ms_per_frame": mean * 1e3, "timing": _FRAME_TIMING, "steps": nsteps,
            "map_points_before": M0, "map_points_after": nm.count(), "local_points": nm.local_count(),
            "scaling": "replicas",
            "config": {"workload": "NeuralPoints.update (+ reset_local_map) of 131072-point scans into the 1M-point "
@@ -416,18 +436,12 @@ def process_frame_leg(args, dev, world, rank):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(nw, T):
-        mapper.process_frame(frames[k], None, pose_t[k], k)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t[0])
+    per_frame = _frame_times(lambda k: mapper.process_frame(frames[k], None, pose_t[k], k), range(nw, T))
+    el, mean = _frames_el(per_frame, nsteps, world, dev)
     res = {"metric": "mapper frames/sec (process_frame)", "value": nsteps * world / el, "unit": "frames/s",
            "samples_per_sec": FRAME_RAYS * mapper.ray_sample_count * nsteps * world / el,
-           "ms_per_frame": el / nsteps * 1e3, "steps": nsteps, "pool_samples": int(mapper.pool_sample_count),
+           "ms_per_frame": el / nsteps * 1e3, "mean_ms_per_frame": mean * 1e3, "timing": _FRAME_TIMING,
+           "steps": nsteps, "pool_samples": int(mapper.pool_sample_count),
            "map_points": nm.count(), "new_samples": int(mapper.new_idx.shape[0]), "scaling": "replicas",
            "config": {"workload": "Mapper.process_frame: 65536-ray frames, 7 samples/ray, into the 1M-point surface "
                                   "map (SURVEY.md 8f rank 4)"}}
