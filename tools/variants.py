@@ -30,15 +30,18 @@ def run(args):
         for lib in libs:
             env = dict(os.environ, PIN_LIB=os.path.join(OUT, lib))
             legs = [] if os.environ.get("VAR_MAPPER") else ["--no-mapper"]
+            legs += [] if os.environ.get("VAR_NWF") else ["--no-nwf-leg"]
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *legs, "--no-cpu-baseline",
-                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", "--no-nwf-leg", *args], env=env, capture_output=True, text=True,
-                               timeout=300)
+                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", *args],
+                               env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(lib, "FAILED", r.stderr[-2000:])
                 sys.exit(1)
             d = json.loads(r.stdout.strip().splitlines()[-1])
             print(f"rep{rep} {lib:24s} {d['value'] / 1e9:.3f} Gq/s  kernel {d['roofline']['kernel_ms'] * 1e3:.1f} us  order {d['roofline'].get('order_pass_ms', 0) * 1e3:.1f} us"
-                  + (f"  mapper {d['mapper']['value']:.1f} it/s" if "mapper" in d else ""), flush=True)
+                  + (f"  mapper {d['mapper']['value']:.1f} it/s" if "mapper" in d else "")
+                  + (f"  per-neighbour {d['per_neighbour']['value'] / 1e9:.3f} Gq/s" if "per_neighbour" in d else ""),
+                  flush=True)
 
 
 if __name__ == "__main__":
