@@ -344,11 +344,22 @@ typedef struct PinTrainCfg {
                                     PIN_TRAIN_DX (weighted_first, mlp->packed set, no decoder gradient):
                                     the forward decodes on the matrix cores and saves s dsdf/dx[0:8] in
                                     x[:, 0:8] instead of the input, and the backward applies it without
-                                    re-evaluating the decoder */
+                                    re-evaluating the decoder;
+                                    PIN_TRAIN_EIK: analytic-gradient eikonal (numerical_grad off,
+                                    mapper.py:481-482, get_gradient create_graph=True, tools.py:174-184):
+                                    n_stencil must be 0; the forward evaluates dsdf/dq of every batch row in
+                                    closed form, its loss weight_e * mean(|g| - 1)^2 and the coefficients of
+                                    its second derivative (st->eik_coef / eik_vec), and the backward adds
+                                    them to the feature / decoder gradients */
+    int64_t n_tail;              /* the last n_tail batch rows (and the stencil groups based on them) are
+                                    scaled by grad_scale_tail instead of grad_scale (slab sharding) */
+    float grad_scale_tail;
+    int32_t reserved;
 } PinTrainCfg;
 
 #define PIN_TRAIN_ROWS 1
 #define PIN_TRAIN_DX 2
+#define PIN_TRAIN_EIK 4
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
 typedef struct PinTrainState {
@@ -363,6 +374,13 @@ typedef struct PinTrainState {
     const float* sorted_rows;    /* [rows,4] the rows in processing order as {x, y, z, bits(row)}
                                     (pin_query_sort over the rows), may be NULL; takes precedence over
                                     order and saves the order -> coordinate dependent load */
+    const float* row_weight;     /* [n_main] BCE weight per batch row (loss_weight_on: |weight|,
+                                    mapper.py:514-516, loss.py:41-42), NULL = unweighted */
+    float* eik_coef;             /* PIN_TRAIN_EIK: [rows, nn_k] per slot, u . dw_j/dq with
+                                    u = dL_eik/dg (the neighbour weights' share of the second derivative) */
+    float* eik_vec;              /* PIN_TRAIN_EIK: weighted_first: [rows, 11] A^T u = sum_j (u . dw_j/dq) x_j
+                                    + (sum_j w_j) [0, u] (decoder-parameter term, written only when
+                                    the decoder trains); per-neighbour: [rows, 3] u */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */
@@ -386,11 +404,16 @@ int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, 
 /*
  * pin_train_gather -- Mapper.get_batch's gathers (utils/mapper.py:352-356) fused with the row
  * build: rows_out [rows,3] = every row of the iteration from coord_pool[index] (batch rows, then
- * the stencil of every decimation-th one), label_out [n_main] = label_pool[index] and, when
- * ts_pool is non-NULL, ts_out [n_main] = ts_pool[index].  index: [n_main] int64 pool rows.
+ * the stencil of every decimation-th one), label_out [n_main] = label_pool[index], when ts_pool is
+ * non-NULL ts_out [n_main] = ts_pool[index], and when weight_pool is non-NULL weight_out [n_main] =
+ * |weight_pool[index]| (mapper.py:514).  index: [n_main] int64 pool rows, each in [0, pool_rows):
+ * an index outside it is clamped to row 0 and raises bit 0 of *error (device int32, may be NULL;
+ * the caller zeroes it and reads it when it wants the check).
  */
-int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool, const int64_t* index,
-                     const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out, void* stream);
+int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool,
+                     const float* weight_pool, int64_t pool_rows, const int64_t* index, const PinTrainCfg* cfg,
+                     float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                     void* stream);
 
 /*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping

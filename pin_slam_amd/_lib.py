@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("PIN_LIB") or os.path.join(_HERE, "libpin_slam_amd.so"
 PIN_OK = 0
 PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
 PIN_TRAIN_DX = 2     # PinTrainCfg.flags: forward saves s dsdf/dx (matrix-core decoder), backward applies it
+PIN_TRAIN_EIK = 4    # PinTrainCfg.flags: analytic-gradient eikonal (double backward in closed form)
 PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 
@@ -76,12 +77,14 @@ MLP_PACK_BYTES = 8288
 
 class PinTrainCfg(ctypes.Structure):
     _fields_ = [("n_main", i64), ("n_stencil", i64), ("decimation", i32), ("nn_k", i32), ("weighted_first", i32),
-                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("flags", i32)]
+                ("eps", f32), ("sigma", f32), ("weight_e", f32), ("grad_scale", f32), ("flags", i32),
+                ("n_tail", i64), ("grad_scale_tail", f32), ("reserved", i32)]
 
 
 class PinTrainState(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
-                ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p), ("sorted_rows", c_void_p)]
+                ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p), ("sorted_rows", c_void_p),
+                ("row_weight", c_void_p), ("eik_coef", c_void_p), ("eik_vec", c_void_p)]
 
 
 class PinAdamStep(ctypes.Structure):
@@ -137,8 +140,8 @@ _SIGS = {
     "pin_query_feature_fwd_grid": [_P(PinGrid), _P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_rows": [c_void_p, _P(PinTrainCfg), c_void_p, c_void_p],
-    "pin_train_gather": [c_void_p, c_void_p, c_void_p, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p, c_void_p,
-                         c_void_p],
+    "pin_train_gather": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,

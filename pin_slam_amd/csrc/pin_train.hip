@@ -276,19 +276,26 @@ k_train_rows(const float* __restrict__ coord, PinTrainCfg c, float* __restrict__
 // the pool is read once per batch row
 __global__ void __launch_bounds__(kBlock)
 k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool, const int64_t* __restrict__ tpool,
-               const int64_t* __restrict__ index, PinTrainCfg c, float* __restrict__ rows, float* __restrict__ label,
-               int64_t* __restrict__ ts) {
+               const float* __restrict__ wpool, int64_t pool_rows, const int64_t* __restrict__ index, PinTrainCfg c,
+               float* __restrict__ rows, float* __restrict__ label, int64_t* __restrict__ ts,
+               float* __restrict__ weight, int* __restrict__ error) {
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main) return;
-    const int64_t i = index[r];
+    int64_t i = index[r];
+    if (i < 0 || i >= pool_rows) {   // never gather outside the pool: clamp and report
+        if (error) atomicOr(error, 1);
+        i = 0;
+    }
     const float qx = cpool[3 * i], qy = cpool[3 * i + 1], qz = cpool[3 * i + 2];
     const float lb = lpool[i];
     const int64_t tv = tpool ? tpool[i] : 0;
+    const float wv = wpool ? fabsf(wpool[i]) : 1.f;
     rows[3 * r] = qx;
     rows[3 * r + 1] = qy;
     rows[3 * r + 2] = qz;
     label[r] = lb;
     if (tpool) ts[r] = tv;
+    if (wpool) weight[r] = wv;
     if (c.n_stencil > 0 && r % c.decimation == 0 && r / c.decimation < c.n_stencil) {
         const int64_t k = r / c.decimation;
 #pragma unroll
@@ -307,16 +314,31 @@ k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool,
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
 
-// dL/dsdf of row r and its loss term (BCE rows: mean over N; stencil groups: weight_e * mean over N/dec)
+// loss / gradient factor of a batch row: grad_scale, or grad_scale_tail for the last n_tail rows
+__device__ __forceinline__ float main_row_scale(const PinTrainCfg& c, int64_t r) {
+    return r >= c.n_main - c.n_tail ? c.grad_scale_tail : c.grad_scale;
+}
+
+// the same for any row: a stencil row takes its group's base row (coord[k * decimation])
+__device__ __forceinline__ float row_scale(const PinTrainCfg& c, int64_t r) {
+    if (r < c.n_main) return main_row_scale(c, r);
+    const int64_t k = (r - c.n_main) % c.n_stencil;
+    return main_row_scale(c, k * c.decimation);
+}
+
+// dL/dsdf of row r and its loss term, unscaled (BCE rows: mean over N, weighted by the row's
+// |weight| under loss_weight_on, loss.py:40-47; stencil groups: weight_e * mean over N/dec)
 __device__ __forceinline__ float row_dsdf(const PinTrainCfg& c, const float* __restrict__ sdf,
-                                          const float* __restrict__ label, int64_t r, double& loss) {
+                                          const float* __restrict__ label, const float* __restrict__ rw, int64_t r,
+                                          double& loss) {
     loss = 0.0;
     if (r < c.n_main) {
         const float pz = sdf[r] / c.sigma;
         const float y = sigmoidf_(label[r] / c.sigma);
+        const float wr = rw ? rw[r] : 1.f;
         loss = (double)fmaxf(pz, 0.f) - (double)pz * y + log1p(exp(-fabs((double)pz)));
-        loss /= (double)c.n_main;
-        return (sigmoidf_(pz) - y) / ((float)c.n_main * c.sigma);
+        loss *= (double)wr / (double)c.n_main;
+        return wr * (sigmoidf_(pz) - y) / ((float)c.n_main * c.sigma);
     }
     const int64_t s = r - c.n_main;
     const int blk = (int)(s / c.n_stencil);
@@ -411,8 +433,9 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     const int nn_k = c.nn_k;
     const int wave = threadIdx.x >> 6;
     double loss = 0.0;
-    const float dsdf = live ? row_dsdf(c, st.sdf, label, row, loss) * c.grad_scale : 0.f;
-    loss *= (double)c.grad_scale;
+    const float rs = live ? row_scale(c, row) : 0.f;
+    const float dsdf = live ? row_dsdf(c, st.sdf, label, st.row_weight, row, loss) * rs : 0.f;
+    loss *= (double)rs;
     const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
     float* mw = MLP_GRAD ? mlds[wave] : nullptr;
     if (WF && MF) {
@@ -617,15 +640,20 @@ int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, 
     return launch_status();
 }
 
-int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool, const int64_t* index,
-                     const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out, void* stream) {
+int pin_train_gather(const float* coord_pool, const float* label_pool, const int64_t* ts_pool,
+                     const float* weight_pool, int64_t pool_rows, const int64_t* index, const PinTrainCfg* cfg,
+                     float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                     void* stream) {
     if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
     if (cfg->n_stencil > 0 && (cfg->n_stencil - 1) * (int64_t)cfg->decimation >= cfg->n_main) return PIN_ERR_ARG;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
-    if (!coord_pool || !label_pool || !index || !rows_out || !label_out || (ts_pool && !ts_out)) return PIN_ERR_ARG;
+    if (!coord_pool || !label_pool || !index || !rows_out || !label_out || (ts_pool && !ts_out) ||
+        (weight_pool && !weight_out) || pool_rows < 1)
+        return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_train_gather, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream), coord_pool,
-                       label_pool, ts_pool, index, *cfg, rows_out, label_out, ts_out);
+                       label_pool, ts_pool, weight_pool, pool_rows, index, *cfg, rows_out, label_out, ts_out,
+                       weight_out, (int*)error);
     return launch_status();
 }
 

@@ -9,9 +9,16 @@
   classes, so every later ``from model.neural_points import NeuralPoints`` binds ours;
 * replaces ``utils.data_sampler.DataSampler`` (and the name ``utils.mapper`` imported) by the
   fused sampler, and ``deskewing`` in ``utils.tools`` / ``dataset.slam_dataset`` by the kernel;
-* transplants the hot-path methods onto the reference's ``utils.mapper.Mapper`` (incl.
-  ``process_frame``), ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, keeping
-  everything else of those classes (bundle adjustment, marching cubes, ...) as it is.
+* transplants the hot-path methods onto the reference's ``utils.mapper.Mapper``,
+  ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, together with every helper
+  method they call, keeping everything else of those classes as it is.  The reference's own
+  control flow (``Tracker.tracking``, ``Mapper.get_batch`` / ``sdf`` /
+  ``get_numerical_gradient``, bundle adjustment, ...) stays: it calls the transplanted
+  hot-path methods and the drop-in ``NeuralPoints`` / ``Decoder``.
+
+``tests/test_integration.py`` imports the real reference modules, runs ``install()``, builds the
+reference ``Mapper`` / ``Tracker`` / ``Mesher`` and checks that every ``self.<name>`` a
+transplanted method reads resolves on those instances.
 
 It returns the list of (module, attribute) pairs it patched.  Nothing in the package calls it.
 """
@@ -25,9 +32,15 @@ from .neural_points import NeuralPoints
 from .tools import deskewing
 from .tracker import Tracker
 
-MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "sdf", "get_numerical_gradient",
-                  "process_frame", "dynamic_filter", "_used_poses", "_pool_append")
-TRACKER_METHODS = ("tracking", "query_source_points", "registration_step")
+# utils/mapper.py:Mapper -- the fused training loop (mapping :425-593), the device-resident data
+# pool (process_frame :110-321, dynamic_filter :79-108) and the helpers those call
+MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "_pools_fusable", "_slab_exact",
+                  "_slab_partition", "_batch_index", "_randint", "_new_sample_mode", "process_frame", "dynamic_filter",
+                  "_used_poses", "_pool_append", "_pool_compact", "_pool_rows_hint", "set_pool")
+# utils/tracker.py:Tracker -- the fused query and the registration step; the reference's
+# tracking() loop (:39-174) drives them unchanged
+TRACKER_METHODS = ("query_source_points", "registration_step")
+# utils/mesher.py:Mesher -- grid queries (:41-136) and marching cubes (:310-337)
 MESHER_METHODS = ("query_points", "mc_mesh")
 
 

@@ -21,7 +21,7 @@ mapping(): nothing inside an iteration reads them.
 drop-in query_feature for callers outside the fused loop.
 """
 import ctypes
-import sys
+import warnings
 
 import numpy as np
 import torch
@@ -30,6 +30,16 @@ import torch.distributed as dist
 from . import _lib
 from .data_sampler import DataSampler
 from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
+
+
+def _viewed_elsewhere(t: torch.Tensor) -> bool:
+    """True if any tensor other than ``t`` shares t's storage (a view kept by a caller).  A view
+    holds its base's storage through its TensorImpl, not through a Python reference to ``t``, so
+    the storage's use count is what sees it: 1 for t itself + 1 for the temporary handle here."""
+    use_count = getattr(torch._C, "_storage_Use_Count", None)
+    if use_count is None:
+        return True     # cannot tell: never reuse
+    return use_count(t.untyped_storage()._cdata) > 2
 
 
 def transform_batch_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -61,6 +71,9 @@ class _TrainBuffers:
             self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_GRAD_SIZE * 4,), dtype=torch.uint8,
                                          device=device)
             self.loss = torch.zeros((1,), dtype=torch.float64, device=device)
+            self.wrow = torch.empty((rows,), dtype=torch.float32, device=device)
+            # bit 0: a batch index outside the pool (pin_train_gather clamps it); read per mapping()
+            self.gather_error = torch.zeros((1,), dtype=torch.int32, device=device)
             self.key = key
         return self
 
@@ -206,7 +219,7 @@ class Mapper:
             pool_sample_count = true_indices.shape[0]
             if pool_sample_count > c.pool_capacity:
                 discard_count = pool_sample_count - int(c.pool_capacity)
-                discarded_index = torch.randint(0, pool_sample_count, (discard_count,), device=self.device)
+                discarded_index = self._randint(pool_sample_count, discard_count)
                 filter_mask[true_indices[discarded_index]] = False
             keep = torch.nonzero(filter_mask).squeeze(1)   # one compaction index for every pool
             self.coord_pool = self._pool_compact("coord", self.coord_pool, keep)
@@ -272,14 +285,15 @@ class Mapper:
     def _pool_compact(self, name, cur, keep):
         """cur.index_select(0, keep) written into the pool's spare buffer (kept per pool and
         swapped with the live one), so the window filter allocates nothing in steady state; the
-        result is the pool's new live prefix view, which _pool_append then extends in place."""
+        result is the pool's new live prefix view, which _pool_append then extends in place.
+        The spare is the live buffer of the previous filter: a pool tensor a caller kept from
+        before that filter is a view of it, so a spare whose storage has any view besides the
+        spare itself is left alone (a fresh buffer is taken) and the kept tensor stays valid."""
         bufs = self.__dict__.setdefault("_pool_bufs", {})
         spares = self.__dict__.setdefault("_pool_spare", {})
         k = keep.shape[0]
         spare = spares.pop(name, None)
-        # a spare still viewed from outside (a pool tensor kept by the caller: slices hold their
-        # base) is left alone; 2 = this local + getrefcount's argument
-        if (spare is None or sys.getrefcount(spare) > 2 or spare.dtype != cur.dtype
+        if (spare is None or _viewed_elsewhere(spare) or spare.dtype != cur.dtype
                 or spare.shape[1:] != cur.shape[1:] or spare.shape[0] < k or spare.device != cur.device):
             live = bufs.get(name, (None, -1))[0]
             rows = max(k, live.shape[0] if live is not None else 0)
@@ -301,26 +315,38 @@ class Mapper:
         self.weight_pool = torch.ones_like(sdf_label) if weight is None else weight
         self.pool_sample_count = int(sdf_label.shape[0])
 
+    def _randint(self, high, n):
+        """torch.randint(0, high, (n,)) on the mapper's device: every draw of get_batch goes through
+        here (tests replay the reference's recorded draws by replacing it on the instance)."""
+        return torch.randint(0, high, (n,), device=self.device)
+
+    def _new_sample_mode(self):
+        """get_batch draws half new / half history samples (utils/mapper.py:325)."""
+        stop = getattr(self.dataset, "stop_status", False) if self.dataset is not None else False
+        return (int(getattr(self.config, "bs_new_sample", 0)) > 0 and self.new_idx is not None
+                and not self.lose_track and not stop)
+
     def _batch_index(self, rows=None, new_idx=None):
         """The pool rows of one batch: get_batch's sampling (utils/mapper.py:323-350), same draws.
         rows / new_idx: the pool rows (and new samples) to draw from instead of the whole pool
-        (a spatially sharded rank's slab)."""
-        stop = getattr(self.dataset, "stop_status", False) if self.dataset is not None else False
+        (a spatially sharded rank's slab).  self._n_new_rows: rows at the end that are new samples."""
         bs = int(self.config.bs)
         bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
         count = self.pool_sample_count if rows is None else rows.shape[0]
         pick = (lambda i: i) if rows is None else (lambda i: rows[i])   # noqa: E731
         new_idx = self.new_idx if rows is None else new_idx
-        if bs_new_sample > 0 and new_idx is not None and not self.lose_track and not stop:
+        self._n_new_rows = 0
+        if self._new_sample_mode() and new_idx is not None:
             new_idx_count = new_idx.shape[0]
             if new_idx_count > 0:
                 bs_new = min(new_idx_count, bs_new_sample)
                 bs_history = bs - bs_new
-                index_history = pick(torch.randint(0, count, (bs_history,), device=self.device))
-                index_new_batch = torch.randint(0, new_idx_count, (bs_new,), device=self.device)
+                index_history = pick(self._randint(count, bs_history))
+                index_new_batch = self._randint(new_idx_count, bs_new)
+                self._n_new_rows = bs_new
                 return torch.cat((index_history, new_idx[index_new_batch]), dim=0)
-            return pick(torch.randint(0, count, (bs,), device=self.device))
-        return pick(torch.randint(0, count, (bs,), device=self.device))
+            return pick(self._randint(count, bs))
+        return pick(self._randint(count, bs))
 
     def get_batch(self, global_coord=False):
         """utils/mapper.py:323-361."""
@@ -348,8 +374,6 @@ class Mapper:
                 raise NotImplementedError("analytic-gradient eikonal (double backward) is not on the fused path")
             if getattr(c, "ekional_add_to", "all") != "all":
                 raise NotImplementedError("fused mapping implements ekional_add_to 'all'")
-        if getattr(c, "loss_weight_on", False):
-            raise NotImplementedError("fused mapping implements the unweighted BCE (loss_weight_on False)")
         # utils/tools.py:89-116: the fused step is Adam without L2 (the reference's defaults)
         if not getattr(c, "opt_adam", True):
             raise NotImplementedError("fused mapping implements the Adam optimizer only (opt_adam True)")
@@ -391,28 +415,24 @@ class Mapper:
         # get_batch's gathers fused into the row build (pin_train_gather) when the pools allow it;
         # a get_batch replaced on the instance (tests, callers) is honoured
         fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
-        part = slab_rows = slab_new = None
-        if world > 1 and getattr(self, "shard", "dense") == "space" and self._slab_exact():
-            if not fused:
-                raise NotImplementedError("shard='space' samples device pools through the fused batch path")
-            from .sharding import SlabPartition, query_reach
-            group = getattr(self, "group", None)
-            part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group)
-            mask = part.sample_mask(self.global_coord_pool[: self.pool_sample_count])
-            slab_rows = torch.nonzero(mask).flatten()
-            if self.new_idx is not None:
-                slab_new = self.new_idx[mask[self.new_idx]]
-            self._partition = part
+        part, slab_rows, slab_new, scales = self._slab_partition(world, fused)
         for _ in range(iter_count):
             if fused:
-                index = self._batch_index() if part is None else self._batch_index(slab_rows, slab_new)
-                self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad, world,
-                                index=index, reduce=part is None)
+                if part is None:
+                    index = self._batch_index()
+                    self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
+                                    world, index=index, weight=self.weight_pool)
+                else:
+                    index = self._batch_index(slab_rows, slab_new)
+                    scale_h, scale_n = scales(int(index.shape[0]) - self._n_new_rows, self._n_new_rows)
+                    self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
+                                    world, index=index, reduce=False, scale=scale_h, n_tail=self._n_new_rows,
+                                    scale_tail=scale_n, weight=self.weight_pool)
             else:
                 coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
                 if self.ba_done_flag:
                     coord = transform_batch_torch(coord, self.used_poses[ts])
-                self.train_step(coord, sdf_label, ts, f_grad, m_grad, world)
+                self.train_step(coord, sdf_label, ts, f_grad, m_grad, world, weight=weight)
             if part is not None:
                 part.exchange_gradients(f_grad)                   # halo rows -> owners
                 if m_grad is not None:
@@ -431,6 +451,62 @@ class Mapper:
             sync_side_effects(cert_delta, nm.local_point_ts_update, getattr(self, "group", None))
             cert.copy_(cert_before + cert_delta)
         nm.assign_local_to_global()
+        if fused and iter_count > 0 and int(self._buf.gather_error.item()):
+            self._buf.gather_error.zero_()
+            raise IndexError("mapping(): a batch index fell outside the sample pool")
+
+    def _slab_partition(self, world, fused):
+        """shard="space" set-up of one mapping() call: (partition, the slab's pool rows, the slab's
+        new samples, scales) -- or four Nones for the dense path.  Every rank takes the same
+        decision (the flags are all-reduced before any rank enters the partition's collectives):
+        maps with global2local-quirk records, or a slab without pool samples, fall back to dense.
+
+        scales(bs_hist_r, bs_new_r) -> (history-row scale, new-row scale).  A rank draws its batch
+        from its slab only, so its rows are weighted to keep the union an unbiased estimate of the
+        reference's single-process batch (utils/mapper.py:323-350: bs_hist rows uniform over the
+        pool of N samples, bs_new rows uniform over the n new samples):
+            scale_h = (bs_hist / bs_hist_r) (N_r / N),   scale_n = (bs_new / bs_new_r) (n_r / n)
+        with N_r / n_r the slab's pool / new sample counts (a flat 1/W would over-weight the samples
+        of sparsely sampled slabs).  A stencil group takes the scale of its base row."""
+        if world <= 1 or getattr(self, "shard", "dense") != "space":
+            return None, None, None, None
+        group = getattr(self, "group", None)
+        nm = self.neural_points
+        dev = nm.local_neural_points.device
+        flag = torch.tensor([0.0 if self._slab_exact() else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if float(flag[0]) > 0:
+            warnings.warn("shard='space': the local map has global2local-quirk records (PIN_RECORD_UNFAITHFUL); "
+                          "this mapping() call uses the dense gradient all-reduce")
+            return None, None, None, None
+        if not fused:
+            raise NotImplementedError("shard='space' samples device pools through the fused batch path")
+        from .sharding import SlabPartition, query_reach
+        part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group)
+        mask = part.sample_mask(self.global_coord_pool[: self.pool_sample_count])
+        slab_rows = torch.nonzero(mask).flatten()
+        slab_new = self.new_idx[mask[self.new_idx]] if self.new_idx is not None else None
+        n_r = 0 if slab_new is None else int(slab_new.numel())
+        cnt = torch.tensor([float(slab_rows.numel()), float(n_r), 1.0 if slab_rows.numel() == 0 else 0.0],
+                           dtype=torch.float64, device=dev)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+        if float(cnt[2]) > 0:
+            warnings.warn("shard='space': a slab holds no pool samples; this mapping() call uses the dense "
+                          "gradient all-reduce")
+            return None, None, None, None
+        N, n = float(cnt[0]), float(cnt[1])
+        N_r = float(slab_rows.numel())
+        bs = int(self.config.bs)
+        bs_new = min(int(n), int(getattr(self.config, "bs_new_sample", 0))) if (self._new_sample_mode() and n > 0) \
+            else 0
+        bs_hist = bs - bs_new
+
+        def scales(bs_hist_r, bs_new_r):
+            sh = (bs_hist / bs_hist_r) * (N_r / N) if bs_hist_r > 0 else 0.0
+            sn = (bs_new / bs_new_r) * (n_r / n) if bs_new_r > 0 else 0.0
+            return sh, sn
+        self._partition = part
+        return part, slab_rows, slab_new, scales
 
     def _slab_exact(self):
         """Slab sharding is exact when every candidate a query can reach is a local point at its own
@@ -447,19 +523,28 @@ class Mapper:
                 and l is not None and l.dtype == torch.float32 and l.is_contiguous()
                 and (t is None or (t.dtype == torch.int64 and t.is_contiguous())))
 
-    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None, reduce=True):
+    def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None, reduce=True,
+                   scale=None, n_tail=0, scale_tail=0.0, weight=None):
         """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
-        SUM all-reduced over the group when world > 1.  Returns the device loss tensor.
+        SUM all-reduced over the group when world > 1 and reduce.  Returns the device loss tensor.
         index ([N] int64): coord / sdf_label / ts are then the sample pools and the batch is their
-        rows `index` (get_batch's gathers done by pin_train_gather)."""
+        rows `index` (get_batch's gathers done by pin_train_gather).
+        scale: loss / gradient factor (default 1/world); the last n_tail batch rows (and the
+        stencil groups based on them) take scale_tail instead (slab sharding's new-sample rows).
+        weight: the batch rows' sample weights (the weight pool with index), used as |weight| by the
+        BCE term when loss_weight_on (utils/mapper.py:514-516)."""
         c = self.config
         nm = self.neural_points
+        weighted = bool(getattr(c, "loss_weight_on", False)) and weight is not None
+        wrow = None
         if index is None:
             q = coord.detach().to(torch.float32).contiguous()
             _lib.require_device(q)
             label = sdf_label.detach().to(torch.float32).contiguous()
             ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
             n = q.shape[0]
+            if weighted:
+                wrow = weight.detach().to(device=q.device, dtype=torch.float32).abs().contiguous()
         else:
             q = coord
             _lib.require_device(q)
@@ -479,7 +564,8 @@ class Mapper:
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
                                sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
-                               grad_scale=float(np.float32(1.0 / world)), flags=0)
+                               grad_scale=float(np.float32(1.0 / world if scale is None else scale)), flags=0,
+                               n_tail=int(n_tail), grad_scale_tail=float(np.float32(scale_tail)))
         hv, pv = nm._views("local", True)
         s = _lib.stream()
         grid = nm.backend() == "grid"
@@ -492,8 +578,11 @@ class Mapper:
         else:
             label = b.label
             ts64 = b.ts if ts is not None else None
-            _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(index),
-                      ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), s)
+            wpool = weight.detach().to(torch.float32).contiguous() if weighted else None
+            wrow = b.wrow if weighted else None
+            _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
+                      int(q.shape[0]), _lib.ptr(index), ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label),
+                      _lib.ptr(ts64), _lib.ptr(wrow), _lib.ptr(b.gather_error), s)
         cfg.flags = _lib.PIN_TRAIN_ROWS
         q = rows_xyz
         sorted_rows = None
@@ -504,7 +593,8 @@ class Mapper:
         st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                 ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
-                                order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None)
+                                order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None,
+                                row_weight=_lib.ptr(wrow))
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK

@@ -664,6 +664,13 @@ class NeuralPoints(nn.Module):
             value = -self.point_certainties
         sample_idx = voxel_down_sample_min_value(self.neural_points, res, value)
         n = sample_idx.shape[0]
+        # the reference's key divides by value.max() (utils/tools.py:459): at 0 the quantised values
+        # are inf / NaN and the wrapped amin keys yield indices outside the map, which its
+        # neural_points[sample_idx] rejects with IndexError (neural_points.py:397 / :407); the
+        # kernels must never gather them
+        if n and int(sample_idx.max()) >= self.count():
+            raise IndexError("recreate_hash: the down-sample returned an index outside the map "
+                             "(value.max() == 0 in voxel_down_sample_min_value, as in the reference)")
         if kept_points:
             pts = self.neural_points.contiguous()
             _lib.call("pin_hash_assign", _lib.ptr(pts), _lib.ptr(sample_idx), n, float(np.float32(res)),

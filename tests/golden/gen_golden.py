@@ -773,6 +773,402 @@ def gen_process_frame_case(name="process_frame", seed=15, frames=4):
     print(name, "pool", mapper.pool_sample_count, "points", npm.count(), "new", mapper.new_idx.shape[0])
 
 
+# ------------------------------------------------------------------ sequence fixtures (configs[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+from tests.replay import ReplayDraws, mapping_pool  # noqa: E402
+
+
+class _ReplayTorch:
+    """Stands in for ``torch`` inside utils/mapper.py and utils/data_sampler.py: the random draws
+    come from a shared ReplayDraws stream (tests/replay.py), everything else is torch."""
+
+    def __init__(self, replay):
+        self.replay = replay
+
+    def __getattr__(self, name):
+        return getattr(torch, name)
+
+    @staticmethod
+    def _numel(size):
+        if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)):
+            size = tuple(size[0])
+        return size, int(np.prod(size))
+
+    def randint(self, low, high, size, **kw):
+        assert low == 0
+        size, n = self._numel((size,))
+        return torch.from_numpy(self.replay.randint(int(high), n)).reshape(size)
+
+    def rand(self, *size, **kw):
+        size, n = self._numel(size)
+        return torch.from_numpy(self.replay.rand(n)).reshape(size)
+
+    def randn(self, *size, **kw):
+        size, n = self._numel(size)
+        return torch.from_numpy(self.replay.randn(n)).reshape(size)
+
+
+SLAM_SENSOR_H = 1.73
+Q_SCALE = 512.0   # sensor-frame points stored as int16 multiples of 2^-9 m (|coord| < 64 m)
+
+
+def street_scene(rng):
+    """Boxes (buildings, cars, a wall) and vertical cylinders (poles / trunks) on a ground plane,
+    in the frame of the first sensor pose (ground at z = -1.73)."""
+    g = -SLAM_SENSOR_H
+    boxes = []
+    x = -40.0
+    while x < 70.0:       # two rows of buildings along the street
+        w = rng.uniform(6.0, 14.0)
+        for side in (-1.0, 1.0):
+            y0 = side * rng.uniform(9.0, 12.0)
+            d = rng.uniform(6.0, 12.0)
+            ylo, yhi = (y0, y0 + d) if side > 0 else (y0 - d, y0)
+            boxes.append((x, x + w, ylo, yhi, g, g + rng.uniform(5.0, 16.0)))
+        x += w + rng.uniform(2.0, 6.0)
+    for _ in range(10):   # parked cars
+        cx = rng.uniform(-30.0, 60.0)
+        cy = rng.choice([-1.0, 1.0]) * rng.uniform(4.5, 6.5)
+        boxes.append((cx, cx + 4.2, cy - 0.9, cy + 0.9, g, g + 1.5))
+    boxes.append((75.0, 76.0, -30.0, 30.0, g, g + 4.0))    # a wall across the street's end
+    cyls = [(rng.uniform(-30.0, 60.0), rng.choice([-1.0, 1.0]) * rng.uniform(3.2, 7.5), rng.uniform(0.15, 0.45),
+             g, g + rng.uniform(3.0, 8.0)) for _ in range(24)]
+    return np.asarray(boxes), np.asarray(cyls), g
+
+
+def lidar_scan(pose, scene, rng, beams=64, cols=1024, noise=0.01):
+    """A 64-beam spinning lidar at `pose` (4x4, f64) ray-cast against the scene; returns the hits in
+    the sensor frame, ranges in [3, 59.5] m (so the reference's crop_frame is a no-op), quantised
+    to multiples of 2^-9 m (int16 storage, exact in float32)."""
+    boxes, cyls, ground = scene
+    el = np.deg2rad(np.linspace(-24.8, 2.0, beams))
+    az = np.linspace(-np.pi, np.pi, cols, endpoint=False)
+    E, A = np.meshgrid(el, az, indexing="ij")
+    ds = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], -1).reshape(-1, 3)
+    R, o = pose[:3, :3], pose[:3, 3]
+    d = ds @ R.T
+    t = np.full(d.shape[0], np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tg = (ground - o[2]) / d[:, 2]
+        t = np.where((d[:, 2] < 0) & (tg > 0), np.minimum(t, tg), t)
+        for (x0, x1, y0, y1, z0, z1) in boxes:
+            lo = (np.array([x0, y0, z0]) - o) / d
+            hi = (np.array([x1, y1, z1]) - o) / d
+            tn = np.minimum(lo, hi).max(1)
+            tf = np.maximum(lo, hi).min(1)
+            hit = (tn <= tf) & (tn > 0)
+            t = np.where(hit, np.minimum(t, tn), t)
+        for (cx, cy, r, z0, z1) in cyls:
+            px, py = o[0] - cx, o[1] - cy
+            a = d[:, 0] ** 2 + d[:, 1] ** 2
+            b = 2 * (px * d[:, 0] + py * d[:, 1])
+            cc = px * px + py * py - r * r
+            disc = b * b - 4 * a * cc
+            tc = (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a)
+            zc = o[2] + tc * d[:, 2]
+            hit = (disc > 0) & (tc > 0) & (zc > z0) & (zc < z1)
+            t = np.where(hit, np.minimum(t, tc), t)
+    t = t + rng.normal(0.0, noise, t.shape)
+    keep = np.isfinite(t) & (t > 3.0) & (t < 59.5)
+    p = ds[keep] * t[keep, None]
+    q = np.round(p * Q_SCALE)
+    assert np.abs(q).max() < 32767
+    return q.astype(np.int16)
+
+
+def slam_poses(frames):
+    """Sensor poses in the first pose's frame: accelerating along the street (0.22 m in the first
+    frame, ~1.6 m per frame by frame 11: the first guess is the identity, later ones the
+    constant-velocity model, off by the 0.14 m/frame^2 acceleration), a slow yaw and sway."""
+    out = []
+    for k in range(frames):
+        yaw = np.deg2rad(0.6 * k + 0.15 * np.sin(0.9 * k))
+        T = np.eye(4)
+        T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
+        T[:3, 3] = [0.15 * k + 0.07 * k * k, 0.08 * np.sin(0.7 * k), 0.01 * k]
+        out.append(T)
+    return out
+
+
+def slam_config():
+    """config/lidar_slam/run_demo.yaml (the reference's sanity-test config, README.md:148-160) on
+    the CPU: deskew off (the synthetic scans carry no point times and roma is absent) and the
+    decoder frozen after frame 6 so both mapper paths (trainable / frozen decoder) run."""
+    c = Config()
+    c.load(os.path.join(REF, "config/lidar_slam/run_demo.yaml"))
+    c.device = "cpu"
+    c.silence = True
+    c.deskew = False
+    c.freeze_after_frame = 6
+    return c
+
+
+def config_scalars(c):
+    out = {}
+    for k, v in vars(c).items():
+        if k in ("device", "dtype") or k.startswith("_"):
+            continue
+        if isinstance(v, bool) or isinstance(v, (int, float, str)):
+            out[k] = v
+    out["track_on"] = bool(c.track_on)
+    return out
+
+
+def gen_slam_sequence(name="slam_seq", frames=12, seed=21, replay_seed=2024):
+    """The sequence with 8 torch threads, saved; then again with 1 thread, whose differences (only
+    the reduction order changes) are kept as the reference's own spread (keys spread_*)."""
+    import math
+    rec = _slam_sequence_run(name, frames, seed, replay_seed, 8)
+    t1 = _slam_sequence_run(name + "[1 thread]", frames, seed, replay_seed, 1)
+    dts, drs = [], []
+    for A, B in zip(rec["hist_pose"], t1["hist_pose"]):
+        dts.append(float(np.linalg.norm(A[:3, 3] - B[:3, 3])))
+        c = (np.trace(A[:3, :3].T @ B[:3, :3]) - 1.0) / 2.0
+        drs.append(math.degrees(math.acos(min(1.0, max(-1.0, c)))))
+    rec["spread_pose_dt"] = np.asarray(dts)
+    rec["spread_pose_dr"] = np.asarray(drs)
+    for key in ("f0_surface_sdf", "end_surface_sdf"):
+        rec["spread_abs_" + key] = np.abs(rec[key] - t1[key]).astype(np.float32)
+        rec["t1_mean_abs_" + key] = np.float64(np.abs(t1[key]).mean())
+    for key in ("map_count", "local_count", "pool", "new"):
+        a, b = rec["hist_" + key].astype(np.float64), t1["hist_" + key].astype(np.float64)
+        rec["spread_rel_" + key] = np.abs(a - b) / np.maximum(a, 1.0)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(name, "saved; 1- vs 8-thread spread: pose", max(dts), "m", max(drs), "deg;",
+          {k: float(np.max(v)) for k, v in rec.items() if k.startswith("spread_rel")},
+          "surface sdf |diff| median", float(np.median(rec["spread_abs_end_surface_sdf"])),
+          "mean |sdf| 8t", float(np.abs(rec["end_surface_sdf"]).mean()), "1t", float(rec["t1_mean_abs_end_surface_sdf"]))
+
+
+def _slam_sequence_run(name, frames, seed, replay_seed, threads):
+    """BASELINE configs[0] (the plumbing run): the reference's pin_slam.py frame loop
+    (pin_slam.py:96-257 -- read/preprocess, tracking, travel distance, process_frame, freeze,
+    mapping(iters)) on a synthetic 64-beam street sequence, with every random draw of the mapper
+    and sampler taken from a ReplayDraws stream, then the end-of-run merge + prune
+    (pin_slam.py:366-367).  Records per-frame poses and map / pool sizes, the features and
+    decoder after frame 0's 15 x 40-iteration mapping() call, and the SDF of the final map at
+    probe points."""
+    import json
+    import dataset.slam_dataset as rds_mod
+    import utils.data_sampler as rds
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(seed)
+    scene = street_scene(rng)
+    poses = slam_poses(frames)
+    scans = [lidar_scan(T, scene, rng) for T in poses]
+    # surface probes: scan points put in the world by the TRUE poses (2,000 per frame), and 5,000
+    # points of frame 0 (its sensor frame is the world frame)
+    prng = np.random.default_rng(seed + 1)
+    surf = []
+    for k in range(frames):
+        q = scans[k][prng.integers(0, scans[k].shape[0], 2000)].astype(np.float64) / Q_SCALE
+        surf.append(q @ poses[k][:3, :3].T + poses[k][:3, 3])
+    surf = np.concatenate(surf).astype(np.float32)
+    surf0 = (scans[0][prng.integers(0, scans[0].shape[0], 5000)].astype(np.float32) / np.float32(Q_SCALE))
+    cfg = slam_config()
+    replay = ReplayDraws(replay_seed)
+    rt = _ReplayTorch(replay)
+    saved = (rds.torch, rmapper.torch)
+    rds.torch = rt
+    rmapper.torch = rt
+    rds_mod.get_time = time.time
+    try:
+        torch.manual_seed(42)
+        geo_mlp = Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1)
+        rec = {"dec_init_" + k: v for k, v in dec_params(geo_mlp).items()}
+        npm = NeuralPoints(cfg)
+        ds = types.SimpleNamespace(config=cfg, silence=True, dtype=cfg.dtype, device="cpu", gt_pose_provided=False,
+                                   odom_poses=[], pgo_poses=None, gt_poses=None, travel_dist=[], processed_frame=0,
+                                   lose_track=False, consecutive_lose_track_frame=0, last_pose_ref=np.eye(4),
+                                   last_odom_tran=np.eye(4), cur_pose_ref=np.eye(4), stop_count=0, stop_status=False,
+                                   cur_point_cloud_torch=None, cur_point_ts_torch=None, cur_sem_labels_torch=None,
+                                   cur_source_points=None, cur_source_normals=None, cur_source_colors=None)
+        preprocess = types.MethodType(rds_mod.SLAMDataset.preprocess_frame, ds)
+        update_odom = types.MethodType(rds_mod.SLAMDataset.update_odom_pose, ds)
+        tracker = rtracker.Tracker(cfg, npm, geo_mlp, None, None)
+        mapper = rmapper.Mapper(cfg, ds, npm, geo_mlp, None, None)
+        hist = {k: [] for k in ("pose", "valid", "n_cloud", "n_source", "map_count", "local_count", "pool", "new",
+                                "iters", "draws_after")}
+        for frame_id in range(frames):
+            t0 = time.time()
+            used = ds.processed_frame
+            # dataset.read_frame (slam_dataset.py:199-229) without a pose file: identity pose
+            ds.cur_pose_ref = np.eye(4)
+            ds.cur_pose_torch = torch.tensor(ds.cur_pose_ref, dtype=cfg.dtype)
+            ds.cur_point_cloud_torch = torch.from_numpy(scans[frame_id].astype(np.float32) / np.float32(Q_SCALE))
+            ds.cur_point_ts_torch = None
+            preprocess(frame_id)
+            valid = True
+            if used > 0:
+                cur_pose_torch, _, _, valid = tracker.tracking(ds.cur_source_points, ds.cur_pose_guess_torch,
+                                                               ds.cur_source_colors, ds.cur_source_normals,
+                                                               vis_result=False)
+                ds.lose_track = not valid
+                mapper.lose_track = not valid
+                update_odom(cur_pose_torch)
+            npm.travel_dist = torch.tensor(np.array(ds.travel_dist), dtype=cfg.dtype)
+            if not mapper.lose_track and not ds.stop_status:
+                mapper.process_frame(ds.cur_point_cloud_torch, ds.cur_sem_labels_torch, ds.cur_pose_torch, used, False)
+            else:
+                npm.reset_local_map(ds.cur_pose_torch[:3, 3], None, used)
+            iters = cfg.iters * cfg.init_iter_ratio if used == 0 else cfg.iters
+            if used == cfg.freeze_after_frame:
+                rtools.freeze_decoders(geo_mlp, None, None, cfg)
+            hist["map_count"].append(npm.count())
+            hist["local_count"].append(npm.local_count())
+            hist["pool"].append(int(mapper.pool_sample_count))
+            hist["new"].append(int(mapper.new_idx.shape[0]) if mapper.new_idx is not None else -1)
+            if used % cfg.mapping_freq_frame == 0:
+                mapper.mapping(iters)
+            hist["iters"].append(iters)
+            hist["draws_after"].append(replay.calls)
+            hist["pose"].append(np.asarray(ds.cur_pose_ref, dtype=np.float64))
+            hist["valid"].append(bool(valid))
+            hist["n_cloud"].append(int(ds.cur_point_cloud_torch.shape[0]))
+            hist["n_source"].append(int(ds.cur_source_points.shape[0]) if used > 0 else 0)
+            if used == 0:   # the map after frame 0's 15 x 40-iteration mapping(): SDF on the surface
+                f0 = run_query(npm, geo_mlp, cfg, surf0, query_locally=False)
+                rec.update(f0_surface_sdf=f0["sdf"], f0_surface_nn=f0["nn_counts"])
+            ds.processed_frame += 1
+            err = np.linalg.norm(np.asarray(ds.cur_pose_ref)[:3, 3] - poses[frame_id][:3, 3])
+            print(f"{name} frame {frame_id}: valid {valid} |dt| vs truth {err:.4f} m, map {npm.count()}, "
+                  f"local {npm.local_count()}, pool {mapper.pool_sample_count}, {time.time() - t0:.1f} s", flush=True)
+        # end-of-loop map, then pin_slam.py:366-367 (merge + prune)
+        end = run_query(npm, geo_mlp, cfg, surf, query_locally=False)
+        rec.update(end_surface_sdf=end["sdf"], end_surface_nn=end["nn_counts"], end_surface_grad=end["grad"],
+                   end_map_count=np.int64(npm.count()))
+        try:
+            npm.recreate_hash(None, None, False, False)
+        except IndexError as e:
+            # voxel_down_sample_min_value_torch divides by value.max(): with every certainty >= 0
+            # and one at 0 that is 0 / 0 and x / 0, the amin keys wrap and the merge indexes out
+            # of range (utils/tools.py:459, model/neural_points.py:407) -- the reference's own
+            # behaviour, recorded as such
+            print(name, "recreate_hash raised", e)
+            rec["merged_raises"] = np.bool_(True)
+        else:
+            npm.prune_map(cfg.max_prune_certainty)
+            merged = run_query(npm, geo_mlp, cfg, surf, query_locally=False)
+            rec.update(merged_surface_sdf=merged["sdf"], merged_map_count=np.int64(npm.count()),
+                       merged_raises=np.bool_(False))
+    finally:
+        rds.torch, rmapper.torch = saved
+    for k in range(frames):
+        rec[f"f{k}_scan"] = scans[k]
+    rec["truth_poses"] = np.stack(poses)
+    rec.update(surface_probes=surf, f0_surface_probes=surf0)
+    rec["config_json"] = np.asarray(json.dumps(config_scalars(cfg)))
+    rec.update(replay_seed=np.int64(replay_seed), frames=np.int64(frames), q_scale=np.float64(Q_SCALE),
+               torch_threads=np.int64(threads))
+    for k, v in hist.items():
+        rec["hist_" + k] = np.asarray(v)
+    torch.set_num_threads(8)
+    return rec
+
+
+def gen_mapping_call(name, cfg_kwargs, frozen, iters=15, pool_n=100000, n_side=100, seed=31, pool_seed=77,
+                     replay_seed=505, **cfg_over):
+    """One whole Mapper.mapping(iters) call (utils/mapper.py:425-593) of the reference's own Mapper:
+    fresh Adam, iters iterations of get_batch (history + new samples, draws from a ReplayDraws
+    stream) / query / loss / backward / step, then assign_local_to_global.  Records the first
+    step's gradients and the global features, certainties, ts and decoder after the call, run with
+    8 torch threads; the same call with 1 thread gives the reference's own run-to-run spread (only
+    the reduction order changes), kept as the norm / max of the difference (keys spread_*)."""
+    rec = _mapping_call(cfg_kwargs, frozen, iters, pool_n, n_side, seed, pool_seed, replay_seed, cfg_over, 8)
+    t1 = _mapping_call(cfg_kwargs, frozen, iters, pool_n, n_side, seed, pool_seed, replay_seed, cfg_over, 1)
+    for k in ("it0_feat_grad", "it0_grad_W1", "it0_grad_b1", "it0_grad_W2", "it0_grad_b2", "global_features_after",
+              "after_W1", "after_b1", "after_W2", "after_b2"):
+        if k in t1:   # the spread as the norm of the difference (and its largest element)
+            diff = (t1[k].astype(np.float64) - rec[k].astype(np.float64)).ravel()
+            rec["spread_norm_" + k] = np.float64(np.linalg.norm(diff))
+            rec["spread_max_" + k] = np.float64(np.abs(diff).max())
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    d = np.abs(rec["global_features_after"] - t1["global_features_after"])
+    print(name, "L=", rec["L"], "require_gradient", rec["require_gradient"], "1- vs 8-thread features: max",
+          float(d.max()), "off > 1e-3", float((d > 1e-3).mean()))
+
+
+def _mapping_call(cfg_kwargs, frozen, iters, pool_n, n_side, seed, pool_seed, replay_seed, cfg_over, threads):
+    torch.set_num_threads(threads)
+    cfg = make_config(**cfg_kwargs)
+    for k, v in cfg_over.items():
+        setattr(cfg, k, v)
+    npm, _ = build_map(cfg, n_side, seed)
+    npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
+    dec = decoder(cfg)
+    if frozen:
+        rtools.freeze_model(dec)
+    rec = dict(nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
+               num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha),
+               iters=np.int64(iters), frozen=np.bool_(frozen), pool_n=np.int64(pool_n), pool_seed=np.int64(pool_seed),
+               replay_seed=np.int64(replay_seed), bs=np.int64(cfg.bs), bs_new_sample=np.int64(cfg.bs_new_sample))
+    rec["config_json"] = np.asarray(__import__("json").dumps(config_scalars(cfg)))
+    rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
+    rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
+    P = npm.local_neural_points.numpy()
+    coord, label, ts, weight = mapping_pool(P, pool_n, pool_seed)
+    ds = types.SimpleNamespace(stop_status=False)
+    mapper = rmapper.Mapper(cfg, ds, npm, dec, None, None)
+    mapper.global_coord_pool = torch.from_numpy(coord)
+    mapper.coord_pool = mapper.global_coord_pool
+    mapper.sdf_label_pool = torch.from_numpy(label)
+    mapper.time_pool = torch.from_numpy(ts)
+    mapper.weight_pool = torch.from_numpy(weight)
+    mapper.sem_label_pool = mapper.color_pool = mapper.normal_label_pool = None
+    mapper.pool_sample_count = pool_n
+    mapper.new_idx = torch.arange(pool_n - pool_n // 10, pool_n)
+    mapper.used_poses = torch.eye(4, dtype=torch.float64).repeat(10, 1, 1)
+    saved = rmapper.torch, rmapper.setup_optimizer
+    first = {}
+
+    def recording_setup(*a, **kw):
+        # the first step's gradients: the double backward of the analytic eikonal in one iteration,
+        # before the (chaotic, see the tests) iteration-to-iteration amplification
+        opt = saved[1](*a, **kw)
+        step = opt.step
+
+        def rec_step(*sa, **skw):
+            if not first:
+                first["feat"] = npm.local_geo_features.grad.detach().numpy().copy()
+                for k, p in zip(["W1", "b1", "W2", "b2"], dec.parameters()):
+                    if p.grad is not None:
+                        first[k] = p.grad.detach().numpy().copy()
+            return step(*sa, **skw)
+        opt.step = rec_step
+        return opt
+    rmapper.torch = _ReplayTorch(ReplayDraws(replay_seed))
+    rmapper.setup_optimizer = recording_setup
+    try:
+        t0 = time.time()
+        mapper.mapping(iters)
+    finally:
+        rmapper.torch, rmapper.setup_optimizer = saved
+    rec["it0_feat_grad"] = first["feat"]
+    for k in ["W1", "b1", "W2", "b2"]:
+        if k in first:
+            rec["it0_grad_" + k] = first[k]
+    rec["global_features_after"] = npm.geo_features.detach().numpy().copy()
+    rec["global_cert_after"] = npm.point_certainties.numpy().copy()
+    rec["global_ts_update_after"] = npm.point_ts_update.numpy().copy()
+    rec.update({f"after_{k}": v for k, v in dec_params(dec).items()})
+    rec["L"] = np.int64(npm.local_count())
+    rec["require_gradient"] = np.bool_(mapper.require_gradient)
+    torch.set_num_threads(8)
+    return rec
+
+
+def gen_mapping_calls():
+    gen_mapping_call("mapping_wf", dict(weighted_first=True), frozen=False)
+    gen_mapping_call("mapping_wf_frozen", dict(weighted_first=True), frozen=True)
+    gen_mapping_call("mapping_nwf_weighted", dict(weighted_first=False, nn_k=6), frozen=False, loss_weight_on=True)
+    # analytic-gradient eikonal (numerical_grad off: get_gradient(create_graph=True), a double
+    # backward, utils/mapper.py:50-54,481-482), the run_livox.yaml neural-point settings
+    livox = dict(voxel=0.15, alpha=0.5, nn_k=8, weighted_first=False)
+    gen_mapping_call("mapping_eik_livox", livox, frozen=False, n_side=140, numerical_grad=False, loss_weight_on=True,
+                     sigma_sigmoid_m=0.08)
+    gen_mapping_call("mapping_eik_wf", dict(weighted_first=True), frozen=False, numerical_grad=False)
+
+
 def gen_neighborhoods():
     cfg = make_config()
     npm = NeuralPoints(cfg)
@@ -797,7 +1193,9 @@ def main(only=None):
                                      gen_sampler_case("sampler_dropoff", 14, behind_dropoff_on=True, surface_sample_n=4,
                                                       free_front_n=3, free_behind_n=2, free_sample_end_dist_m=1.5,
                                                       dist_weight_on=False, surface_sample_range_m=0.3)),
-                 "process_frame": lambda: gen_process_frame_case()}
+                 "process_frame": lambda: gen_process_frame_case(),
+                 "slam_seq": lambda: gen_slam_sequence(),
+                 "mapping_calls": lambda: gen_mapping_calls()}
         for name in only:
             cases[name]()
         return

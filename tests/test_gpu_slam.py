@@ -1,0 +1,207 @@
+"""BASELINE configs[0], the plumbing run: the reference's pin_slam.py frame loop (:96-257) over a
+12-frame synthetic 64-beam street sequence (64K points per scan), replayed through
+pin_slam_amd's classes and compared with the reference's own run of the same loop
+(tests/golden/slam_seq.npz, written by tests/golden/gen_golden.py gen_slam_sequence with the
+reference's Tracker / Mapper / NeuralPoints / DataSampler and its dataset bookkeeping methods).
+
+Both runs take every random draw of the sampler and of get_batch from the same ReplayDraws
+stream (tests/replay.py), in the reference's call order, so they differ only by floating-point
+summation order.  The loop is chaotic in that difference: the reference run twice, with 1 and with
+8 torch threads (only its reduction order changes), ends frame 0's 15 x 40-iteration mapping()
+with different decoders (|dW1| up to 1.7) and features, yet poses within ~2 cm / 0.03 deg and
+the same surface.  That spread is stored in the fixture (spread_*) and the tolerances below are
+stated against it -- element-wise feature parity after hundreds of iterations is not a property
+the reference has.  (A single 15-iteration mapping() call is pinned element-wise in
+tests/test_gpu_mapper.py::test_whole_mapping_call_fixture.)
+
+Tolerances, checked per frame:
+  * preprocessed cloud / source point counts, tracking validity, draw-stream position: exact;
+  * pose within max(5 cm, 3 x spread) and max(0.1 deg, 3 x spread) of the reference's estimate,
+    and within 5 cm of the ground truth;
+  * neural-point / local-map counts within max(1 %, 3 x spread), pool size within 0.1 %, new
+    samples within max(15 %, 3 x spread) (they follow the certainty threshold);
+  * the map's SDF on the surface (scan points placed by the TRUE poses) after frame 0 and at the
+    end: mean |SDF| at most 1.25 x the reference's + 1 mm, and median |ours - reference| at most
+    3 x the median 1- vs 8-thread spread + 1 mm;
+  * the end-of-run merge (recreate_hash(kept_points=False), pin_slam.py:366) raises where the
+    reference's does, and otherwise leaves a map of the same size within 1 %.
+"""
+import json
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import pin_slam_amd as P
+from pin_slam_amd.neural_points import voxel_down_sample
+from tests.replay import ReplayDraws
+
+pytestmark = pytest.mark.gpu
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return "cuda"
+
+
+class DatasetReplay:
+    """The pose / travel-distance bookkeeping of dataset/slam_dataset.py:260-430 (preprocess_frame,
+    update_odom_pose) restated for the replay: read_frame without a pose file (identity),
+    voxel down-sample at vox_down_m, crop, constant-velocity guess, source cloud at
+    source_vox_down_m.  Dataset IO is out of scope; this is the test's harness."""
+
+    def __init__(self, cfg, dev):
+        self.config = cfg
+        self.dev = dev
+        self.odom_poses = []
+        self.travel_dist = []
+        self.processed_frame = 0
+        self.lose_track = False
+        self.last_pose_ref = np.eye(4)
+        self.last_odom_tran = np.eye(4)
+        self.cur_pose_ref = np.eye(4)
+        self.stop_count = 0
+        self.stop_status = False
+        self.gt_pose_provided = False
+
+    def read_and_preprocess(self, pts):
+        c = self.config
+        self.cur_pose_ref = np.eye(4)
+        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
+        cloud = pts[voxel_down_sample(pts, c.vox_down_m)]
+        dist = torch.norm(cloud, dim=1)
+        keep = (dist > c.min_range) & (dist < c.max_range) & (cloud[:, 2] > c.min_z) & (cloud[:, 2] < c.max_z)
+        self.cur_point_cloud_torch = cloud[keep]
+        self.cur_source_points = None
+        if self.processed_frame == 0:
+            self.odom_poses.append(self.cur_pose_ref)
+            self.travel_dist.append(0.0)
+            self.last_pose_ref = self.cur_pose_ref
+        else:
+            guess = self.last_pose_ref @ self.last_odom_tran if (c.uniform_motion_on and not self.lose_track) \
+                else self.last_pose_ref
+            self.cur_pose_guess_torch = torch.tensor(guess, dtype=torch.float64, device=self.dev)
+            src = self.cur_point_cloud_torch
+            self.cur_source_points = src[voxel_down_sample(src, c.source_vox_down_m)]
+
+    def update_odom_pose(self, cur_pose_torch):
+        c = self.config
+        self.cur_pose_torch = cur_pose_torch.detach()
+        self.cur_pose_ref = self.cur_pose_torch.cpu().numpy()
+        self.last_odom_tran = np.linalg.inv(self.last_pose_ref) @ self.cur_pose_ref
+        rot_close = np.all(np.abs(self.last_odom_tran[:3, :3] - np.eye(3)) < 1e-3)
+        tran_close = np.all(self.last_odom_tran[:3, 3] < c.voxel_size_m * 0.1)
+        self.stop_count = self.stop_count + 1 if (rot_close and tran_close) else 0
+        self.stop_status = self.stop_count > c.stop_frame_thre
+        self.odom_poses.append(self.odom_poses[-1] @ self.last_odom_tran)
+        step = np.linalg.norm(self.last_odom_tran[:3, 3])
+        if step > c.surface_sample_range_m * 40.0:
+            self.lose_track = True
+        self.travel_dist.append(self.travel_dist[-1] + step)
+        self.last_pose_ref = self.cur_pose_ref
+
+
+def _pose_err(a, b):
+    dt = float(np.linalg.norm(a[:3, 3] - b[:3, 3]))
+    c = (np.trace(a[:3, :3].T @ b[:3, :3]) - 1.0) / 2.0
+    return dt, math.degrees(math.acos(min(1.0, max(-1.0, c))))
+
+
+def _within(got, want, rel):
+    return abs(int(got) - int(want)) <= max(1, rel * abs(int(want)))
+
+
+def _surface_check(nm, dec, z, dev, probes_key, sdf_key):
+    """The map's SDF at surface points against the reference's (see the module docstring)."""
+    probes = torch.from_numpy(z[probes_key]).to(dev)
+    sdf, _, _, _, _ = P.query_sdf(nm, dec, probes, query_locally=False, want_grad=False, want_certainty=False)
+    got = sdf.cpu().numpy()
+    want = z[sdf_key]
+    mine, ref = float(np.abs(got).mean()), float(np.abs(want).mean())
+    diff = float(np.median(np.abs(got - want)))
+    spread = float(np.median(z["spread_abs_" + sdf_key]))
+    print(f"{sdf_key}: mean |SDF| ours {mine:.4f} m, reference {ref:.4f} m (1 thread "
+          f"{float(z['t1_mean_abs_' + sdf_key]):.4f}); median |ours - reference| {diff:.4f} m, reference spread "
+          f"{spread:.4f} m")
+    assert mine <= 1.25 * ref + 1e-3, (mine, ref)
+    assert diff <= 3 * spread + 1e-3, (diff, spread)
+
+
+def test_slam_sequence_matches_reference(golden, dev):
+    z = golden("slam_seq")
+    conf = json.loads(str(z["config_json"]))
+    cfg = P.Config(**conf)
+    cfg.device = dev
+    frames = int(z["frames"])
+    nm = P.NeuralPoints(cfg)
+    dec = P.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1)
+    with torch.no_grad():
+        dec.layers[0].weight.copy_(torch.as_tensor(z["dec_init_W1"]))
+        dec.layers[0].bias.copy_(torch.as_tensor(z["dec_init_b1"]))
+        dec.lout.weight.copy_(torch.as_tensor(z["dec_init_W2"]))
+        dec.lout.bias.copy_(torch.as_tensor(z["dec_init_b2"]))
+    dec.to(dev)
+    ds = DatasetReplay(cfg, dev)
+    tracker = P.Tracker(cfg, nm, dec)
+    mapper = P.Mapper(cfg, ds, nm, dec)
+    replay = ReplayDraws(int(z["replay_seed"]))
+    mapper._randint = lambda high, n: torch.from_numpy(replay.randint(high, n)).to(dev)
+    S, Ff, Fb = int(cfg.surface_sample_n), int(cfg.free_front_n), int(cfg.free_behind_n)
+    report = []
+    for k in range(frames):
+        pts = torch.from_numpy(z[f"f{k}_scan"].astype(np.float32) / np.float32(z["q_scale"])).to(dev)
+        used = ds.processed_frame
+        ds.read_and_preprocess(pts)
+        assert ds.cur_point_cloud_torch.shape[0] == int(z["hist_n_cloud"][k]), f"frame {k}: cloud size"
+        valid = True
+        if used > 0:
+            assert ds.cur_source_points.shape[0] == int(z["hist_n_source"][k]), f"frame {k}: source size"
+            T, _, _, valid = tracker.tracking(ds.cur_source_points, ds.cur_pose_guess_torch, None, None)
+            ds.lose_track = not valid
+            mapper.lose_track = not valid
+            ds.update_odom_pose(T)
+        assert bool(valid) == bool(z["hist_valid"][k]), f"frame {k}: tracking validity"
+        nm.travel_dist = torch.tensor(np.array(ds.travel_dist), dtype=torch.float32, device=dev)
+        n = ds.cur_point_cloud_torch.shape[0]
+        draws = (torch.from_numpy(replay.randn(n * S)), torch.from_numpy(replay.rand(n * Ff)),
+                 torch.from_numpy(replay.rand(n * Fb)))
+        if not mapper.lose_track and not ds.stop_status:
+            mapper.process_frame(ds.cur_point_cloud_torch, None, ds.cur_pose_torch, used, False, draws=draws)
+        else:
+            nm.reset_local_map(ds.cur_pose_torch[:3, 3], None, used)
+        iters = cfg.iters * cfg.init_iter_ratio if used == 0 else cfg.iters
+        if used == cfg.freeze_after_frame:
+            for p in dec.parameters():
+                p.requires_grad_(False)
+        counts = (nm.count(), nm.local_count(), int(mapper.pool_sample_count), int(mapper.new_idx.shape[0]))
+        want = tuple(int(z[f"hist_{n_}"][k]) for n_ in ("map_count", "local_count", "pool", "new"))
+        mapper.mapping(iters)
+        assert replay.calls == int(z["hist_draws_after"][k]), f"frame {k}: draw stream out of step"
+        dt, dr = _pose_err(ds.cur_pose_ref, z["hist_pose"][k])
+        dt_true, _ = _pose_err(ds.cur_pose_ref, z["truth_poses"][k])
+        report.append((k, round(dt, 4), round(dr, 4), round(dt_true, 4), counts, want))
+        tol_t = max(0.05, 3 * float(z["spread_pose_dt"][k]))
+        tol_r = max(0.1, 3 * float(z["spread_pose_dr"][k]))
+        assert dt <= tol_t and dr <= tol_r, f"frame {k}: pose differs from the reference by {dt:.4f} m / {dr:.4f} deg"
+        assert dt_true <= 0.05, f"frame {k}: pose {dt_true:.4f} m from the ground truth"
+        for name, g, w, rel in zip(("map_count", "local_count", "pool", "new"), counts, want, (0.01, 0.01, 0.001, 0.15)):
+            rel = max(rel, 3 * float(z[f"spread_rel_{name}"][k]))
+            assert _within(g, w, rel), f"frame {k}: {name} {g} vs reference {w}"
+        if used == 0:
+            _surface_check(nm, dec, z, dev, "f0_surface_probes", "f0_surface_sdf")
+        ds.processed_frame += 1
+    print("frame, |dt| m, |dR| deg vs reference, |dt| m vs truth, (map, local, pool, new) ours / reference")
+    for r in report:
+        print(*r)
+    # the map at the end of the loop
+    _surface_check(nm, dec, z, dev, "surface_probes", "end_surface_sdf")
+    # pin_slam.py:366-367: merge + prune
+    if bool(z["merged_raises"]):
+        with pytest.raises(IndexError):
+            nm.recreate_hash(None, None, False, False)
+    else:
+        nm.recreate_hash(None, None, False, False)
+        nm.prune_map(cfg.max_prune_certainty)
+        assert _within(nm.count(), int(z["merged_map_count"]), 0.01)
