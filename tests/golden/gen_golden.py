@@ -1082,6 +1082,7 @@ def gen_mapping_call(name, cfg_kwargs, frozen, iters=15, pool_n=100000, n_side=1
             diff = (t1[k].astype(np.float64) - rec[k].astype(np.float64)).ravel()
             rec["spread_norm_" + k] = np.float64(np.linalg.norm(diff))
             rec["spread_max_" + k] = np.float64(np.abs(diff).max())
+            rec["spread_frac1e4_" + k] = np.float64((np.abs(diff) > 1e-4).mean())
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
     d = np.abs(rec["global_features_after"] - t1["global_features_after"])
     print(name, "L=", rec["L"], "require_gradient", rec["require_gradient"], "1- vs 8-thread features: max",

@@ -360,6 +360,25 @@ def _norm(a):
     return float(np.linalg.norm(np.asarray(a, dtype=np.float64).ravel()))
 
 
+def _first_step_check(z, dev, backend, rel=1e-5):
+    """The call's first iteration (same draws): the feature gradient and, while the decoder
+    trains, the decoder gradients before Adam's first step against the reference's (it0_*),
+    within `rel` of their norm; no element of non-negligible size changes sign."""
+    nm, dec, mapper, _ = _mapping_call_setup(z, dev, backend)
+    fg = torch.zeros_like(nm.local_geo_features.data)
+    mg = None if bool(z["frozen"]) else torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+    mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, fg, mg, 1,
+                      index=mapper._batch_index(), weight=mapper.weight_pool)
+    g, w = _np(fg), z["it0_feat_grad"]
+    assert _norm(g - w) <= rel * _norm(w), ("feature gradient", _norm(g - w) / _norm(w))
+    big = np.abs(w) > 1e-4 * np.abs(w).max()
+    assert not (np.sign(g) != np.sign(w))[big].any()
+    if mg is not None:
+        for key, part in _split(_np(mg)).items():
+            ref = z[f"it0_grad_{key}"].reshape(-1)
+            assert _norm(part - ref) <= rel * _norm(ref), (key, _norm(part - ref) / _norm(ref))
+
+
 @pytest.mark.parametrize("case", ["mapping_wf", "mapping_wf_frozen", "mapping_nwf_weighted"])
 @pytest.mark.parametrize("backend", BACKENDS)
 def test_whole_mapping_call_fixture(golden, dev, backend, case):
@@ -367,12 +386,14 @@ def test_whole_mapping_call_fixture(golden, dev, backend, case):
     gen_mapping_call: fresh Adam, 15 x get_batch with history + new samples, BCE + numerical
     eikonal, backward, step; the draws replayed) -- trainable decoder, frozen decoder (the
     matrix-core PIN_TRAIN_DX path) and per-neighbour decoding with the weighted BCE
-    (loss_weight_on).  The reference's own 1- vs 8-thread spread over this call is at most 4e-4
-    per element (fixture keys spread_*).  Tolerance: the features after the call differ from the
-    reference's by at most 1e-4 on >= 99.9 % of elements (an element whose gradient is within float
-    noise of 0 takes Adam's +-lr step on either sign) and by ||.|| <= 1e-3 ||features moved||;
-    the trained decoder within 1e-4 relative."""
+    (loss_weight_on).  Tolerances: the first iteration's feature and decoder gradients within 1e-5 of
+    their norm (measured ~4e-6; the reference's own 1- vs 8-thread spread is ~1e-6); after the 15
+    iterations the features differ by more than 1e-4 on at most 0.5 % of the elements (fresh Adam
+    moves an element by +-lr on the sign of its gradient, so float noise at a near-zero gradient
+    is amplified -- measured 0.18 % per-neighbour, 0 weighted_first) and by ||.|| <= 1e-3
+    ||features moved||; the trained decoder within 1e-4 relative."""
     z = golden(case)
+    _first_step_check(z, dev, backend)
     nm, dec, mapper, replay = _mapping_call_setup(z, dev, backend)
     before = nm.geo_features.detach().cpu().numpy().copy()
     mapper.mapping(int(z["iters"]))
@@ -380,7 +401,7 @@ def test_whole_mapping_call_fixture(golden, dev, backend, case):
     got = _np(nm.geo_features)
     want = z["global_features_after"]
     off = np.abs(got - want) > 1e-4
-    assert off.mean() <= 1e-3, f"{off.sum()} of {off.size} feature elements off by > 1e-4"
+    assert off.mean() <= 5e-3, f"{off.sum()} of {off.size} feature elements off by > 1e-4"
     assert _norm(got - want) <= 1e-3 * _norm(want - before), (_norm(got - want), _norm(want - before))
     np.testing.assert_allclose(_np(nm.point_certainties), z["global_cert_after"], rtol=1e-5, atol=1e-4)
     np.testing.assert_array_equal(_np(nm.point_ts_update), z["global_ts_update_after"])
