@@ -354,6 +354,228 @@ __device__ __forceinline__ float row_dsdf(const PinTrainCfg& c, const float* __r
     return (blk & 1) ? -d_axis : d_axis;
 }
 
+// ------------------------------------------------------------------ analytic-gradient eikonal
+// numerical_grad off (utils/mapper.py:50-54, :481-482): g = dsdf/dq by autograd with
+// create_graph=True (utils/tools.py:174-184) and the eikonal term weight_e * mean((|g| - 1)^2)
+// over the batch, backpropagated through g -- a double backward.  Closed form, per row, with the
+// neighbour weights w_j = u_j / S, u_j = 1 / (d_j^2 + eps), c_j = du_j/dq / S = -2 u_j^2 (q - p_j) / S
+// (so dw_j/dq = c_j - w_j C, C = sum_j c_j):
+//   weighted_first:  g = J^T gx - (gx . x) C + Wr gx[8:],  J = sum_j x_j (x) c_j,  Wr = sum_j w_j R_j
+//   per-neighbour:   g = sum_j s_j c_j - sdf C + sum_j w_j R_j gx_j[8:]
+// (R_j the point's rotation after PGO, else I; gx = dsdf/dx of the decoder, which depends on the
+// features / parameters only through x and the ReLU mask, whose derivative is 0).  With
+// u = dL/dg = weight_e (|g| - 1) 2 g / (|g| N) (0 at |g| = 0, torch's norm backward) and
+// alpha_j = u . (c_j - w_j C):
+//   dL/df_j   = alpha_j gx[0:8]                         (weighted_first; gx_j[0:8] per-neighbour)
+//   dL/dtheta = through gx (W1, w2; b1 and b2 only through the mask):
+//     weighted_first: dL/dgx = r = J u - (u . C) x + [0, Wr^T u]
+//     per-neighbour:  dL/ds_j += alpha_j, dL/dgx_j[8:] = w_j R_j^T u
+// The forward writes alpha_j per slot (eik_coef) and r / u plus the row's eikonal loss (eik_vec);
+// the backward adds them to the BCE terms.
+constexpr int kEikWf = 20;    // eik_vec row, weighted_first: r[0..10], loss, gx[0..7]
+constexpr int kEikNwf = 4;    // eik_vec row, per-neighbour: u[0..2], loss
+
+template <bool WF, class Src>
+__device__ __forceinline__ void train_forward_eik_body(const Src& src, const PinPoints& p, const MlpW& m,
+                                                       const float* __restrict__ coord,
+                                                       const int64_t* __restrict__ ts, const PinTrainCfg& c,
+                                                       int64_t t, const PinTrainState& st, bool mlp_trains,
+                                                       int (&cid)[kK], float (&cw)[kK], int64_t& qts_out) {
+    int64_t r;
+    float qx, qy, qz;
+    if (st.sorted_rows) {
+        const float4 v = ((const float4*)st.sorted_rows)[t];
+        qx = v.x; qy = v.y; qz = v.z;
+        r = __float_as_int(v.w);
+    } else {
+        r = st.order ? st.order[t] : t;
+        row_coord(coord, c, r, qx, qy, qz);
+    }
+    TopK tk;
+    tk.init();
+    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    const int nn_k = c.nn_k;
+    float u[kK];
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        u[j] = (j < nn_k && tk.g[j] >= 0) ? 1.0f / (tk.d[j] + kIdwEps) : 0.f;
+        S = S + u[j];
+    }
+    const float invS = nn > 0 ? 1.f / S : 0.f;
+    qts_out = (ts && r < c.n_main) ? ts[r] : -1;
+    float x[kD], J[kD][3], C[3] = {0.f, 0.f, 0.f}, Wr[3][3], cc[kK][3];
+    float A[3] = {0.f, 0.f, 0.f}, G[3] = {0.f, 0.f, 0.f}, sdf = 0.f;
+#pragma unroll
+    for (int d = 0; d < kD; ++d) { x[d] = 0.f; J[d][0] = J[d][1] = J[d][2] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) Wr[a][0] = Wr[a][1] = Wr[a][2] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        const bool valid = u[j] > 0.f;
+        const float4 rc = src.record(tk.g[j]);
+        const int raw = __float_as_int(rc.w);
+        const int id = valid ? (raw & kIdMask) : -1;
+        const int64_t ii = id > 0 ? id : 0;
+        float4 f0, f1;
+        src.features(tk.g[j], ii, f0, f1);
+        const float pg[3] = {qx - rc.x, qy - rc.y, qz - rc.z};   // the distance's (global) position
+        float v0 = pg[0], v1 = pg[1], v2 = pg[2];
+        if (valid && (raw & PIN_RECORD_UNFAITHFUL)) {
+            v0 = qx - p.positions[3 * ii];
+            v1 = qy - p.positions[3 * ii + 1];
+            v2 = qz - p.positions[3 * ii + 2];
+        }
+        float4 qt = make_float4(1.f, 0.f, 0.f, 0.f);
+        if (p.after_pgo && valid) {
+            qt = ((const float4*)p.orientations)[ii];
+            quat_rotate_passive(qt, v0, v1, v2);
+        }
+        const float w = valid && nn > 0 ? u[j] / S : 0.f;
+        const float xj[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
+        if (j < nn_k) {
+            st.ids[t * nn_k + j] = id;
+            st.weights[t * nn_k + j] = w;
+        }
+        cid[j] = id;
+        cw[j] = w;
+        const float cu = valid ? -2.f * u[j] * u[j] * invS : 0.f;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            cc[j][a] = cu * pg[a];
+            C[a] += cc[j][a];
+        }
+        float R[3][3];
+        quat_rotmat(qt, R);
+        if (WF) {
+#pragma unroll
+            for (int d = 0; d < kD; ++d) {
+                const float xv = valid ? xj[d] : 0.f;
+                x[d] = x[d] + xv * w;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) J[d][a] = fmaf(xv, cc[j][a], J[d][a]);
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int b = 0; b < 3; ++b) Wr[a][b] = fmaf(w, R[a][b], Wr[a][b]);
+        } else {
+            float g3[3] = {0.f, 0.f, 0.f};
+            float sk = 0.f;
+            if (valid) sk = mlp_sdf<true, kF, 3>(m, xj, g3);
+            sdf = sdf + sk * w;   // sum_j sdf_j w_j (mapper.py:467-468)
+            float r0, r1, r2;
+            quat_rotate_active(qt, g3[0], g3[1], g3[2], r0, r1, r2);
+            G[0] = fmaf(w, r0, G[0]);
+            G[1] = fmaf(w, r1, G[1]);
+            G[2] = fmaf(w, r2, G[2]);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) A[a] = fmaf(sk, cc[j][a], A[a]);
+            if (j < nn_k) {
+                float* xo = st.x + (t * nn_k + j) * 3;   // neighbour vectors for the backward
+                xo[0] = v0;
+                xo[1] = v1;
+                xo[2] = v2;
+            }
+        }
+    }
+    float g[3] = {0.f, 0.f, 0.f};
+    float gx[kD];
+    if (WF) {
+        sdf = mlp_sdf<true, 0, kD>(m, x, gx);
+        if (nn > 0) {
+            float abar = 0.f;
+#pragma unroll
+            for (int d = 0; d < kD; ++d) abar = fmaf(gx[d], x[d], abar);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                float s = -abar * C[a];
+#pragma unroll
+                for (int d = 0; d < kD; ++d) s = fmaf(gx[d], J[d][a], s);
+#pragma unroll
+                for (int b = 0; b < 3; ++b) s = fmaf(Wr[a][b], gx[kF + b], s);
+                g[a] = s;
+            }
+        }
+    } else if (nn > 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) g[a] = A[a] - sdf * C[a] + G[a];
+    }
+    // eikonal term of this row: weight_e (|g| - 1)^2 / N, scaled like the row's BCE term
+    const float gn = sqrtf((g[0] * g[0] + g[1] * g[1]) + g[2] * g[2]);
+    const float rs = main_row_scale(c, r);
+    const float cu = gn > 0.f ? c.weight_e * rs * 2.f * (gn - 1.f) / (gn * (float)c.n_main) : 0.f;
+    const float uq[3] = {cu * g[0], cu * g[1], cu * g[2]};
+    const float loss = c.weight_e * rs * (gn - 1.f) * (gn - 1.f) / (float)c.n_main;
+    const float uC = (uq[0] * C[0] + uq[1] * C[1]) + uq[2] * C[2];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        if (j >= nn_k) break;
+        const float al = (uq[0] * cc[j][0] + uq[1] * cc[j][1]) + uq[2] * cc[j][2] - cw[j] * uC;
+        st.eik_coef[t * nn_k + j] = al;
+    }
+    if (WF) {
+        float* ev = st.eik_vec + t * kEikWf;
+#pragma unroll
+        for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+#pragma unroll
+        for (int d = 0; d < kF; ++d) ev[12 + d] = gx[d];
+        ev[11] = loss;
+        if (mlp_trains) {
+#pragma unroll
+            for (int d = 0; d < kD; ++d) {
+                float rv = -uC * x[d];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) rv = fmaf(J[d][a], uq[a], rv);
+                if (d >= kF) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) rv = fmaf(Wr[a][d - kF], uq[a], rv);
+                }
+                ev[d] = rv;
+            }
+        }
+    } else {
+        float* ev = st.eik_vec + t * kEikNwf;
+        ev[0] = uq[0];
+        ev[1] = uq[1];
+        ev[2] = uq[2];
+        ev[3] = loss;
+    }
+    st.sdf[r] = sdf;
+}
+
+template <bool WF, class Src>
+__device__ __forceinline__ void train_forward_eik_kernel_body(const Src& src, const PinPoints& p, const MlpW& mw,
+                                                              const float* coord, const int64_t* ts, PinTrainCfg c,
+                                                              PinTrainState st, bool mlp_trains) {
+    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    int cid[kK];
+    float cw[kK];
+    int64_t qts = -1;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
+    if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains, cid, cw, qts);
+    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
+}
+
+template <bool WF>
+__global__ void __launch_bounds__(kBlock)
+k_train_forward_eik_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
+                         const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st, int mlp_trains) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
+    train_forward_eik_kernel_body<WF>(HashSource(h, p), p, mw, coord, ts, c, st, mlp_trains != 0);
+}
+
+template <bool WF>
+__global__ void __launch_bounds__(kBlock)
+k_train_forward_eik_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
+                         const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st, int mlp_trains) {
+    __shared__ float s_mlp[kWSize];
+    const MlpW mw = stage_mlp(m, s_mlp);
+    train_forward_eik_kernel_body<WF>(GridSource<false, false>(g, p), p, mw, coord, ts, c, st, mlp_trains != 0);
+}
+
 // backward: one row per lane for the decoder; the row's k x 8 feature-gradient terms are staged
 // in LDS and scattered with 64 lanes covering 8 rows x 32 contiguous bytes per instruction.
 // Decoder-parameter gradients: wave shuffle sums -> per-block partials (fixed order, no
@@ -368,9 +590,12 @@ __device__ __forceinline__ float wave_sum_f(float v) {
 
 // decoder backward of one input row x with upstream dL/d(out) = so (already times sdf_scale):
 // gf += sum_c delta_c W1[c][0:8]; decoder-parameter terms summed over the wave into mw (lane 0)
-template <bool MLP_GRAD>
+// EXTRA (analytic eikonal): e = dL/d(gx) of the row (dsdf/dx through the mask-linear path,
+// gx = s W1^T (w2 o 1[pre > 0])): dW1[c][i] += s w2_c 1[pre_c > 0] e_i, dw2_c += s 1[pre_c > 0] W1[c] . e
+template <bool MLP_GRAD, bool EXTRA = false>
 __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)[kD], float so, float (&gf)[kF],
-                                                 float* __restrict__ mw, bool accumulate) {
+                                                 float* __restrict__ mw, bool accumulate,
+                                                 const float* __restrict__ e = nullptr) {
 #pragma unroll 2
     for (int cc = 0; cc < kH; ++cc) {
         float wr[kWRow];
@@ -385,10 +610,16 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
         for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
         if (MLP_GRAD) {
             float dw[kD + 2];
+            const float de = (EXTRA && on) ? m.sdf_scale * m.w[kWW2 + cc] : 0.f;
+            float ew = 0.f;
+            if (EXTRA) {
 #pragma unroll
-            for (int i = 0; i < kD; ++i) dw[i] = wave_sum_f(delta * x[i]);
+                for (int i = 0; i < kD; ++i) ew = fmaf(wr[i], e[i], ew);
+            }
+#pragma unroll
+            for (int i = 0; i < kD; ++i) dw[i] = wave_sum_f(EXTRA ? fmaf(de, e[i], delta * x[i]) : delta * x[i]);
             dw[kD] = wave_sum_f(delta);                       // b1
-            dw[kD + 1] = wave_sum_f(on ? so * pre : 0.f);     // W2
+            dw[kD + 1] = wave_sum_f(on ? (EXTRA ? fmaf(m.sdf_scale, ew, so * pre) : so * pre) : 0.f);   // W2
             if ((threadIdx.x & 63) == 0) {
 #pragma unroll
                 for (int i = 0; i < kD; ++i) mw[cc * kD + i] = (accumulate ? mw[cc * kD + i] : 0.f) + dw[i];
@@ -410,18 +641,20 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
 //     instead of the f32 decoder backward.
 // (A per-block LDS pre-sum of the scatter -- hash table on the feature row, 512 tile-sorted slots,
 // ~2.7 references per row -- measured slower: 683 vs 467 us, the LDS float atomics alone 470 us.)
-template <bool WF, bool MLP_GRAD, bool MF = false>
+template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false>
 __global__ void __launch_bounds__(kBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
                  double* __restrict__ loss_part) {
     static_assert(!MF || !MLP_GRAD, "matrix-core backward: frozen decoder");
+    static_assert(!EIK || !(WF && MF), "analytic eikonal, weighted_first: gx from the forward");
     constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
     constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
     __shared__ float gst[kBlock * kJ * kF];
     __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[kDecode ? kPkBytes / 16 : 1];
+    __shared__ float s_dsdf[WF && EIK ? kBlock : 1];
     const MlpW mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk)
                               : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
@@ -436,9 +669,25 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     const float rs = live ? row_scale(c, row) : 0.f;
     const float dsdf = live ? row_dsdf(c, st.sdf, label, st.row_weight, row, loss) * rs : 0.f;
     loss *= (double)rs;
+    if (EIK && live) loss += (double)st.eik_vec[r * (WF ? kEikWf : kEikNwf) + (WF ? 11 : 3)];   // (|g| - 1)^2 term
     const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
     float* mw = MLP_GRAD ? mlds[wave] : nullptr;
-    if (WF && MF) {
+    if (WF && EIK) {
+        // feature terms (w_j dsdf + alpha_j) gx[0:8] in the scatter; gx from the forward
+        const float* ev = st.eik_vec + (live ? r : 0) * kEikWf;
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? ev[12 + d] : 0.f;
+        s_dsdf[threadIdx.x] = dsdf;
+        if (MLP_GRAD) {
+            float x[kD], e[kD], gf[kF];
+#pragma unroll
+            for (int d = 0; d < kD; ++d) {
+                x[d] = live ? st.x[r * kD + d] : 0.f;
+                e[d] = live ? ev[d] : 0.f;
+            }
+            decoder_backward<MLP_GRAD, true>(mlpw, x, so, gf, mw, false, e);
+        }
+    } else if (WF && MF) {
 #pragma unroll
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? dsdf * st.x[r * kD + d] : 0.f;
     } else if (WF) {
@@ -452,11 +701,21 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
 #pragma unroll
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = gf[d];
     } else {
-        // per-neighbour decoder backward: dL/dsdf_j = dsdf * w_j (mapper.py:467-468)
+        // per-neighbour decoder backward: dL/dsdf_j = dsdf * w_j (mapper.py:467-468), + alpha_j
+        // with the analytic eikonal (whose gx_j[8:] path adds e = [0, w_j R_j^T u])
+        float uq[3] = {0.f, 0.f, 0.f};
+        if (EIK && live) {
+            const float* ev = st.eik_vec + r * kEikNwf;
+            uq[0] = ev[0];
+            uq[1] = ev[1];
+            uq[2] = ev[2];
+        }
         for (int j = 0; j < kK; ++j) {
             const int id = (live && j < nn_k) ? st.ids[r * nn_k + j] : -1;
             const bool ok = id >= 0;
             const float w = ok ? st.weights[r * nn_k + j] : 0.f;
+            const float al = (EIK && ok) ? st.eik_coef[r * nn_k + j] : 0.f;
+            const float coef = dsdf * w + al;        // dL/dsdf_j
             float x[kD];
             if (ok) {
                 const float4* fr = (const float4*)(p.features + (int64_t)id * kF);
@@ -477,10 +736,20 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                     float g8[kF];
                     mlp_sdf_mfma16<true, 0, kF>(mlpw, x, g8);
 #pragma unroll
-                    for (int d = 0; d < kF; ++d) gf[d] = (dsdf * w) * g8[d];
+                    for (int d = 0; d < kF; ++d) gf[d] = coef * g8[d];
                 }
+            } else if (EIK && MLP_GRAD) {
+                float e[kD];
+#pragma unroll
+                for (int d = 0; d < kF; ++d) e[d] = 0.f;
+                float u0 = uq[0], u1 = uq[1], u2 = uq[2];
+                if (ok && p.after_pgo) quat_rotate_passive(((const float4*)p.orientations)[id], u0, u1, u2);
+                e[kF] = w * u0;
+                e[kF + 1] = w * u1;
+                e[kF + 2] = w * u2;
+                decoder_backward<true, true>(mlpw, x, coef * mlpw.sdf_scale, gf, mw, j > 0, e);
             } else if (__any(ok) || MLP_GRAD) {
-                decoder_backward<MLP_GRAD>(mlpw, x, so * w, gf, mw, j > 0);
+                decoder_backward<MLP_GRAD>(mlpw, x, coef * mlpw.sdf_scale, gf, mw, j > 0);
             }
 #pragma unroll
             for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
@@ -511,12 +780,14 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     // scatter loop issues its atomics back to back instead of waiting on a load per element.
     __shared__ int s_ids[kBlock * kK];
     __shared__ float s_wt[WF ? kBlock * kK : 1];
+    __shared__ float s_al[WF && EIK ? kBlock * kK : 1];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int nrow_blk = (int)(nrows - row0 < kBlock ? nrows - row0 : kBlock);
     const int npair = nrow_blk * nn_k;
     for (int e = threadIdx.x; e < npair; e += kBlock) {
         s_ids[e] = st.ids[row0 * nn_k + e];
         if (WF) s_wt[e] = st.weights[row0 * nn_k + e];
+        if (WF && EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
     }
     __syncthreads();
     const int total = npair * kF;
@@ -526,7 +797,9 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         const int id = s_ids[rj];
         if (id < 0) continue;
         const int lr = rj / nn_k, j = rj - lr * nn_k;
-        const float g = WF ? s_wt[rj] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        float g;
+        if (WF && EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
+        else g = WF ? s_wt[rj] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
         atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }
@@ -666,8 +939,25 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     const bool dx = (cfg->flags & PIN_TRAIN_DX) != 0;
     if (dx && (!cfg->weighted_first || !mlp->packed)) return PIN_ERR_ARG;
+    const bool eik = (cfg->flags & PIN_TRAIN_EIK) != 0;
+    if (eik && (dx || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec)) return PIN_ERR_ARG;
     if (rows == 0) return PIN_OK;
     auto s = as_stream(stream);
+    if (eik) {
+        const bool wf = cfg->weighted_first != 0;
+        if (grid) {
+            if (wf) hipLaunchKernelGGL(k_train_forward_eik_grid<true>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts,
+                                       *mlp, coord, ts, *cfg, *st, 1);
+            else hipLaunchKernelGGL(k_train_forward_eik_grid<false>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts,
+                                    *mlp, coord, ts, *cfg, *st, 1);
+        } else {
+            if (wf) hipLaunchKernelGGL(k_train_forward_eik_hash<true>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts,
+                                       *mlp, coord, ts, *cfg, *st, 1);
+            else hipLaunchKernelGGL(k_train_forward_eik_hash<false>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts,
+                                    *mlp, coord, ts, *cfg, *st, 1);
+        }
+        return launch_status();
+    }
 #define PIN_LAUNCH_FWD(KERNEL, SRC)                                                                             \
     do {                                                                                                        \
         if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp, \
@@ -701,7 +991,19 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 #define PIN_LAUNCH_BWD(WF, MG)                                                                               \
     hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
-    if (cfg->flags & PIN_TRAIN_DX) {
+#define PIN_LAUNCH_BWD_EIK(WF, MG, MF)                                                                                 \
+    hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
+                       grad_features, mpart, lpart)
+    if (cfg->flags & PIN_TRAIN_EIK) {
+        if ((cfg->flags & PIN_TRAIN_DX) || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec) return PIN_ERR_ARG;
+        if (cfg->weighted_first) {
+            if (mlp_grad) PIN_LAUNCH_BWD_EIK(true, true, false); else PIN_LAUNCH_BWD_EIK(true, false, false);
+        } else {
+            if (mlp_grad) PIN_LAUNCH_BWD_EIK(false, true, false);
+            else if (mlp->packed) PIN_LAUNCH_BWD_EIK(false, false, true);
+            else PIN_LAUNCH_BWD_EIK(false, false, false);
+        }
+    } else if (cfg->flags & PIN_TRAIN_DX) {
         if (mlp_grad || !cfg->weighted_first) return PIN_ERR_UNSUPPORTED;
         hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st,
                            grad_features, mpart, lpart);
@@ -715,6 +1017,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         else PIN_LAUNCH_BWD(false, false);
     }
 #undef PIN_LAUNCH_BWD
+#undef PIN_LAUNCH_BWD_EIK
     if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
     if (mlp_grad)
         hipLaunchKernelGGL(k_mlp_grad_final, dim3((kMlpGrad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, mpart, nblk,

@@ -55,6 +55,16 @@ class _TrainBuffers:
     def __init__(self):
         self.key = None
 
+    def eik(self, rows, nn_k, wf):
+        """Analytic-eikonal buffers (PinTrainState.eik_coef / eik_vec), allocated on first use."""
+        key = (rows, nn_k, wf, str(self.sdf.device))
+        if getattr(self, "_eik_key", None) != key:
+            dev = self.sdf.device
+            self.eik_coef = torch.empty((rows, nn_k), dtype=torch.float32, device=dev)
+            self.eik_vec = torch.empty((rows, 20 if wf else 4), dtype=torch.float32, device=dev)
+            self._eik_key = key
+        return self.eik_coef, self.eik_vec
+
     def get(self, rows, nn_k, wf, device):
         key = (rows, nn_k, wf, str(device))
         if key != self.key:
@@ -370,8 +380,6 @@ class Mapper:
         if getattr(c, "proj_correction_on", False) or getattr(c, "consistency_loss_on", False):
             raise NotImplementedError("proj_correction / consistency losses are not on the fused path")
         if c.ekional_loss_on and c.weight_e > 0:
-            if not c.numerical_grad:
-                raise NotImplementedError("analytic-gradient eikonal (double backward) is not on the fused path")
             if getattr(c, "ekional_add_to", "all") != "all":
                 raise NotImplementedError("fused mapping implements ekional_add_to 'all'")
         # utils/tools.py:89-116: the fused step is Adam without L2 (the reference's defaults)
@@ -554,7 +562,10 @@ class Mapper:
             raise ValueError("grad_features must be a contiguous [L+1, 8] float32 tensor")
         dec = int(c.gradient_decimation)
         eik = bool(c.ekional_loss_on and c.weight_e > 0)
-        nd = (n + dec - 1) // dec if eik else 0
+        # numerical_grad off: the eikonal term on the analytic gradient of every batch row, its
+        # double backward in closed form (PIN_TRAIN_EIK, utils/mapper.py:50-54, :481-482)
+        analytic = eik and not bool(c.numerical_grad)
+        nd = (n + dec - 1) // dec if (eik and not analytic) else 0
         nn_k = int(c.query_nn_k)
         wf = bool(c.weighted_first)
         rows = n + 6 * nd
@@ -597,11 +608,15 @@ class Mapper:
                                 row_weight=_lib.ptr(wrow))
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
-        dx = wf and mlp_grad is None and _MLP_PACK
+        dx = wf and mlp_grad is None and _MLP_PACK and not analytic
         # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores
         mv = mlp_view(self.geo_mlp, packed=mlp_grad is None and _MLP_PACK)
         if dx:
             cfg.flags |= _lib.PIN_TRAIN_DX
+        if analytic:
+            cfg.flags |= _lib.PIN_TRAIN_EIK
+            ec, ev = b.eik(rows, nn_k, wf)
+            st.eik_coef, st.eik_vec = ec.data_ptr(), ev.data_ptr()
         if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
             raise RuntimeError("local_geo_features must be a contiguous float32 tensor")
         if grid:

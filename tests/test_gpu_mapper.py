@@ -409,3 +409,42 @@ def test_whole_mapping_call_fixture(golden, dev, backend, case):
         for key, p in zip(MLP_KEYS, dec.parameters()):
             w = z[f"after_{key}"]
             assert _norm(_np(p) - w) <= 1e-4 * _norm(w), (key, _norm(_np(p) - w), _norm(w))
+
+
+@pytest.mark.parametrize("case", ["mapping_eik_wf", "mapping_eik_livox"])
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_analytic_eikonal_mapping_call(golden, dev, backend, case):
+    """numerical_grad off: the eikonal term on autograd's dsdf/dq with create_graph=True, a double
+    backward (utils/mapper.py:50-54, :481-482, utils/tools.py:174-184), here in closed form
+    (PIN_TRAIN_EIK).  Cases: weighted_first, and the run_livox.yaml neural-point settings
+    (voxel 0.15, alpha 0.5 -> Kc 81, k 8, per-neighbour decoding, weighted BCE, sigma 0.08).
+
+    The reference's own double backward is ill-conditioned on the per-neighbour case: with 1
+    instead of 8 threads its first-step feature gradient moves by 18 % of its norm (queries a few
+    mm from a neural point make du/dq ~ 1/d^3, and the terms cancel).  Tolerances: first-step
+    gradients within 1e-4 of their norm + 3 x the reference's own spread (fixture spread_norm_*);
+    after the 15 iterations the features within 1e-3 ||moved|| + 3 x the reference's spread."""
+    z = golden(case)
+    nm, dec, mapper, replay = _mapping_call_setup(z, dev, backend)
+    assert not bool(nm.config.numerical_grad) and bool(z["require_gradient"])
+    fg = torch.zeros_like(nm.local_geo_features.data)
+    mg = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+    mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, fg, mg, 1,
+                      index=mapper._batch_index(), weight=mapper.weight_pool)
+    g, w = _np(fg), z["it0_feat_grad"]
+    tol = 1e-4 * _norm(w) + 3 * float(z["spread_norm_it0_feat_grad"])
+    print(f"{case}: first-step feature gradient |ours - ref| {_norm(g - w):.3e}, |ref| {_norm(w):.3e}, "
+          f"reference spread {float(z['spread_norm_it0_feat_grad']):.3e}")
+    assert _norm(g - w) <= tol, (_norm(g - w), tol)
+    for key, part in _split(_np(mg)).items():
+        ref = z[f"it0_grad_{key}"].reshape(-1)
+        tol = 1e-4 * _norm(ref) + 3 * float(z[f"spread_norm_it0_grad_{key}"])
+        print(f"   {key}: |ours - ref| {_norm(part - ref):.3e}, |ref| {_norm(ref):.3e}")
+        assert _norm(part - ref) <= tol, (key, _norm(part - ref), tol)
+    nm, dec, mapper, replay = _mapping_call_setup(z, dev, backend)
+    before = nm.geo_features.detach().cpu().numpy().copy()
+    mapper.mapping(int(z["iters"]))
+    got, want = _np(nm.geo_features), z["global_features_after"]
+    tol = 1e-3 * _norm(want - before) + 3 * float(z["spread_norm_global_features_after"])
+    print(f"   after {int(z['iters'])} iterations: |ours - ref| {_norm(got - want):.3e}, moved {_norm(want - before):.3e}")
+    assert _norm(got - want) <= tol, (_norm(got - want), tol)
