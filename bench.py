@@ -117,6 +117,7 @@ def parse():
     ap.add_argument("--no-map-update", action="store_true", help="skip the map-maintenance leg (8f rank 1)")
     ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
     ap.add_argument("--no-nwf-leg", action="store_true", help="skip the per-neighbour-decoding leg")
+    ap.add_argument("--no-slam", action="store_true", help="skip the whole-frame leg (configs[0])")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-shard", default="space", choices=["space", "dense"],
                     help="N > 1 mapper data parallelism: owner-partitioned slabs with halo exchange (space) or "
@@ -127,25 +128,70 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(nm, dec, q, wf):
-    """Oracle (numpy, 1 thread) on one full batch of the same workload; median of 3."""
-    from threadpoolctl import threadpool_limits
-    from oracle import pin_oracle as O
-    from tests.helpers import oracle_mlp, oracle_state
-    st = oracle_state(nm)
-    mlp = oracle_mlp(dec)
-    qh = q.cpu().numpy()
-    dx = O.neighbor_offsets(2, 0.2)
+def cpu_threads():
+    """The CPU baseline's thread count: the cores this process may run on (BASELINE.md's plan),
+    capped by OMP_NUM_THREADS when the host sets it (the GPU box gives one GPU's job 16)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _timed_median(fn, runs=5):
+    """One warm-up run, then the median of `runs` (BASELINE.md CPU-baseline plan)."""
+    fn()
     times = []
-    with threadpool_limits(limits=1):
-        for _ in range(3):
-            t0 = time.perf_counter()
-            O.sdf_and_grad(st, mlp, qh, nm.config.query_nn_k, dx, nm.max_valid_dist2, wf, False)
-            times.append(time.perf_counter() - t0)
-    t = statistics.median(times)
-    return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": f"one full {qh.shape[0]}-query batch over the same 1M-point map, numpy oracle "
-                      f"single-threaded, median of 3 ({t:.2f} s each)"}
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return statistics.median(times)
+
+
+def _torch_cpu_map(nm, wf, local=False):
+    """The map of a drop-in NeuralPoints as oracle/pin_torch_cpu tensors on the host (the whole
+    map is local in the synthetic workloads: global2local is the identity there)."""
+    from oracle import pin_torch_cpu as T
+    c = nm.config
+    feats = nm.local_geo_features.detach() if local else nm.geo_features
+    if local:
+        assert nm.local_count() == nm.count(), "CPU baseline expects the whole map local"
+    return T.TorchMap(nm.resolution, nm.buffer_size, nm.buffer_pt_index.cpu(), nm.neural_points.cpu(), feats.cpu(),
+                      nm.point_certainties.cpu(), nm.neighbor_dx.cpu(), nm.max_valid_dist2, c.query_nn_k, wf)
+
+
+def cpu_baseline(nm, dec, q, wf):
+    """The PyTorch-CPU restatement (oracle/pin_torch_cpu.py: hash probes, sort, IDW, decoder,
+    autograd gradient -- the reference's own algorithm as torch CPU ops) on one full batch of the
+    same workload, on this process's cores; one warm-up, median of 5."""
+    import torch as _t
+    from oracle import pin_torch_cpu as T
+    threads = cpu_threads()
+    old = _t.get_num_threads()
+    _t.set_num_threads(threads)
+    try:
+        m = _torch_cpu_map(nm, wf)
+        mlp = T.TorchMLP(dec.layers[0].weight.detach().cpu(), dec.layers[0].bias.detach().cpu(),
+                         dec.lout.weight.detach().cpu(), dec.lout.bias.detach().cpu(), dec.sdf_scale)
+        qh = q.cpu()
+        t = _timed_median(lambda: T.sdf_and_grad(m, mlp, qh))
+    finally:
+        _t.set_num_threads(old)
+    return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"one full {qh.shape[0]}-query batch over the same 1M-point map: oracle/pin_torch_cpu.py "
+                      f"(torch {_t.__version__} CPU, {threads} threads, autograd gradient), one warm-up, median of 5 "
+                      f"({t:.3f} s each)"}
 
 
 def time_kernel(nm, dec, q, wf, backend, steps):
@@ -332,8 +378,8 @@ def mesher_leg(nm, dec, pts, args, dev, world, rank):
 
 
 _FRAME_TIMING = ("each frame timed on its own (synchronised before and after; the frame's own host syncs "
-                 "already serialise it): median frame time x frames, max over ranks; the mean is reported "
-                 "beside it (one-off caching-allocator growth of the growing map / pool shows there)")
+                 "already serialise it): value = frames / (mean frame time x frames), max over ranks; the "
+                 "median frame time is reported beside it")
 
 
 def _frame_times(run, frames):
@@ -349,8 +395,9 @@ def _frame_times(run, frames):
 
 
 def _frames_el(per_frame, nsteps, world, dev):
-    """(median frame time x nsteps, mean frame time), each the max over ranks."""
-    t = torch.tensor([statistics.median(per_frame) * nsteps, statistics.mean(per_frame)], dtype=torch.float64,
+    """(mean frame time x nsteps, median frame time), each the max over ranks: the value is the
+    whole sequence's throughput (the mean), the median is reported beside it."""
+    t = torch.tensor([statistics.mean(per_frame) * nsteps, statistics.median(per_frame)], dtype=torch.float64,
                      device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -382,10 +429,10 @@ def map_leg(args, dev, world, rank):
     if world > 1:
         dist.barrier()
     per_frame = _frame_times(lambda k: nm.update(frames[k], sensors[k], None, k), range(nw, T))
-    el, mean = _frames_el(per_frame, nsteps, world, dev)
+    el, med = _frames_el(per_frame, nsteps, world, dev)
     res = {"metric": "map update frames/sec", "value": nsteps * world / el, "unit": "frames/s",
            "points_per_sec": MAP_FRAME * nsteps * world / el, "ms_per_frame": el / nsteps * 1e3,
-           "mean_ms_per_frame": mean * 1e3, "timing": _FRAME_TIMING, "steps": nsteps,
+           "median_ms_per_frame": med * 1e3, "timing": _FRAME_TIMING, "steps": nsteps,
            "map_points_before": M0, "map_points_after": nm.count(), "local_points": nm.local_count(),
            "scaling": "replicas",
            "config": {"workload": "NeuralPoints.update (+ reset_local_map) of 131072-point scans into the 1M-point "
@@ -437,10 +484,10 @@ def process_frame_leg(args, dev, world, rank):
     if world > 1:
         dist.barrier()
     per_frame = _frame_times(lambda k: mapper.process_frame(frames[k], None, pose_t[k], k), range(nw, T))
-    el, mean = _frames_el(per_frame, nsteps, world, dev)
+    el, med = _frames_el(per_frame, nsteps, world, dev)
     res = {"metric": "mapper frames/sec (process_frame)", "value": nsteps * world / el, "unit": "frames/s",
            "samples_per_sec": FRAME_RAYS * mapper.ray_sample_count * nsteps * world / el,
-           "ms_per_frame": el / nsteps * 1e3, "mean_ms_per_frame": mean * 1e3, "timing": _FRAME_TIMING,
+           "ms_per_frame": el / nsteps * 1e3, "median_ms_per_frame": med * 1e3, "timing": _FRAME_TIMING,
            "steps": nsteps, "pool_samples": int(mapper.pool_sample_count),
            "map_points": nm.count(), "new_samples": int(mapper.new_idx.shape[0]), "scaling": "replicas",
            "config": {"workload": "Mapper.process_frame: 65536-ray frames, 7 samples/ray, into the 1M-point surface "
@@ -486,33 +533,96 @@ def map_cpu_baseline(nm, frame, sensor):
             "sample": "one 131072-point frame into the 1M-point map (oracle map_update + reset_local_map)"}
 
 
-def mapper_cpu_baseline(nm, dec, coord, label, ts, sample):
-    """Oracle (numpy, 1 thread) mapper forward/backward on `sample` rows of one batch plus the
-    dense Adam over the whole map, extrapolated to a full batch (the map query work is linear
-    in the rows)."""
-    from threadpoolctl import threadpool_limits
-    from oracle import pin_oracle as O
-    from tests.helpers import oracle_mlp, oracle_state
-    st = oracle_state(nm)
-    mlp = oracle_mlp(dec)
+SLAM_FRAMES = 16           # configs[0]: timed frames after frame 0
+
+
+def slam_frame_leg(args, dev, world, rank):
+    """BASELINE configs[0] on the GPU: pin_slam.py's whole per-frame loop (:96-257) -- voxel
+    down-sample + crop, the tracker's registration (run_demo.yaml: up to 20 iterations), travel
+    distance, Mapper.process_frame (sampling, map update, pool), mapping(15) with the decoder
+    training (frames < freeze_after_frame) -- over 64-beam x 1024-column scans of a synthetic
+    street (pin_slam_amd.synthetic), run_demo.yaml settings, deskew off.  Frame 0 (the 15 x 40
+    iteration warm-up of the empty map) is not timed; every later frame is, part by part
+    (device-synchronised boundaries), the query index of the updated map (occupancy grid +
+    compact records) as a part of its own."""
+    from pin_slam_amd.synthetic import FrameLoop, Q_SCALE, lidar_scan, slam_poses, street_scene
+    nsteps = SLAM_FRAMES
+    rng = np.random.default_rng(21 + 1000 * rank)
+    scene = street_scene(rng)
+    poses = slam_poses(1 + nsteps)
+    scans = [torch.from_numpy(lidar_scan(T, scene, rng).astype(np.float32) / np.float32(Q_SCALE)).to(dev)
+             for T in poses]
+    cfg = P.Config(device=dev, reg_iter_n=20, track_on=True)     # config/lidar_slam/run_demo.yaml
+    nm = P.NeuralPoints(cfg)
+    torch.manual_seed(42)
+    dec = P.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(dev)
+    tracker = P.Tracker(cfg, nm, dec)
+    mapper = P.Mapper(cfg, None, nm, dec)
+    loop = FrameLoop(cfg, nm, dec, tracker, mapper, build_index=True)
+    loop.frame(scans[0])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    parts, frame_s, valid = {}, [], 0
+    for k in range(1, 1 + nsteps):
+        stamps = []
+
+        def mark(name):
+            torch.cuda.synchronize()
+            stamps.append((name, time.perf_counter()))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        valid += int(loop.frame(scans[k], timer=mark))
+        prev = t0
+        for name, t in stamps:
+            parts.setdefault(name, []).append(t - prev)
+            prev = t
+        frame_s.append(prev - t0)
+    el, med = _frames_el(frame_s, nsteps, world, dev)
+    err = max(float(np.linalg.norm(np.asarray(loop.odom_poses[k])[:3, 3] - poses[k][:3, 3]))
+              for k in range(1 + nsteps))
+    return {"metric": "SLAM frames/sec (pin_slam.py frame loop)", "value": nsteps * world / el, "unit": "frames/s",
+            "ms_per_frame": el / nsteps * 1e3, "median_ms_per_frame": med * 1e3,
+            "parts_mean_ms": {k: round(statistics.mean(v) * 1e3, 4) for k, v in parts.items()},
+            "frames": nsteps, "valid_frames": valid, "max_pose_error_m": err, "map_points": nm.count(),
+            "pool_samples": int(mapper.pool_sample_count), "scaling": "replicas", "timing": _FRAME_TIMING,
+            "config": {"workload": "configs[0]: synthetic 64-beam street sequence (64K points/scan), run_demo.yaml "
+                                   "settings (voxel 0.3, k 6, weighted_first, tracker iter_n 20, bs 16384, iters "
+                                   "15, decoder trained), deskew off",
+                       "note": "frame 0 (15 x 40 mapping iterations on the empty map) is not timed"}}
+
+
+def mapper_cpu_baseline(nm, dec, coord, label):
+    """One full mapper iteration of the same workload in the PyTorch-CPU restatement
+    (oracle/pin_torch_cpu.py: the 1M-row batch + 6 x 100K numerical-gradient stencil rows,
+    training-mode query, BCE + eikonal, backward, Adam on the [L+1, 8] features, decoder frozen),
+    on this process's cores; one warm-up, median of 5."""
+    import torch as _t
+    from oracle import pin_torch_cpu as T
+    threads = cpu_threads()
+    old = _t.get_num_threads()
+    _t.set_num_threads(threads)
     c = nm.config
-    dx = O.neighbor_offsets(2, 0.2)
-    ch, lh, th = coord[:sample].cpu().numpy(), label[:sample].cpu().numpy(), ts[:sample].cpu().numpy()
-    with threadpool_limits(limits=1):
-        t0 = time.perf_counter()
-        out = O.mapper_forward_backward(st, mlp, ch, lh, th, 8, dx, nm.max_valid_dist2, bool(c.weighted_first),
-                                        float(np.float32(0.055)), 0.5, 10, 0.3 * 0.2)
-        t_fb = time.perf_counter() - t0
-        m = np.zeros_like(st.local_features)
-        v = np.zeros_like(st.local_features)
-        t0 = time.perf_counter()
-        O.adam_step(st.local_features, out["feat_grad"], m, v, 1, 0.01)
-        t_adam = time.perf_counter() - t0
-    n = coord.shape[0]
-    t_iter = t_fb * (n / sample) + t_adam
-    return {"value": 1.0 / t_iter, "unit": "iters/s", "cores": 1, "kind": "port",
-            "sample": f"numpy oracle single-threaded: forward+backward of {sample} of the {n} batch rows "
-                      f"({t_fb:.2f} s, scaled x{n / sample:.0f}) + dense Adam over the map ({t_adam:.2f} s)"}
+    try:
+        m = _torch_cpu_map(nm, True, local=True)
+        mlp = T.TorchMLP(dec.layers[0].weight.detach().cpu(), dec.layers[0].bias.detach().cpu(),
+                         dec.lout.weight.detach().cpu(), dec.lout.bias.detach().cpu(), dec.sdf_scale)
+        feats = _t.nn.Parameter(m.features.clone())
+        cert = m.certainties.clone()
+        ch, lh = coord.cpu(), label.cpu()
+        sigma = float(c.logistic_gaussian_ratio * c.sigma_sigmoid_m)
+        eps = float(c.voxel_size_m * c.num_grad_step_ratio)
+
+        def one():
+            opt = _t.optim.Adam([feats], lr=c.lr, betas=(0.9, 0.99), eps=c.adam_eps)
+            T.mapping_iteration(m, mlp, feats, opt, ch, lh, sigma, c.weight_e, int(c.gradient_decimation), eps, cert)
+        t = _timed_median(one)
+    finally:
+        _t.set_num_threads(old)
+    return {"value": 1.0 / t, "unit": "iters/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"one full iteration ({coord.shape[0]} batch rows + stencil, {m.points.shape[0]}-point map): "
+                      f"oracle/pin_torch_cpu.py (torch {_t.__version__} CPU, {threads} threads, autograd backward, "
+                      f"torch.optim.Adam), one warm-up, median of 5 ({t:.2f} s each)"}
 
 
 def _shard_info(mapper):
@@ -579,7 +689,7 @@ def mapper_leg(args, dev, world, rank):
                         "scope": "whole iteration", "algorithmic_bytes_per_iter": bpi}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         idx = torch.randint(0, MAPPER_POOL, (MAPPER_BS,), device=dev)
-        res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx], ts[idx], 16384)
+        res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx])
     return res
 
 
@@ -642,11 +752,14 @@ def main():
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
     # the launched instance: <WF, PGO, GRAD, FAT, MF> (grid) / <WF, PGO, GRAD, MF> (hash)
+    traffic = None
     from pin_slam_amd.query import _MLP_PACK
     mf = str(bool(_MLP_PACK)).lower()
     kernel_name = "k_query_sdf_grid" if backend == "grid" else "k_query_sdf"
     kernel_tpl = (f"{str(wf).lower()}, false, true, true, {mf}>" if backend == "grid"
                   else f"{str(wf).lower()}, false, true, {mf}>")
+    traffic = (args.traffic_bytes if args.traffic_bytes is not None
+               else measured_traffic(f"{kernel_name}<" + kernel_tpl))
     out = {
         "metric": "SDF+grad queries/sec over 1M-point map",
         "value": value,
@@ -658,7 +771,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (decoder operands as f16 hi+lo pairs on the matrix cores, f32 accumulate)",
         "data": "synthetic",
         "config": {"workload": "SDF+analytic-grad, 1M-point surface map, 262144 queries/step/GPU (configs[1])",
                    "map_points": int(pts.shape[0]), "queries_per_step_per_gpu": N_QUERY, "Kc": int(nm.neighbor_K),
@@ -667,13 +780,19 @@ def main():
                    "candidate_backend": backend, "map_index_build_ms": round(build_ms, 3)},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
-                     "traffic": (args.traffic_bytes if args.traffic_bytes is not None
-                                 else measured_traffic(f"{kernel_name}<" + kernel_tpl)),
+                     "traffic": traffic,
                      "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
                                        "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
                      "kernel": kernel_name, "kernel_ms": kern_ms,
                      "order_pass_ms": order_ms,
-                     "algorithmic_bytes_per_query": BYTES_PER_QUERY},
+                     "algorithmic_bytes_per_query": BYTES_PER_QUERY,
+                     # the three views of the same number: the kernel alone (frac, above);
+                     # the whole step by BASELINE.md's formula, queries/s x 944 B / 8 TB/s (sort, launches
+                     # and host time included); the HBM bytes the PMC counters saw per launch over the
+                     # kernel's time (below 1 where neighbouring queries share lines in L2)
+                     "frac_kernel": achieved / HBM_PEAK,
+                     "frac_step": (value / world) * BYTES_PER_QUERY / HBM_PEAK,
+                     "frac_pmc_traffic": (traffic / (kern_ms * 1e-3) / HBM_PEAK) if traffic else None},
         "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -689,6 +808,8 @@ def main():
         out["map_update"] = map_leg(args, dev, world, rank)
     if not args.no_process_frame:
         out["process_frame"] = process_frame_leg(args, dev, world, rank)
+    if not args.no_slam:
+        out["slam_frame"] = slam_frame_leg(args, dev, world, rank)
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)
     if rank == 0:

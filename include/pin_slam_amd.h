@@ -209,6 +209,7 @@ typedef struct PinRegParams {
     float max_sdf_std;           /* surface_sample_range_m * max_sdf_std_ratio (only if sdf_std given) */
     float gm_dist;               /* reg_GM_dist_m, <= 0: no residual weight */
     float gm_grad;               /* reg_GM_grad, <= 0: no gradient weight */
+    int32_t div_grad_norm;       /* reg_dist_div_grad_norm: r = sdf / |g| - label (:335-336) */
 } PinRegParams;
 
 /* accumulator layout of pin_reg_normal_eq's output */

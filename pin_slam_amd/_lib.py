@@ -60,7 +60,7 @@ class PinGrid(ctypes.Structure):
 
 class PinRegParams(ctypes.Structure):
     _fields_ = [("min_nn_count", i32), ("min_grad_norm", f32), ("max_grad_norm", f32), ("max_sdf_std", f32),
-                ("gm_dist", f32), ("gm_grad", f32)]
+                ("gm_dist", f32), ("gm_grad", f32), ("div_grad_norm", i32)]
 
 
 REG_NACC = 31

@@ -95,6 +95,17 @@ class Config:
         self.reg_term_thre_m = 0.0005
         self.eigenvalue_check = True
         self.photometric_loss_on = False
+        # frame loop / dataset (pin_slam.py, dataset/slam_dataset.py; utils/config.py:45-67, :157-176,
+        # :190, :235-241, :382, :483)
+        self.deskew = False
+        self.min_range = 2.5
+        self.min_z = -4.0
+        self.max_z = 60.0
+        self.uniform_motion_on = True
+        self.stop_frame_thre = 20
+        self.freeze_after_frame = 40
+        self.init_iter_ratio = 40
+        self.mapping_freq_frame = 1
         # mesher (:296-308)
         self.mc_res_m = 0.1
         self.mesh_min_nn = 8
@@ -108,3 +119,7 @@ class Config:
             self.local_map_radius = self.max_range + 2.0  # utils/config.py:574
         if "window_radius" not in overrides:
             self.window_radius = max(self.max_range, 6.0)  # utils/config.py:572
+        if "vox_down_m" not in overrides:
+            self.vox_down_m = self.max_range * 1e-3        # utils/config.py:382
+        if "source_vox_down_m" not in overrides:
+            self.source_vox_down_m = self.vox_down_m * 10  # utils/config.py:483

@@ -46,7 +46,8 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
         }
         if (valid_out) valid_out[i] = valid ? 1 : 0;
         if (!valid) continue;
-        const float r = sdf[i] - (label ? label[i] : 0.f);
+        const float sd = prm.div_grad_norm ? sdf[i] / gn : sdf[i];   // :335-336, "fix the overshot"
+        const float r = sd - (label ? label[i] : 0.f);
         float w = 1.f;
         if (weight) {
             w = weight[i];

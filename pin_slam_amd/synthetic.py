@@ -4,7 +4,13 @@ Map: one neural point per ``res`` voxel column on z = 0.5 sin(x/7) cos(y/5) + 0.
 an n x n grid, xy = (i + 0.5) * res; features ~ N(0, 0.05^2) (the reference default
 feature_std = 0 would make the benchmark degenerate); decoder = nn.Linear default init
 under torch.manual_seed(seed).  Queries: random map points + N(0, sigma^2) per axis.
+
+Sequence (BASELINE configs[0], the plumbing run): a street of box buildings, cars and poles,
+ray-cast by a 64-beam x 1024-column spinning lidar along an accelerating trajectory, and
+``FrameLoop``, pin_slam.py's per-frame order (:96-257) over the drop-in classes with the
+dataset's pose bookkeeping (dataset/slam_dataset.py:260-430) restated.
 """
+import numpy as np
 import torch
 
 from .config import Config
@@ -95,3 +101,184 @@ def train_surface(nm, dec, pts, iters=300, bs=16384, seed=3, pool=1 << 20):
     nm.reset_local_map(torch.zeros(3, device=nm.neural_points.device),
                        torch.eye(3, device=nm.neural_points.device), 0)
     return float(mapper.last_loss)
+
+
+# ------------------------------------------------------------------ the street sequence
+SLAM_SENSOR_H = 1.73
+Q_SCALE = 512.0   # sensor-frame points stored as int16 multiples of 2^-9 m (|coord| < 64 m)
+
+
+def street_scene(rng):
+    """Boxes (buildings, cars, a wall) and vertical cylinders (poles / trunks) on a ground plane,
+    in the frame of the first sensor pose (ground at z = -1.73)."""
+    g = -SLAM_SENSOR_H
+    boxes = []
+    x = -40.0
+    while x < 70.0:       # two rows of buildings along the street
+        w = rng.uniform(6.0, 14.0)
+        for side in (-1.0, 1.0):
+            y0 = side * rng.uniform(9.0, 12.0)
+            d = rng.uniform(6.0, 12.0)
+            ylo, yhi = (y0, y0 + d) if side > 0 else (y0 - d, y0)
+            boxes.append((x, x + w, ylo, yhi, g, g + rng.uniform(5.0, 16.0)))
+        x += w + rng.uniform(2.0, 6.0)
+    for _ in range(10):   # parked cars
+        cx = rng.uniform(-30.0, 60.0)
+        cy = rng.choice([-1.0, 1.0]) * rng.uniform(4.5, 6.5)
+        boxes.append((cx, cx + 4.2, cy - 0.9, cy + 0.9, g, g + 1.5))
+    boxes.append((75.0, 76.0, -30.0, 30.0, g, g + 4.0))    # a wall across the street's end
+    cyls = [(rng.uniform(-30.0, 60.0), rng.choice([-1.0, 1.0]) * rng.uniform(3.2, 7.5), rng.uniform(0.15, 0.45),
+             g, g + rng.uniform(3.0, 8.0)) for _ in range(24)]
+    return np.asarray(boxes), np.asarray(cyls), g
+
+
+def lidar_scan(pose, scene, rng, beams=64, cols=1024, noise=0.01):
+    """A 64-beam spinning lidar at `pose` (4x4, f64) ray-cast against the scene; returns the hits in
+    the sensor frame, ranges in [3, 59.5] m (so the reference's crop_frame is a no-op), quantised
+    to multiples of 2^-9 m (int16 storage, exact in float32)."""
+    boxes, cyls, ground = scene
+    el = np.deg2rad(np.linspace(-24.8, 2.0, beams))
+    az = np.linspace(-np.pi, np.pi, cols, endpoint=False)
+    E, A = np.meshgrid(el, az, indexing="ij")
+    ds = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], -1).reshape(-1, 3)
+    R, o = pose[:3, :3], pose[:3, 3]
+    d = ds @ R.T
+    t = np.full(d.shape[0], np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tg = (ground - o[2]) / d[:, 2]
+        t = np.where((d[:, 2] < 0) & (tg > 0), np.minimum(t, tg), t)
+        for (x0, x1, y0, y1, z0, z1) in boxes:
+            lo = (np.array([x0, y0, z0]) - o) / d
+            hi = (np.array([x1, y1, z1]) - o) / d
+            tn = np.minimum(lo, hi).max(1)
+            tf = np.maximum(lo, hi).min(1)
+            hit = (tn <= tf) & (tn > 0)
+            t = np.where(hit, np.minimum(t, tn), t)
+        for (cx, cy, r, z0, z1) in cyls:
+            px, py = o[0] - cx, o[1] - cy
+            a = d[:, 0] ** 2 + d[:, 1] ** 2
+            b = 2 * (px * d[:, 0] + py * d[:, 1])
+            cc = px * px + py * py - r * r
+            disc = b * b - 4 * a * cc
+            tc = (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a)
+            zc = o[2] + tc * d[:, 2]
+            hit = (disc > 0) & (tc > 0) & (zc > z0) & (zc < z1)
+            t = np.where(hit, np.minimum(t, tc), t)
+    t = t + rng.normal(0.0, noise, t.shape)
+    keep = np.isfinite(t) & (t > 3.0) & (t < 59.5)
+    p = ds[keep] * t[keep, None]
+    q = np.round(p * Q_SCALE)
+    assert np.abs(q).max() < 32767
+    return q.astype(np.int16)
+
+
+def slam_poses(frames):
+    """Sensor poses in the first pose's frame: accelerating along the street (0.22 m in the first
+    frame, ~1.6 m per frame by frame 11: the first guess is the identity, later ones the
+    constant-velocity model, off by the 0.14 m/frame^2 acceleration), a slow yaw and sway."""
+    out = []
+    for k in range(frames):
+        yaw = np.deg2rad(0.6 * k + 0.15 * np.sin(0.9 * k))
+        T = np.eye(4)
+        T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
+        T[:3, 3] = [0.15 * k + 0.07 * k * k, 0.08 * np.sin(0.7 * k), 0.01 * k]
+        out.append(T)
+    return out
+
+
+
+class FrameLoop:
+    """pin_slam.py:96-257 on the drop-in classes for scans already in memory: read (identity pose,
+    no pose file), voxel down-sample + crop, constant-velocity guess, source cloud, tracking,
+    update_odom_pose, travel distance, process_frame, decoder freeze, mapping(iters) -- the
+    dataset bookkeeping of dataset/slam_dataset.py:260-430 restated (deskew off).  ``draws``
+    (optional callable n -> (randn, rand, rand)) replays the sampler's draws."""
+
+    def __init__(self, cfg, nm, dec, tracker, mapper, build_index=False):
+        self.config, self.nm, self.dec, self.tracker, self.mapper = cfg, nm, dec, tracker, mapper
+        # build_index: build the query index of the updated map (occupancy grid + compact records)
+        # as a part of its own before tracking, instead of inside the tracker's first query
+        self.build_index = build_index
+        self.dev = nm.neural_points.device
+        self.odom_poses, self.travel_dist = [], []
+        self.processed_frame = 0
+        self.lose_track = False
+        self.last_pose_ref = np.eye(4)
+        self.last_odom_tran = np.eye(4)
+        self.cur_pose_ref = np.eye(4)
+        self.stop_count = 0
+        self.stop_status = False
+        self.gt_pose_provided = False
+        mapper.dataset = self
+
+    def read_and_preprocess(self, pts):
+        from .neural_points import voxel_down_sample
+        c = self.config
+        self.cur_pose_ref = np.eye(4)
+        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
+        cloud = pts[voxel_down_sample(pts, c.vox_down_m)]                 # slam_dataset.py:286
+        dist = torch.norm(cloud, dim=1)                                    # crop_frame, :827-834
+        keep = (dist > c.min_range) & (dist < c.max_range) & (cloud[:, 2] > c.min_z) & (cloud[:, 2] < c.max_z)
+        self.cur_point_cloud_torch = cloud[keep]
+        self.cur_source_points = None
+        if self.processed_frame == 0:
+            self.odom_poses.append(self.cur_pose_ref)
+            self.travel_dist.append(0.0)
+            self.last_pose_ref = self.cur_pose_ref
+        else:                                                              # :320-339
+            guess = self.last_pose_ref @ self.last_odom_tran if (c.uniform_motion_on and not self.lose_track) \
+                else self.last_pose_ref
+            self.cur_pose_guess_torch = torch.tensor(guess, dtype=torch.float64, device=self.dev)
+            src = self.cur_point_cloud_torch
+            self.cur_source_points = src[voxel_down_sample(src, c.source_vox_down_m)]
+
+    def update_odom_pose(self, cur_pose_torch):
+        """dataset/slam_dataset.py:376-430."""
+        c = self.config
+        self.cur_pose_torch = cur_pose_torch.detach()
+        self.cur_pose_ref = self.cur_pose_torch.cpu().numpy()
+        self.last_odom_tran = np.linalg.inv(self.last_pose_ref) @ self.cur_pose_ref
+        rot_close = np.all(np.abs(self.last_odom_tran[:3, :3] - np.eye(3)) < 1e-3)
+        tran_close = np.all(self.last_odom_tran[:3, 3] < c.voxel_size_m * 0.1)
+        self.stop_count = self.stop_count + 1 if (rot_close and tran_close) else 0
+        self.stop_status = self.stop_count > c.stop_frame_thre
+        self.odom_poses.append(self.odom_poses[-1] @ self.last_odom_tran)
+        step = np.linalg.norm(self.last_odom_tran[:3, 3])
+        if step > c.surface_sample_range_m * 40.0:
+            self.lose_track = True
+        self.travel_dist.append(self.travel_dist[-1] + step)
+        self.last_pose_ref = self.cur_pose_ref
+
+    def frame(self, pts, draws=None, timer=None):
+        """One frame of the loop; timer(name) (optional) is called at each part's end."""
+        c, nm, mapper = self.config, self.nm, self.mapper
+        mark = timer or (lambda name: None)
+        used = self.processed_frame
+        self.read_and_preprocess(pts)
+        mark("preprocess")
+        if self.build_index and used > 0 and nm.backend() == "grid":
+            nm.grid_view("local", True)
+            mark("index")
+        valid = True
+        if used > 0:
+            T, _, _, valid = self.tracker.tracking(self.cur_source_points, self.cur_pose_guess_torch, None, None)
+            self.lose_track = not valid
+            mapper.lose_track = not valid
+            self.update_odom_pose(T)
+        mark("tracking")
+        nm.travel_dist = torch.tensor(np.array(self.travel_dist), dtype=torch.float32, device=self.dev)
+        if not mapper.lose_track and not self.stop_status:
+            d = draws(self.cur_point_cloud_torch.shape[0]) if draws is not None else None
+            mapper.process_frame(self.cur_point_cloud_torch, None, self.cur_pose_torch, used, False, draws=d)
+        else:
+            nm.reset_local_map(self.cur_pose_torch[:3, 3], None, used)
+        mark("process_frame")
+        iters = c.iters * c.init_iter_ratio if used == 0 else c.iters
+        if used == c.freeze_after_frame:
+            for p in self.dec.parameters():
+                p.requires_grad_(False)
+        if used % c.mapping_freq_frame == 0:
+            mapper.mapping(iters)
+        mark("mapping")
+        self.processed_frame += 1
+        return valid

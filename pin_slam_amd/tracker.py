@@ -269,7 +269,8 @@ class Tracker:
         prm = _lib.PinRegParams(min_nn_count=int(cfg.query_nn_k), min_grad_norm=float(min_grad_norm),
                                 max_grad_norm=float(max_grad_norm), max_sdf_std=float(max_sdf_std),
                                 gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
-                                gm_grad=float(GM_grad) if GM_grad is not None else 0.0)
+                                gm_grad=float(GM_grad) if GM_grad is not None else 0.0,
+                                div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))))
         if cfg.weighted_first:
             std = None  # reference: sdf_std stays 0 < max_sdf_std
         labels = sdf_labels.detach().to(torch.float32).contiguous() if sdf_labels is not None else None

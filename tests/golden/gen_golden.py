@@ -428,6 +428,12 @@ def gen_tracker_case(name, cfg_kwargs, n_src, seed, n_train=150):
                                     cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
                                     cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, False)
     delta_T, _, _, _, valid_points, resid_cm, _ = res
+    # reg_dist_div_grad_norm (utils/tracker.py:335-336, off in every config): residual sdf / |g|
+    cfg.reg_dist_div_grad_norm = True
+    res_dn = tracker.registration_step(pts, None, torch.zeros(n_src), None, 9,
+                                       cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
+                                       cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, False)
+    cfg.reg_dist_div_grad_norm = False
     # the whole registration loop (utils/tracker.py:39-174) from the identity guess, with the
     # per-iteration increments and residuals recorded
     hist_dT, hist_res, hist_cnt = [], [], []
@@ -448,6 +454,7 @@ def gen_tracker_case(name, cfg_kwargs, n_src, seed, n_train=150):
                source=src, sdf=sdf_pred.numpy(), grad=sdf_grad.numpy(), mask=mask.numpy(),
                certainty=certainty.numpy(), sdf_std=sdf_std.numpy(),
                delta_T=delta_T.numpy(), valid_count=np.int64(valid_points.shape[0]),
+               divnorm_delta_T=res_dn[0].numpy(), divnorm_resid_cm=np.float64(res_dn[5]),
                tracking_T=T_track.numpy(), tracking_valid=np.bool_(valid_track),
                tracking_delta_T=np.stack(hist_dT), tracking_resid_cm=np.asarray(hist_res),
                tracking_valid_count=np.asarray(hist_cnt, dtype=np.int64),
@@ -776,6 +783,7 @@ def gen_process_frame_case(name="process_frame", seed=15, frames=4):
 # ------------------------------------------------------------------ sequence fixtures (configs[0])
 sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
 from tests.replay import ReplayDraws, mapping_pool  # noqa: E402
+from pin_slam_amd.synthetic import Q_SCALE, lidar_scan, slam_poses, street_scene  # noqa: E402
 
 
 class _ReplayTorch:
@@ -806,88 +814,6 @@ class _ReplayTorch:
     def randn(self, *size, **kw):
         size, n = self._numel(size)
         return torch.from_numpy(self.replay.randn(n)).reshape(size)
-
-
-SLAM_SENSOR_H = 1.73
-Q_SCALE = 512.0   # sensor-frame points stored as int16 multiples of 2^-9 m (|coord| < 64 m)
-
-
-def street_scene(rng):
-    """Boxes (buildings, cars, a wall) and vertical cylinders (poles / trunks) on a ground plane,
-    in the frame of the first sensor pose (ground at z = -1.73)."""
-    g = -SLAM_SENSOR_H
-    boxes = []
-    x = -40.0
-    while x < 70.0:       # two rows of buildings along the street
-        w = rng.uniform(6.0, 14.0)
-        for side in (-1.0, 1.0):
-            y0 = side * rng.uniform(9.0, 12.0)
-            d = rng.uniform(6.0, 12.0)
-            ylo, yhi = (y0, y0 + d) if side > 0 else (y0 - d, y0)
-            boxes.append((x, x + w, ylo, yhi, g, g + rng.uniform(5.0, 16.0)))
-        x += w + rng.uniform(2.0, 6.0)
-    for _ in range(10):   # parked cars
-        cx = rng.uniform(-30.0, 60.0)
-        cy = rng.choice([-1.0, 1.0]) * rng.uniform(4.5, 6.5)
-        boxes.append((cx, cx + 4.2, cy - 0.9, cy + 0.9, g, g + 1.5))
-    boxes.append((75.0, 76.0, -30.0, 30.0, g, g + 4.0))    # a wall across the street's end
-    cyls = [(rng.uniform(-30.0, 60.0), rng.choice([-1.0, 1.0]) * rng.uniform(3.2, 7.5), rng.uniform(0.15, 0.45),
-             g, g + rng.uniform(3.0, 8.0)) for _ in range(24)]
-    return np.asarray(boxes), np.asarray(cyls), g
-
-
-def lidar_scan(pose, scene, rng, beams=64, cols=1024, noise=0.01):
-    """A 64-beam spinning lidar at `pose` (4x4, f64) ray-cast against the scene; returns the hits in
-    the sensor frame, ranges in [3, 59.5] m (so the reference's crop_frame is a no-op), quantised
-    to multiples of 2^-9 m (int16 storage, exact in float32)."""
-    boxes, cyls, ground = scene
-    el = np.deg2rad(np.linspace(-24.8, 2.0, beams))
-    az = np.linspace(-np.pi, np.pi, cols, endpoint=False)
-    E, A = np.meshgrid(el, az, indexing="ij")
-    ds = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], -1).reshape(-1, 3)
-    R, o = pose[:3, :3], pose[:3, 3]
-    d = ds @ R.T
-    t = np.full(d.shape[0], np.inf)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        tg = (ground - o[2]) / d[:, 2]
-        t = np.where((d[:, 2] < 0) & (tg > 0), np.minimum(t, tg), t)
-        for (x0, x1, y0, y1, z0, z1) in boxes:
-            lo = (np.array([x0, y0, z0]) - o) / d
-            hi = (np.array([x1, y1, z1]) - o) / d
-            tn = np.minimum(lo, hi).max(1)
-            tf = np.maximum(lo, hi).min(1)
-            hit = (tn <= tf) & (tn > 0)
-            t = np.where(hit, np.minimum(t, tn), t)
-        for (cx, cy, r, z0, z1) in cyls:
-            px, py = o[0] - cx, o[1] - cy
-            a = d[:, 0] ** 2 + d[:, 1] ** 2
-            b = 2 * (px * d[:, 0] + py * d[:, 1])
-            cc = px * px + py * py - r * r
-            disc = b * b - 4 * a * cc
-            tc = (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a)
-            zc = o[2] + tc * d[:, 2]
-            hit = (disc > 0) & (tc > 0) & (zc > z0) & (zc < z1)
-            t = np.where(hit, np.minimum(t, tc), t)
-    t = t + rng.normal(0.0, noise, t.shape)
-    keep = np.isfinite(t) & (t > 3.0) & (t < 59.5)
-    p = ds[keep] * t[keep, None]
-    q = np.round(p * Q_SCALE)
-    assert np.abs(q).max() < 32767
-    return q.astype(np.int16)
-
-
-def slam_poses(frames):
-    """Sensor poses in the first pose's frame: accelerating along the street (0.22 m in the first
-    frame, ~1.6 m per frame by frame 11: the first guess is the identity, later ones the
-    constant-velocity model, off by the 0.14 m/frame^2 acceleration), a slow yaw and sway."""
-    out = []
-    for k in range(frames):
-        yaw = np.deg2rad(0.6 * k + 0.15 * np.sin(0.9 * k))
-        T = np.eye(4)
-        T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
-        T[:3, 3] = [0.15 * k + 0.07 * k * k, 0.08 * np.sin(0.7 * k), 0.01 * k]
-        out.append(T)
-    return out
 
 
 def slam_config():

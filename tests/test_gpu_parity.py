@@ -373,6 +373,14 @@ def test_registration_step_fixture(golden, dev, backend, case):
     assert abs(valid_points.shape[0] - int(z["valid_count"])) <= 2
     assert resid_cm == pytest.approx(float(z["resid_cm"]), rel=1e-3)
     np.testing.assert_allclose(_np(T), z["delta_T"], atol=5e-6)
+    # reg_dist_div_grad_norm (utils/tracker.py:335-336): residual sdf / |g| - label
+    cfg.reg_dist_div_grad_norm = True
+    T, _, _, _, _, resid_cm, _ = tr.registration_step(
+        src, None, torch.zeros(src.shape[0], device=dev), None, 9, float(z["reg_min_grad_norm"]),
+        float(z["reg_max_grad_norm"]), float(z["reg_GM_dist_m"]), float(z["reg_GM_grad"]), float(z["reg_lm_lambda"]))
+    cfg.reg_dist_div_grad_norm = False
+    assert resid_cm == pytest.approx(float(z["divnorm_resid_cm"]), rel=1e-3)
+    np.testing.assert_allclose(_np(T), z["divnorm_delta_T"], atol=5e-6)
 
 
 @pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])

@@ -34,73 +34,17 @@ import pytest
 import torch
 
 import pin_slam_amd as P
-from pin_slam_amd.neural_points import voxel_down_sample
+from pin_slam_amd.synthetic import FrameLoop
 from tests.replay import ReplayDraws
 
 pytestmark = pytest.mark.gpu
+
 
 @pytest.fixture(scope="module")
 def dev():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     return "cuda"
-
-
-class DatasetReplay:
-    """The pose / travel-distance bookkeeping of dataset/slam_dataset.py:260-430 (preprocess_frame,
-    update_odom_pose) restated for the replay: read_frame without a pose file (identity),
-    voxel down-sample at vox_down_m, crop, constant-velocity guess, source cloud at
-    source_vox_down_m.  Dataset IO is out of scope; this is the test's harness."""
-
-    def __init__(self, cfg, dev):
-        self.config = cfg
-        self.dev = dev
-        self.odom_poses = []
-        self.travel_dist = []
-        self.processed_frame = 0
-        self.lose_track = False
-        self.last_pose_ref = np.eye(4)
-        self.last_odom_tran = np.eye(4)
-        self.cur_pose_ref = np.eye(4)
-        self.stop_count = 0
-        self.stop_status = False
-        self.gt_pose_provided = False
-
-    def read_and_preprocess(self, pts):
-        c = self.config
-        self.cur_pose_ref = np.eye(4)
-        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
-        cloud = pts[voxel_down_sample(pts, c.vox_down_m)]
-        dist = torch.norm(cloud, dim=1)
-        keep = (dist > c.min_range) & (dist < c.max_range) & (cloud[:, 2] > c.min_z) & (cloud[:, 2] < c.max_z)
-        self.cur_point_cloud_torch = cloud[keep]
-        self.cur_source_points = None
-        if self.processed_frame == 0:
-            self.odom_poses.append(self.cur_pose_ref)
-            self.travel_dist.append(0.0)
-            self.last_pose_ref = self.cur_pose_ref
-        else:
-            guess = self.last_pose_ref @ self.last_odom_tran if (c.uniform_motion_on and not self.lose_track) \
-                else self.last_pose_ref
-            self.cur_pose_guess_torch = torch.tensor(guess, dtype=torch.float64, device=self.dev)
-            src = self.cur_point_cloud_torch
-            self.cur_source_points = src[voxel_down_sample(src, c.source_vox_down_m)]
-
-    def update_odom_pose(self, cur_pose_torch):
-        c = self.config
-        self.cur_pose_torch = cur_pose_torch.detach()
-        self.cur_pose_ref = self.cur_pose_torch.cpu().numpy()
-        self.last_odom_tran = np.linalg.inv(self.last_pose_ref) @ self.cur_pose_ref
-        rot_close = np.all(np.abs(self.last_odom_tran[:3, :3] - np.eye(3)) < 1e-3)
-        tran_close = np.all(self.last_odom_tran[:3, 3] < c.voxel_size_m * 0.1)
-        self.stop_count = self.stop_count + 1 if (rot_close and tran_close) else 0
-        self.stop_status = self.stop_count > c.stop_frame_thre
-        self.odom_poses.append(self.odom_poses[-1] @ self.last_odom_tran)
-        step = np.linalg.norm(self.last_odom_tran[:3, 3])
-        if step > c.surface_sample_range_m * 40.0:
-            self.lose_track = True
-        self.travel_dist.append(self.travel_dist[-1] + step)
-        self.last_pose_ref = self.cur_pose_ref
 
 
 def _pose_err(a, b):
@@ -143,44 +87,37 @@ def test_slam_sequence_matches_reference(golden, dev):
         dec.lout.weight.copy_(torch.as_tensor(z["dec_init_W2"]))
         dec.lout.bias.copy_(torch.as_tensor(z["dec_init_b2"]))
     dec.to(dev)
-    ds = DatasetReplay(cfg, dev)
     tracker = P.Tracker(cfg, nm, dec)
-    mapper = P.Mapper(cfg, ds, nm, dec)
+    mapper = P.Mapper(cfg, None, nm, dec)
+    loop = FrameLoop(cfg, nm, dec, tracker, mapper)     # pin_slam.py:96-257 on the drop-in classes
     replay = ReplayDraws(int(z["replay_seed"]))
     mapper._randint = lambda high, n: torch.from_numpy(replay.randint(high, n)).to(dev)
     S, Ff, Fb = int(cfg.surface_sample_n), int(cfg.free_front_n), int(cfg.free_behind_n)
+
+    def draws(n):
+        return (torch.from_numpy(replay.randn(n * S)), torch.from_numpy(replay.rand(n * Ff)),
+                torch.from_numpy(replay.rand(n * Fb)))
     report = []
     for k in range(frames):
         pts = torch.from_numpy(z[f"f{k}_scan"].astype(np.float32) / np.float32(z["q_scale"])).to(dev)
-        used = ds.processed_frame
-        ds.read_and_preprocess(pts)
-        assert ds.cur_point_cloud_torch.shape[0] == int(z["hist_n_cloud"][k]), f"frame {k}: cloud size"
-        valid = True
-        if used > 0:
-            assert ds.cur_source_points.shape[0] == int(z["hist_n_source"][k]), f"frame {k}: source size"
-            T, _, _, valid = tracker.tracking(ds.cur_source_points, ds.cur_pose_guess_torch, None, None)
-            ds.lose_track = not valid
-            mapper.lose_track = not valid
-            ds.update_odom_pose(T)
+        seen = {}
+
+        def check(part, k=k):
+            """Per-part checks, called by FrameLoop.frame at the end of each part."""
+            if part == "tracking":
+                assert loop.cur_point_cloud_torch.shape[0] == int(z["hist_n_cloud"][k]), f"frame {k}: cloud size"
+                if k > 0:
+                    assert loop.cur_source_points.shape[0] == int(z["hist_n_source"][k]), f"frame {k}: source size"
+            if part == "process_frame":
+                seen["counts"] = (nm.count(), nm.local_count(), int(mapper.pool_sample_count),
+                                  int(mapper.new_idx.shape[0]))
+        valid = loop.frame(pts, draws=draws, timer=check)
         assert bool(valid) == bool(z["hist_valid"][k]), f"frame {k}: tracking validity"
-        nm.travel_dist = torch.tensor(np.array(ds.travel_dist), dtype=torch.float32, device=dev)
-        n = ds.cur_point_cloud_torch.shape[0]
-        draws = (torch.from_numpy(replay.randn(n * S)), torch.from_numpy(replay.rand(n * Ff)),
-                 torch.from_numpy(replay.rand(n * Fb)))
-        if not mapper.lose_track and not ds.stop_status:
-            mapper.process_frame(ds.cur_point_cloud_torch, None, ds.cur_pose_torch, used, False, draws=draws)
-        else:
-            nm.reset_local_map(ds.cur_pose_torch[:3, 3], None, used)
-        iters = cfg.iters * cfg.init_iter_ratio if used == 0 else cfg.iters
-        if used == cfg.freeze_after_frame:
-            for p in dec.parameters():
-                p.requires_grad_(False)
-        counts = (nm.count(), nm.local_count(), int(mapper.pool_sample_count), int(mapper.new_idx.shape[0]))
-        want = tuple(int(z[f"hist_{n_}"][k]) for n_ in ("map_count", "local_count", "pool", "new"))
-        mapper.mapping(iters)
         assert replay.calls == int(z["hist_draws_after"][k]), f"frame {k}: draw stream out of step"
-        dt, dr = _pose_err(ds.cur_pose_ref, z["hist_pose"][k])
-        dt_true, _ = _pose_err(ds.cur_pose_ref, z["truth_poses"][k])
+        counts = seen["counts"]
+        want = tuple(int(z[f"hist_{n_}"][k]) for n_ in ("map_count", "local_count", "pool", "new"))
+        dt, dr = _pose_err(loop.cur_pose_ref, z["hist_pose"][k])
+        dt_true, _ = _pose_err(loop.cur_pose_ref, z["truth_poses"][k])
         report.append((k, round(dt, 4), round(dr, 4), round(dt_true, 4), counts, want))
         tol_t = max(0.05, 3 * float(z["spread_pose_dt"][k]))
         tol_r = max(0.1, 3 * float(z["spread_pose_dr"][k]))
@@ -189,9 +126,8 @@ def test_slam_sequence_matches_reference(golden, dev):
         for name, g, w, rel in zip(("map_count", "local_count", "pool", "new"), counts, want, (0.01, 0.01, 0.001, 0.15)):
             rel = max(rel, 3 * float(z[f"spread_rel_{name}"][k]))
             assert _within(g, w, rel), f"frame {k}: {name} {g} vs reference {w}"
-        if used == 0:
+        if k == 0:
             _surface_check(nm, dec, z, dev, "f0_surface_probes", "f0_surface_sdf")
-        ds.processed_frame += 1
     print("frame, |dt| m, |dR| deg vs reference, |dt| m vs truth, (map, local, pool, new) ours / reference")
     for r in report:
         print(*r)

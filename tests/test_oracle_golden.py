@@ -174,3 +174,66 @@ def test_mesher_query_points(golden):
     sdf, mask = O.mesher_query_points(st, mlp, z["coord"], k, dx, maxd2, wf, int(z["mesh_min_nn"]))
     np.testing.assert_array_equal(mask, z["mc_mask"])
     np.testing.assert_allclose(sdf, z["sdf"], atol=1e-6)
+
+
+# ---------------------------------------------------------------- the PyTorch-CPU restatement
+def _torch_map(z, ql):
+    """oracle.pin_torch_cpu.TorchMap over a fixture's map, global (ql=0) or local (ql=1) mode."""
+    import torch
+    from oracle import pin_torch_cpu as T
+    st = O.map_from_fixture(z)
+    dx, maxd2, k, wf = _cfg(z)
+    t = torch.from_numpy
+    if not ql:
+        return T.TorchMap(st.resolution, st.buffer_size, t(st.table), t(st.points), t(st.geo_features),
+                          t(st.certainties), dx, maxd2, k, wf), st
+    dtd = np.abs(st.travel_dist[st.cur_ts] - st.travel_dist[st.ts_create])
+    return T.TorchMap(st.resolution, st.buffer_size, t(st.table), t(st.points), t(st.local_features),
+                      t(st.local_certainties), dx, maxd2, k, wf, time_ok=t(dtd < np.float32(st.diff_travel_dist_local)),
+                      global2local=t(st.global2local), local_points=t(st.local_points)), st
+
+
+@pytest.mark.parametrize("case", QUERY_CASES)
+@pytest.mark.parametrize("ql", [0, 1])
+def test_torch_cpu_query_sdf_grad(golden, case, ql):
+    """bench.py's CPU baseline (oracle/pin_torch_cpu.py) reproduces the reference's SDF and
+    autograd gradient: nn_count exact, SDF 1e-6, gradient rel 1e-4 / abs 2e-5."""
+    import torch
+    from oracle import pin_torch_cpu as T
+    z = golden(case)
+    m, _ = _torch_map(z, ql)
+    mlp = T.TorchMLP(z["dec_W1"], z["dec_b1"], z["dec_W2"], z["dec_b2"], float(z["dec_sdf_scale"]))
+    sdf, grad, nn = T.sdf_and_grad(m, mlp, torch.from_numpy(z["queries"]))
+    p = f"q{ql}_"
+    np.testing.assert_array_equal(nn.numpy(), z[p + "nn_counts"])
+    np.testing.assert_allclose(sdf.numpy(), z[p + "sdf"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(grad.numpy(), z[p + "grad"], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("case", ["mapper_wf", "mapper_nwf"])
+def test_torch_cpu_mapping_iteration(golden, case):
+    """The restatement's mapping iteration: loss and feature / decoder gradients of the
+    reference's first iteration (rel 1e-5 / 1e-4)."""
+    import torch
+    from oracle import pin_torch_cpu as T
+    z = golden(case)
+    m, st = _torch_map(z, 1)
+    mlp = T.TorchMLP(z["dec_W1"], z["dec_b1"], z["dec_W2"], z["dec_b2"], float(z["dec_sdf_scale"]),
+                     requires_grad=True)
+    feats = torch.nn.Parameter(torch.from_numpy(st.local_features.copy()))
+
+    class NoStep:   # keep the gradients for the comparison
+        def zero_grad(self, set_to_none=True):
+            feats.grad = None
+            for p in mlp.params:
+                p.grad = None
+
+        def step(self):
+            pass
+    loss = T.mapping_iteration(m, mlp, feats, NoStep(), torch.from_numpy(z["it0_coord"]),
+                               torch.from_numpy(z["it0_label"]), float(z["sigma"]), float(z["weight_e"]),
+                               int(z["gradient_decimation"]), float(z["num_grad_eps"]))
+    assert loss == pytest.approx(float(z["it0_loss"]), rel=1e-5)
+    np.testing.assert_allclose(feats.grad.numpy(), z["it0_feat_grad"], rtol=1e-4, atol=1e-8)
+    for key, p in zip(("W1", "b1", "W2", "b2"), mlp.params):
+        np.testing.assert_allclose(p.grad.numpy(), z[f"it0_grad_{key}"].reshape(p.shape), rtol=1e-4, atol=1e-7)
