@@ -231,6 +231,24 @@ int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, 
                       const float* sdf_std, const float* sdf_label, const float* weight, int64_t n,
                       const PinRegParams* prm, double* workspace, double* out, uint8_t* valid_out, void* stream);
 
+/* Status record of pin_reg_solve (doubles). */
+#define PIN_REG_NSTATUS 8        /* [0] n_valid, [1] mean |r| in cm, [2] rotation of dT in degrees,
+                                    [3] |translation of dT| m, [4] 1 if solved (n_valid >= 10) */
+
+/*
+ * pin_reg_solve -- implicit_reg's 6x6 solve on the device (utils/tracker.py:483-496, expmap
+ * :580-589) from pin_reg_normal_eq's accumulators: N += lm_lambda diag(N), t = N^-1 g in f64,
+ * delta_pose [4,4] f64 = [expmap(t[0:3]) | t[3:6]] (identity below 10 valid points, :310-312);
+ * pose_out = delta_pose @ pose_in when both are non-NULL (the tracking loop's T = dT T, :115);
+ * status[PIN_REG_NSTATUS] as above (the rotation angle is :132's, rotation_matrix_to_axis_angle).
+ */
+int pin_reg_solve(const double* acc, double lm_lambda, const double* pose_in, double* delta_pose, double* pose_out,
+                  double* status, void* stream);
+
+/* pin_transform_points -- transform_torch (utils/tools.py:386-399): out [n,3] f32 = the points
+ * under pose [4,4] (row-major f64 on the device, cast to f32), one fma chain per coordinate. */
+int pin_transform_points(const float* points, int64_t n, const double* pose, float* out, void* stream);
+
 /*
  * pin_cell_bounds -- out[0..2] = min, out[3..5] = max over the points of floor(p / resolution)
  * (f32 division, the reference's voxel rule, neural_points.py:214); the occupancy-grid box.

@@ -64,6 +64,7 @@ class PinRegParams(ctypes.Structure):
 
 
 REG_NACC = 31
+REG_NSTATUS = 8
 REG_WORKSPACE_DOUBLES = 256 * REG_NACC
 
 
@@ -119,6 +120,8 @@ _SIGS = {
     "pin_reg_normal_eq": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64,
                           _P(PinRegParams), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_cell_bounds": [c_void_p, i64, f32, c_void_p, c_void_p],
+    "pin_reg_solve": [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_transform_points": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_fill": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -106,9 +106,117 @@ __global__ void __launch_bounds__(256) k_reg_final(const double* __restrict__ pa
     if (k < PIN_REG_NACC && l == 0) out[k] = v;
 }
 
+// transform_torch (utils/tools.py:386-399): [p, 1] @ T^T in f32 with T cast to f32, as the fma
+// chain x, y, z then + t (the same arithmetic as pin_sample_rays' world copy)
+__global__ void __launch_bounds__(kRegBlock)
+k_transform_points(const float* __restrict__ src, int64_t n, const double* __restrict__ T, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kRegBlock + threadIdx.x;
+    if (i >= n) return;
+    float t[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) t[e] = (float)T[e];
+    const float px = src[3 * i], py = src[3 * i + 1], pz = src[3 * i + 2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) out[3 * i + a] = fmaf(pz, t[4 * a + 2], fmaf(py, t[4 * a + 1], px * t[4 * a])) + t[4 * a + 3];
+}
+
+// implicit_reg's solve on the device (utils/tracker.py:483-496, expmap :580-589) and the tracking
+// loop's bookkeeping of one iteration (:115, :132-133): from the accumulators of
+// pin_reg_normal_eq, N = s sum w J^T J, g = -s sum w r J with s = n / (2 sum w) (the w /= 2 mean(w)
+// of :394), N += lambda diag(N), t = N^-1 g (f64 Gaussian elimination, partial pivoting),
+// dT = [expmap(t[0:3]) | t[3:6]], pose_out = dT pose_in.  One thread.
+__global__ void k_reg_solve(const double* __restrict__ acc, double lm_lambda, const double* __restrict__ pose_in,
+                            double* __restrict__ dT, double* __restrict__ pose_out, double* __restrict__ status) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double s_w = acc[0], s_r = acc[1], cnt = acc[3];
+    status[0] = cnt;
+    status[1] = cnt > 0.0 ? s_r / cnt * 100.0 : 0.0;
+    double D[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    double rot_deg = 0.0, tran = 0.0;
+    const bool solve = cnt >= 10.0;   // :310-312 returns the identity below 10 valid points
+    if (solve) {
+        const double sc = cnt / (2.0 * s_w);
+        double A[6][7];
+        int k = 4;
+        for (int a = 0; a < 6; ++a)
+            for (int b = a; b < 6; ++b) {
+                A[a][b] = A[b][a] = acc[k++] * sc;
+            }
+        for (int a = 0; a < 6; ++a) {
+            A[a][a] += lm_lambda * A[a][a];
+            A[a][6] = -acc[25 + a] * sc;
+        }
+        for (int c = 0; c < 6; ++c) {            // forward elimination with partial pivoting
+            int piv = c;
+            for (int r = c + 1; r < 6; ++r)
+                if (fabs(A[r][c]) > fabs(A[piv][c])) piv = r;
+            if (piv != c)
+                for (int e = 0; e < 7; ++e) {
+                    const double tmp = A[c][e];
+                    A[c][e] = A[piv][e];
+                    A[piv][e] = tmp;
+                }
+            for (int r = c + 1; r < 6; ++r) {
+                const double f = A[r][c] / A[c][c];
+                for (int e = c; e < 7; ++e) A[r][e] -= f * A[c][e];
+            }
+        }
+        double t[6];
+        for (int r = 5; r >= 0; --r) {
+            double v = A[r][6];
+            for (int e = r + 1; e < 6; ++e) v -= A[r][e] * t[e];
+            t[r] = v / A[r][r];
+        }
+        // expmap: R = I + S sin(angle) + S^2 (1 - cos(angle)), S = skew(axis)
+        const double angle = sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        const double ax = t[0] / angle, ay = t[1] / angle, az = t[2] / angle;
+        const double S[3][3] = {{0.0, -az, ay}, {az, 0.0, -ax}, {-ay, ax, 0.0}};
+        const double sn = sin(angle), cs = 1.0 - cos(angle);
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                double s2 = 0.0;
+                for (int e = 0; e < 3; ++e) s2 += S[a][e] * S[e][b];
+                D[4 * a + b] = (a == b ? 1.0 : 0.0) + S[a][b] * sn + s2 * cs;
+            }
+        D[3] = t[3];
+        D[7] = t[4];
+        D[11] = t[5];
+        rot_deg = acos((D[0] + D[5] + D[10] - 1.0) / 2.0) * 180.0 / 3.141592653589793;   // :591-598
+        tran = sqrt(t[3] * t[3] + t[4] * t[4] + t[5] * t[5]);
+    }
+    for (int e = 0; e < 16; ++e) dT[e] = D[e];
+    if (pose_in && pose_out) {
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b) {
+                double v = 0.0;
+                for (int e = 0; e < 4; ++e) v += D[4 * a + e] * pose_in[4 * e + b];
+                pose_out[4 * a + b] = v;
+            }
+    }
+    status[2] = rot_deg;
+    status[3] = tran;
+    status[4] = solve ? 1.0 : 0.0;
+}
+
 }  // namespace
 
 extern "C" {
+
+int pin_transform_points(const float* points, int64_t n, const double* pose, float* out, void* stream) {
+    if (n < 0 || (n > 0 && (!points || !pose || !out))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_transform_points, dim3((unsigned)((n + kRegBlock - 1) / kRegBlock)), dim3(kRegBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), points, n, pose, out);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}
+
+int pin_reg_solve(const double* acc, double lm_lambda, const double* pose_in, double* delta_pose, double* pose_out,
+                  double* status, void* stream) {
+    if (!acc || !delta_pose || !status || (pose_out && !pose_in)) return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_reg_solve, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), acc, lm_lambda,
+                       pose_in, delta_pose, pose_out, status);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}
 
 int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, const int32_t* nn_count,
                       const float* sdf_std, const float* sdf_label, const float* weight, int64_t n,

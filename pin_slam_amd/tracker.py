@@ -4,16 +4,20 @@ Per Gauss-Newton / LM iteration the reference evaluates ``query_feature`` + ``De
 + autograd ``get_gradient`` on every source point, filters, weights and forms a 6x6 system
 with torch ops (:176-496).  Here one iteration is:
 
+0. ``pin_transform_points``: the source cloud under the current pose (``tracking`` only);
 1. ``pin_query_sdf{,_grid}``: fused k-NN gather, IDW, decoder and closed-form dSDF/dq;
 2. ``pin_reg_normal_eq``: validity mask, Geman-McClure weights and the f64 normal equations
    in one deterministic reduction;
-3. a 6x6 f64 solve on the host (the reference also moves these 36 numbers around with
-   ``.item()``-style syncs every iteration).
+3. ``pin_reg_solve``: the 6x6 f64 solve, expmap, T = dT T and the convergence measures of dT on
+   the device; one host read of a 39-double record per iteration drives the control flow
+   (the reference syncs on ``.item()``-style reads several times per iteration).
 
 The control flow of ``tracking`` (convergence, validity checks, fall-back to the initial
-guess) follows :39-174 line by line.  Colour / photometric registration is out of scope
+guess) follows :39-174.  When ``install()`` puts registration_step on the reference class, the
+reference's own tracking loop drives it.  Colour / photometric registration is out of scope
 (off in every lidar config).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -131,24 +135,43 @@ _REG_BUF: dict = {}
 
 
 def _reg_buffers(dev):
-    """Per-device workspace + accumulator buffer and a pinned host mirror (reused every step;
-    the host read below synchronises the stream, so reuse is safe)."""
+    """Per-device buffers reused every step: the reduction workspace, the accumulators + status
+    record (one D2H copy), delta_T and two pose slots (the loop ping-pongs between them), and the
+    pinned host mirror of accumulators + status.  The host read in _register synchronises the
+    stream, so reuse is safe."""
     key = str(dev)
     if key not in _REG_BUF:
-        ws = torch.empty(_lib.REG_WORKSPACE_DOUBLES + _lib.REG_NACC, dtype=torch.float64, device=dev)
-        host = torch.empty(_lib.REG_NACC, dtype=torch.float64, pin_memory=ws.is_cuda)
-        _REG_BUF[key] = (ws, host)
+        W = _lib.REG_WORKSPACE_DOUBLES
+        n = W + _lib.REG_NACC + _lib.REG_NSTATUS + 16 * 3
+        buf = torch.empty(n, dtype=torch.float64, device=dev)
+        host = torch.empty(_lib.REG_NACC + _lib.REG_NSTATUS, dtype=torch.float64, pin_memory=buf.is_cuda)
+        o = W + _lib.REG_NACC + _lib.REG_NSTATUS
+        _REG_BUF[key] = dict(ws=buf[:W], acc_status=buf[W:o], acc=buf[W:W + _lib.REG_NACC],
+                             status=buf[W + _lib.REG_NACC:o], dT=buf[o:o + 16].view(4, 4),
+                             poses=(buf[o + 16:o + 32].view(4, 4), buf[o + 32:o + 48].view(4, 4)), host=host, flip=0)
     return _REG_BUF[key]
 
 
 def _reg_accumulate(points, sdf, grad, nn_count, sdf_std, label, weight, prm, valid_out=None):
-    ws, host = _reg_buffers(points.device)
-    out = ws[_lib.REG_WORKSPACE_DOUBLES:]
+    """pin_reg_normal_eq; the accumulators copied to the host (implicit_reg's pre-weighted form)."""
+    b = _reg_buffers(points.device)
     _lib.call("pin_reg_normal_eq", _lib.ptr(points), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count),
-              _lib.ptr(sdf_std), _lib.ptr(label), _lib.ptr(weight), points.shape[0], prm, _lib.ptr(ws),
-              _lib.ptr(out), _lib.ptr(valid_out), _lib.stream())
-    host.copy_(out)
-    return host.numpy().copy()
+              _lib.ptr(sdf_std), _lib.ptr(label), _lib.ptr(weight), points.shape[0], prm, _lib.ptr(b["ws"]),
+              _lib.ptr(b["acc"]), _lib.ptr(valid_out), _lib.stream())
+    h = b["host"][:_lib.REG_NACC]
+    h.copy_(b["acc"])
+    return h.numpy().copy()
+
+
+def transform_points(points: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
+    """transform_torch (utils/tools.py:386-399) as one launch (pin_transform_points): f32 points
+    [N,3] under a [4,4] pose (f64 on the device)."""
+    p = points.detach().to(torch.float32).contiguous()
+    _lib.require_device(p)
+    T = pose.detach().to(device=p.device, dtype=torch.float64).contiguous()
+    out = torch.empty_like(p)
+    _lib.call("pin_transform_points", _lib.ptr(p), p.shape[0], _lib.ptr(T), _lib.ptr(out), _lib.stream())
+    return out
 
 
 class Tracker:
@@ -168,8 +191,14 @@ class Tracker:
     def tracking(self, source_points, init_pose=None, source_colors=None, source_normals=None,
                  source_semantics=None, source_sdf=None, cur_ts=None, loop_reg: bool = False,
                  vis_result: bool = False):
+        """The registration loop with the pose kept on the device: per iteration one transform
+        launch, the fused query, the normal equations and their solve (pin_reg_solve, which also
+        applies T = dT T and measures dT for the convergence test), then ONE host read of a
+        39-double record that drives the reference's control flow (:92-159)."""
         cfg = self.config
-        T = torch.eye(4, dtype=torch.float64, device=self.device) if init_pose is None else init_pose
+        dev = torch.device(self.device) if not torch.is_tensor(source_points) else source_points.device
+        T = torch.eye(4, dtype=torch.float64, device=dev) if init_pose is None else \
+            init_pose.to(device=dev, dtype=torch.float64)
         cov_mat = None
         min_grad_norm = cfg.reg_min_grad_norm
         max_grad_norm = cfg.reg_max_grad_norm
@@ -191,36 +220,39 @@ class Tracker:
         valid_flag = True
         last_sdf_residual_cm = 1e5
         source_point_count = source_points.shape[0]
-        if source_sdf is None:
-            source_sdf = torch.zeros(source_point_count, device=self.device)
+        src = source_points.detach().to(torch.float32).contiguous()
+        labels = None if source_sdf is None else source_sdf.detach().to(torch.float32).contiguous()
         weight_point_cloud = None
         eigenvalues = None
         sdf_residual_cm = 0.0
         valid_point_count = 0
         for i in range(iter_n):
-            cur_points = transform_torch(source_points, T)
-            reg = self.registration_step(cur_points, source_normals, source_sdf, source_colors, cur_ts,
-                                         min_grad_norm, max_grad_norm, cur_GM_dist_m, cur_GM_grad, lm_lambda,
-                                         (vis_result and converged))
-            delta_T, cov_mat, eigenvalues, weight_point_cloud, valid_points, sdf_residual_cm, _ = reg
-            T = delta_T @ T
+            cur_points = transform_points(src, T)
+            want_stats = vis_result and converged
+            r = self._register(cur_points, source_normals, labels, min_grad_norm, max_grad_norm, cur_GM_dist_m,
+                               cur_GM_grad, lm_lambda, want_stats, pose_in=T)
+            T = r["pose"]                                                     # :115, T = dT @ T
+            st = r["status"]
+            valid_point_count = int(st[0])
+            sdf_residual_cm = float(st[1]) if st[4] > 0 else 0.0
+            eigenvalues = r["eig"]
+            cov_mat = r["cov"]
             if (sdf_residual_cm - last_sdf_residual_cm) / last_sdf_residual_cm > max_increment_sdf_residual_ratio:
                 if not self.silence:
                     print("(Warning) registration failed: wrong optimization")
                 valid_flag = False
             else:
                 last_sdf_residual_cm = sdf_residual_cm
-            valid_point_count = valid_points.shape[0]
             if valid_point_count < min_valid_points or 1.0 * valid_point_count / source_point_count < min_valid_ratio:
                 if not self.silence:
                     print("(Warning) registration failed: not enough valid points")
                 valid_flag = False
             if not valid_flag or converged:
                 break
-            rot_angle_deg = rotation_matrix_to_axis_angle(delta_T[:3, :3]) * 180.0 / np.pi
-            tran_m = delta_T[:3, 3].norm()
+            rot_angle_deg, tran_m = float(st[2]), float(st[3])                # :132-133, from the solve
             if abs(rot_angle_deg) < term_thre_deg and tran_m < term_thre_m or i == iter_n - 2:
                 converged = True
+        T = T.clone()    # the loop's pose lives in a reused slot
         if sdf_residual_cm > max_valid_final_sdf_residual_cm:
             if not self.silence:
                 print("(Warning) registration failed: too large final residual")
@@ -255,16 +287,16 @@ class Tracker:
         return sdf, grad, None, None, None, mc_mask, cert, std
 
     # ------------------------------------------------------------------ utils/tracker.py:277-452
-    def registration_step(self, points, normals, sdf_labels, colors, cur_ts, min_grad_norm, max_grad_norm,
-                          GM_dist=None, GM_grad=None, lm_lambda=0.0, vis_weight_pc=False):
-        if colors is not None and getattr(self.config, "photometric_loss_on", False):
-            raise NotImplementedError("photometric registration is out of scope")
+    def _register(self, pts, normals, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda,
+                  want_stats, pose_in=None, valid_out=None):
+        """query + normal equations + solve of one registration step, all stream-ordered, then one
+        host read of accumulators + status.  Returns dict(delta (device f64 [4,4]), pose (dT @
+        pose_in, device), status (host [8]), acc (host [31]), cov, eig)."""
         if normals is not None:
             raise NotImplementedError("normal-consistency weights are not used by any reference config")
         cfg = self.config
-        pts = points.detach().to(torch.float32).contiguous()
         sdf, grad, nn, _, std = fused_query_sdf(self.neural_points, self.geo_decoder, pts, query_locally=True,
-                                          want_grad=True, want_std=not cfg.weighted_first, want_certainty=False)
+                                                want_grad=True, want_std=not cfg.weighted_first, want_certainty=False)
         max_sdf_std = cfg.surface_sample_range_m * cfg.max_sdf_std_ratio
         prm = _lib.PinRegParams(min_nn_count=int(cfg.query_nn_k), min_grad_norm=float(min_grad_norm),
                                 max_grad_norm=float(max_grad_norm), max_sdf_std=float(max_sdf_std),
@@ -273,15 +305,42 @@ class Tracker:
                                 div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))))
         if cfg.weighted_first:
             std = None  # reference: sdf_std stays 0 < max_sdf_std
+        b = _reg_buffers(pts.device)
+        s = _lib.stream()
+        _lib.call("pin_reg_normal_eq", _lib.ptr(pts), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), _lib.ptr(std),
+                  _lib.ptr(labels), None, pts.shape[0], ctypes.byref(prm), _lib.ptr(b["ws"]), _lib.ptr(b["acc"]),
+                  _lib.ptr(valid_out), s)
+        pose_out = None
+        if pose_in is not None:
+            b["flip"] ^= 1
+            pose_out = b["poses"][b["flip"]]
+            pin = pose_in if pose_in.is_contiguous() else pose_in.contiguous()
+        _lib.call("pin_reg_solve", _lib.ptr(b["acc"]), float(lm_lambda), _lib.ptr(pin) if pose_in is not None else None,
+                  _lib.ptr(b["dT"]), _lib.ptr(pose_out), _lib.ptr(b["status"]), s)
+        host = b["host"]
+        host.copy_(b["acc_status"])          # the step's one synchronisation
+        h = host.numpy()
+        acc, status = h[:_lib.REG_NACC].copy(), h[_lib.REG_NACC:].copy()
+        cov = eig = None
+        if want_stats and status[4] > 0:
+            _, cov, eig = _solve(acc, lm_lambda, True, True, pts.device)
+        return dict(delta=b["dT"], pose=pose_out, status=status, acc=acc, cov=cov, eig=eig)
+
+    def registration_step(self, points, normals, sdf_labels, colors, cur_ts, min_grad_norm, max_grad_norm,
+                          GM_dist=None, GM_grad=None, lm_lambda=0.0, vis_weight_pc=False):
+        """utils/tracker.py:277-452 -> (delta_T, cov_mat, eigenvalues, None, valid_points,
+        sdf_residual_cm, None).  valid_points keeps the source order."""
+        if colors is not None and getattr(self.config, "photometric_loss_on", False):
+            raise NotImplementedError("photometric registration is out of scope")
+        pts = points.detach().to(torch.float32).contiguous()
         labels = sdf_labels.detach().to(torch.float32).contiguous() if sdf_labels is not None else None
         valid = torch.empty(pts.shape[0], dtype=torch.uint8, device=pts.device)
-        acc = _reg_accumulate(pts, sdf, grad, nn, std, labels, None, prm, valid)
-        cnt = int(acc[3])
+        r = self._register(pts, normals, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda,
+                           vis_weight_pc, valid_out=valid)
+        cnt = int(r["status"][0])
         # the count is on the host already: gather the valid rows without another sync
         valid_points = points[torch.nonzero_static(valid, size=cnt).squeeze(1)]
         if cnt < 10:
             T = torch.eye(4, device=points.device, dtype=torch.float64)
             return T, None, None, None, valid_points, 0.0, 0.0
-        sdf_residual_cm = float(acc[1] / cnt) * 100.0
-        T, cov, eig = _solve(acc, lm_lambda, vis_weight_pc, vis_weight_pc, points.device)
-        return T, cov, eig, None, valid_points, sdf_residual_cm, None
+        return r["delta"].clone(), r["cov"], r["eig"], None, valid_points, float(r["status"][1]), None
