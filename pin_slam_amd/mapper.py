@@ -30,6 +30,7 @@ import torch.distributed as dist
 from . import _lib
 from .data_sampler import DataSampler
 from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
+from .sharding import all_reduce
 
 
 def _viewed_elsewhere(t: torch.Tensor) -> bool:
@@ -92,7 +93,7 @@ class Mapper:
     """utils/mapper.py:Mapper -- constructor signature, pools and training entry points."""
 
     def __init__(self, config, dataset, neural_points, geo_mlp, sem_mlp=None, color_mlp=None, group=None,
-                 shard="dense"):
+                 shard="dense", slab_layout="auto"):
         self.config = config
         self.silence = config.silence
         self.dataset = dataset
@@ -132,10 +133,12 @@ class Mapper:
         self.group = group
         # data-parallel mode with a group of W > 1: "dense" (every rank samples the whole pool,
         # SUM all-reduce of the [L+1,8] gradient) or "space" (owner-partitioned slabs, halo
-        # exchange only: pin_slam_amd.sharding)
+        # exchange only: pin_slam_amd.sharding); slab_layout "auto" (2-D cells where the map is
+        # wide in both axes) or "1d" (slabs along the longer axis)
         if shard not in ("dense", "space"):
             raise ValueError("shard must be 'dense' or 'space'")
         self.shard = shard
+        self.slab_layout = slab_layout
         self.last_loss = None        # device f64 tensor: loss of the last iteration
         self._buf = _TrainBuffers()
         self._adam_t = 0
@@ -444,7 +447,7 @@ class Mapper:
             if part is not None:
                 part.exchange_gradients(f_grad)                   # halo rows -> owners
                 if m_grad is not None:
-                    dist.all_reduce(m_grad, op=dist.ReduceOp.SUM, group=getattr(self, "group", None))
+                    all_reduce(m_grad, group=getattr(self, "group", None))
             self._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, partition=part)
             if part is not None:
                 part.exchange_features(fdata)                     # owners -> halo copies
@@ -466,8 +469,9 @@ class Mapper:
     def _slab_partition(self, world, fused):
         """shard="space" set-up of one mapping() call: (partition, the slab's pool rows, the slab's
         new samples, scales) -- or four Nones for the dense path.  Every rank takes the same
-        decision (the flags are all-reduced before any rank enters the partition's collectives):
-        maps with global2local-quirk records, or a slab without pool samples, fall back to dense.
+        decision (the counts are all-reduced before any rank leaves the set-up): a slab without
+        pool samples makes the call fall back to dense, with a warning.  The global2local
+        fill-quirk row (local row 1) is a shared row of the partition, not a fallback.
 
         scales(bs_hist_r, bs_new_r) -> (history-row scale, new-row scale).  A rank draws its batch
         from its slab only, so its rows are weighted to keep the union an unbiased estimate of the
@@ -481,23 +485,18 @@ class Mapper:
         group = getattr(self, "group", None)
         nm = self.neural_points
         dev = nm.local_neural_points.device
-        flag = torch.tensor([0.0 if self._slab_exact() else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        if float(flag[0]) > 0:
-            warnings.warn("shard='space': the local map has global2local-quirk records (PIN_RECORD_UNFAITHFUL); "
-                          "this mapping() call uses the dense gradient all-reduce")
-            return None, None, None, None
         if not fused:
             raise NotImplementedError("shard='space' samples device pools through the fused batch path")
         from .sharding import SlabPartition, query_reach
-        part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group)
+        part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group,
+                             layout=getattr(self, "slab_layout", "auto"))
         mask = part.sample_mask(self.global_coord_pool[: self.pool_sample_count])
         slab_rows = torch.nonzero(mask).flatten()
         slab_new = self.new_idx[mask[self.new_idx]] if self.new_idx is not None else None
         n_r = 0 if slab_new is None else int(slab_new.numel())
         cnt = torch.tensor([float(slab_rows.numel()), float(n_r), 1.0 if slab_rows.numel() == 0 else 0.0],
                            dtype=torch.float64, device=dev)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+        all_reduce(cnt, group=group)
         if float(cnt[2]) > 0:
             warnings.warn("shard='space': a slab holds no pool samples; this mapping() call uses the dense "
                           "gradient all-reduce")
@@ -515,15 +514,6 @@ class Mapper:
             return sh, sn
         self._partition = part
         return part, slab_rows, slab_new, scales
-
-    def _slab_exact(self):
-        """Slab sharding is exact when every candidate a query can reach is a local point at its own
-        position: the reference's global2local fill quirk (a non-local point passing the travel
-        filter reads local row 1, neural_points.py:290-300) would route gradients to a far-away
-        row.  Such records carry PIN_RECORD_UNFAITHFUL; with any of them the dense path is used."""
-        rec = self.neural_points.records("local")
-        flags = rec[:, 3].contiguous().view(torch.int32) & _lib.PIN_RECORD_UNFAITHFUL
-        return not bool((flags != 0).any())
 
     def _pools_fusable(self):
         c, l, t = self.global_coord_pool, self.sdf_label_pool, self.time_pool
@@ -647,7 +637,7 @@ class Mapper:
                       fdata.numel(), ctypes.byref(st), s)
         else:
             _lib.call("pin_adam_rows", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
-                      _lib.ptr(partition.owned), partition.owned.numel(), ctypes.byref(st), s)
+                      _lib.ptr(partition.adam_rows), partition.adam_rows.numel(), ctypes.byref(st), s)
             partition.zero_halo(f_grad)
         feats = self.neural_points.local_geo_features
         self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
@@ -712,17 +702,17 @@ def allreduce_gradients(grads, group=None):
             continue
         if g.dim() == 2 and g.shape[1] == 16:
             packed = g[:, :8].contiguous()
-            dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+            all_reduce(packed, group=group)
             g[:, :8].copy_(packed)
         else:
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+            all_reduce(g, group=group)
 
 
 def sync_side_effects(cert_delta, ts_update, group=None):
     """Training-mode side effects of a data-parallel mapping() call: the ranks' certainty deltas
     add up (scatter_add_, neural_points.py:640) and ts_update takes the max (:644)."""
-    dist.all_reduce(cert_delta, op=dist.ReduceOp.SUM, group=group)
-    dist.all_reduce(ts_update, op=dist.ReduceOp.MAX, group=group)
+    all_reduce(cert_delta, group=group)
+    all_reduce(ts_update, op=dist.ReduceOp.MAX, group=group)
 
 
 def adam_scalars(lr, step, eps, beta1=0.9, beta2=0.99, zero_grad=True, grad_stride=8) -> "_lib.PinAdamStep":

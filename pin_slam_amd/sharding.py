@@ -2,23 +2,27 @@
 dense all-reduce of the [L+1, 8] feature gradient (128 MB per iteration at 4M points).
 
 Every rank holds the same local map (the SLAM front end is replicated).  The local-map points
-are split into W slabs along the longer horizontal axis (cuts from a histogram of the
-coordinates, so every rank computes the same cuts), rank r owns slab r and draws its batches
-from the pool samples inside slab r.  Its rows then only reach owned points and the halo: the
-points of other slabs within the query reach (search radius + numerical-gradient step) of slab
-r.  Per iteration (Mapper.mapping with shard="space"):
+are split into W cells: a x b equal-count columns x rows in the horizontal plane (cuts from
+integer histograms of the coordinates, so every rank computes the same cuts; the factor pair
+with the shortest cut length).  Rank r owns cell r and draws its batches from the pool samples
+inside it.  Its rows then only reach owned points, the halo (the points of other cells within
+the query reach -- search radius + numerical-gradient step -- of cell r) and the shared rows
+(local row 1, which the reference's global2local fill quirk makes every non-local candidate
+read).  Per iteration (Mapper.mapping with shard="space"):
 
-  1. exchange_gradients: each rank sends the gradient rows of its halo to their owners, which
-     add them to their own rows (point-to-point with the ranks whose slabs are within reach);
-  2. Adam on the owned rows only (pin_adam_rows);
+  1. exchange_gradients: shared rows' gradients SUM all-reduced (one 32-B row); each rank sends
+     the gradient rows of its halo to their owners, which add them to their own rows
+     (point-to-point with the ranks whose cells are within reach);
+  2. Adam on the owned rows and the shared rows (pin_adam_rows);
   3. exchange_features: owners send the updated rows that other ranks hold as halo.
 
-At the end of mapping(): halo certainty deltas (sum) and ts (max) go to the owners, then the
-owned rows of every rank are all-gathered, so every replica holds the whole updated local map.
+At the end of mapping(): halo certainty deltas (sum) and ts (max) go to the owners (shared rows
+by all-reduce), then the owned rows of every rank are all-gathered, so every replica holds the
+whole updated local map.
 
 With the same batches this is the dense data-parallel step: an owned row's gradient is the sum
-of every rank's contribution (only ranks whose slab is within reach can contribute), and Adam is
-elementwise.  Wire bytes per iteration: 2 x halo rows x 32 B (about 1 MB at 4M points on 8
+of every rank's contribution (only ranks whose cell is within reach can contribute), and Adam
+is elementwise.  Wire bytes per iteration: 2 x halo rows x 32 B (about 1 MB at 4M points on 8
 ranks) instead of 2 x 7/8 x 128 MB.
 """
 import math
@@ -31,10 +35,47 @@ def _ranks(group):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
-class SlabPartition:
-    """Slab ownership of the local-map rows [L, 3] (the padding feature row L is nobody's)."""
+def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
+    """In-place all-reduce; device tensors go through host copies on gloo (CPU tests, 1-GPU
+    rehearsals), directly over RCCL otherwise."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
 
-    def __init__(self, positions: torch.Tensor, reach: float, group=None, bins: int = 4096):
+
+def _factor_pairs(W):
+    return [(a, W // a) for a in range(1, W + 1) if W % a == 0]
+
+
+def _equal_count_cuts(counts_cum, total, parts, lo, span, bins):
+    """parts-1 cut coordinates at histogram bin edges so that each part holds ~total/parts points
+    (integer cumulative counts: every rank computes the same cuts)."""
+    cuts = []
+    for k in range(1, parts):
+        e = int(torch.searchsorted(counts_cum, torch.tensor(k * total / parts, dtype=counts_cum.dtype)))
+        cuts.append(lo + span * (e + 1) / bins)
+    return cuts
+
+
+class SlabPartition:
+    """Ownership of the local-map rows [L, 3] (the padding feature row L is nobody's) by a grid of
+    cells: the map is cut into `a` equal-count columns along x, each column into `b` equal-count
+    cells along y (a x b = W, a k-d split); rank r owns cell (r // b, r % b).  layout "auto"
+    picks the factor pair with the shortest total cut length ((a-1) span_y + (b-1) span_x,
+    proportional to the halo volume), so 8 ranks on a square map become 4 x 2 cells instead of 8
+    thin strips, and a corridor stays 1-D; "1d" cuts only along the longer horizontal axis.
+
+    shared_rows: local rows whose gradient may come from any slab.  The reference's global2local
+    table maps every non-local point to local row 1 (neural_points.py:290-300, the fill quirk):
+    a non-local candidate that passes the travel filter reads and trains row 1 wherever the
+    query is.  Those rows are taken out of the halo lists and handled by tiny all-reduces
+    instead (gradient and certainty delta SUM, ts MAX, Adam applied by every rank)."""
+
+    def __init__(self, positions: torch.Tensor, reach: float, group=None, bins: int = 4096, layout: str = "auto",
+                 shared_rows=(1,)):
         self.group = group
         self.world, self.rank = _ranks(group)
         W = self.world
@@ -44,38 +85,56 @@ class SlabPartition:
         dev = pos.device
         if L == 0:
             raise ValueError("SlabPartition: empty local map")
+        if layout not in ("auto", "1d"):
+            raise ValueError("layout must be 'auto' or '1d'")
         lo = pos.min(0).values.double().cpu()
         hi = pos.max(0).values.double().cpu()
-        self.axis = 0 if (hi[0] - lo[0]) >= (hi[1] - lo[1]) else 1
-        a = pos[:, self.axis].double()
-        a_lo, a_hi = float(lo[self.axis]), float(hi[self.axis])
-        span = max(a_hi - a_lo, 1e-9)
-        # equal-count cuts at histogram bin edges (integer counts: identical on every rank)
-        b = torch.clamp(((a - a_lo) / span * bins).long(), 0, bins - 1)
-        cnt = torch.bincount(b, minlength=bins).cumsum(0).cpu()
-        cuts = []
-        for k in range(1, W):
-            e = int(torch.searchsorted(cnt, torch.tensor(k * L / W, dtype=cnt.dtype)))
-            cuts.append(a_lo + span * (e + 1) / bins)
-        self.cuts = torch.tensor(cuts, dtype=torch.float64)
-        self.bounds = [(-math.inf if r == 0 else cuts[r - 1], math.inf if r == W - 1 else cuts[r]) for r in range(W)]
-        self.reach = float(reach)
-        cuts_d = self.cuts.to(dev)
-        owner = torch.bucketize(a, cuts_d, right=True)          # slab r = [cut_{r-1}, cut_r)
+        span = [max(float(hi[d] - lo[d]), 1e-9) for d in (0, 1)]
+        if layout == "1d":
+            self.shape = (W, 1) if span[0] >= span[1] else (1, W)
+        else:
+            # shortest total cut length; ties to more columns (the 1-D case along x first)
+            self.shape = min(_factor_pairs(W), key=lambda ab: ((ab[0] - 1) * span[1] + (ab[1] - 1) * span[0], -ab[0]))
+        a, b = self.shape
+        x = pos[:, 0].double()
+        y = pos[:, 1].double()
+        bx = torch.clamp(((x - float(lo[0])) / span[0] * bins).long(), 0, bins - 1)
+        xcum = torch.bincount(bx, minlength=bins).cumsum(0).cpu()
+        self.xcuts = torch.tensor(_equal_count_cuts(xcum, L, a, float(lo[0]), span[0], bins), dtype=torch.float64)
+        col = torch.bucketize(x, self.xcuts.to(dev), right=True)          # column c = [xcut_{c-1}, xcut_c)
+        by = torch.clamp(((y - float(lo[1])) / span[1] * bins).long(), 0, bins - 1)
+        ycnt = torch.bincount(col * bins + by, minlength=a * bins).reshape(a, bins).cpu()
+        ycum = ycnt.cumsum(1)
+        ycuts = [_equal_count_cuts(ycum[c], int(ycum[c, -1]), b, float(lo[1]), span[1], bins) for c in range(a)]
+        self.ycuts = torch.tensor(ycuts, dtype=torch.float64).reshape(a, b - 1)
+        owner = self._owner_of(x, y)
         self.owner = owner
-        self.owned = torch.nonzero(owner == self.rank).flatten()
+        # cell boxes [x_lo, x_hi) x [y_lo, y_hi)
+        xe = [-math.inf] + self.xcuts.tolist() + [math.inf]
+        self.boxes = []
+        for r in range(W):
+            c, k = divmod(r, b)
+            ye = [-math.inf] + self.ycuts[c].tolist() + [math.inf]
+            self.boxes.append((xe[c], xe[c + 1], ye[k], ye[k + 1]))
+        self.reach = float(reach)
+        shared = torch.as_tensor([s for s in shared_rows if 0 <= s < L], dtype=torch.long, device=dev)
+        self.shared = shared
+        not_shared = torch.ones(L, dtype=torch.bool, device=dev)
+        not_shared[shared] = False
+        mine = owner == self.rank
+        self.owned = torch.nonzero(mine).flatten()
+        # Adam runs on the owned rows plus the shared rows every rank holds the summed gradient of
+        self.adam_rows = torch.unique(torch.cat((self.owned, shared)))
         self.counts = torch.bincount(owner, minlength=W).cpu().tolist()
-        # halo lists, ordered by row: recv_rows[s] = rows owned by s inside my band (I hold them
-        # as halo), send_rows[s] = my rows inside s's band (s holds them as halo).  Both sides
-        # evaluate the same predicate on the same data, so the lists pair up element by element.
+        # halo lists, ordered by row: recv_rows[s] = rows owned by s inside my reach box (I hold
+        # them as halo), send_rows[s] = my rows inside s's reach box (s holds them as halo).  Both
+        # sides evaluate the same predicate on the same data, so the lists pair up element by element.
         self.recv_rows, self.send_rows = {}, {}
-        mine_lo, mine_hi = self.bounds[self.rank]
         for s in range(W):
             if s == self.rank:
                 continue
-            s_lo, s_hi = self.bounds[s]
-            rr = torch.nonzero((owner == s) & (a >= mine_lo - self.reach) & (a < mine_hi + self.reach)).flatten()
-            sr = torch.nonzero((owner == self.rank) & (a >= s_lo - self.reach) & (a < s_hi + self.reach)).flatten()
+            rr = torch.nonzero((owner == s) & self._in_reach(x, y, self.rank) & not_shared).flatten()
+            sr = torch.nonzero(mine & self._in_reach(x, y, s) & not_shared).flatten()
             if rr.numel() or sr.numel():
                 self.recv_rows[s] = rr
                 self.send_rows[s] = sr
@@ -85,11 +144,29 @@ class SlabPartition:
         # every rank in the first batch_isend_irecv of a group)
         dist.barrier(group=group)
 
+    @property
+    def axis(self):
+        """The cut axis of a 1-D partition (None for a 2-D grid)."""
+        a, b = self.shape
+        return 0 if b == 1 else (1 if a == 1 else None)
+
+    def _owner_of(self, x, y):
+        a, b = self.shape
+        col = torch.bucketize(x, self.xcuts.to(x.device), right=True)
+        if b == 1:
+            return col
+        yc = self.ycuts.to(x.device)[col]                          # [n, b-1] the column's cuts
+        return col * b + (y[:, None] >= yc).sum(1)
+
+    def _in_reach(self, x, y, r):
+        x0, x1, y0, y1 = self.boxes[r]
+        R = self.reach
+        return (x >= x0 - R) & (x < x1 + R) & (y >= y0 - R) & (y < y1 + R)
+
     # ------------------------------------------------------------------ samples
     def sample_mask(self, coords: torch.Tensor) -> torch.Tensor:
         """Samples whose slab (by their coordinate) is this rank's."""
-        a = coords[:, self.axis].double()
-        return torch.bucketize(a, self.cuts.to(coords.device), right=True) == self.rank
+        return self._owner_of(coords[:, 0].double(), coords[:, 1].double()) == self.rank
 
     # ------------------------------------------------------------------ point-to-point
     def _p2p(self, sends, recv_like):
@@ -122,7 +199,12 @@ class SlabPartition:
             recv_like[s].copy_(t)
 
     def exchange_gradients(self, grad: torch.Tensor):
-        """Owners add the halo holders' gradient rows (grad [L+1, F], in place)."""
+        """Shared rows take the sum over ranks; owners add the halo holders' gradient rows
+        (grad [L+1, F], in place)."""
+        if self.shared.numel():
+            g = grad.index_select(0, self.shared)
+            all_reduce(g, group=self.group)
+            grad.index_copy_(0, self.shared, g)
         if not self.recv_rows:
             return
         sends = {s: grad.index_select(0, r) for s, r in self.recv_rows.items()}
@@ -150,7 +232,15 @@ class SlabPartition:
     # ------------------------------------------------------------------ end of mapping()
     def reconcile_side_effects(self, cert_before: torch.Tensor, cert: torch.Tensor, ts: torch.Tensor):
         """Owners add the halo holders' certainty deltas (scatter_add) and take the max of their
-        ts (scatter_reduce amax), neural_points.py:640-644; cert / ts [L] in place on owned rows."""
+        ts (scatter_reduce amax), neural_points.py:640-644; cert / ts [L] in place on owned rows.
+        Shared rows: every rank's delta summed, the max ts."""
+        if self.shared.numel():
+            d = cert.index_select(0, self.shared) - cert_before.index_select(0, self.shared)
+            all_reduce(d, group=self.group)
+            cert.index_copy_(0, self.shared, cert_before.index_select(0, self.shared) + d)
+            t = ts.index_select(0, self.shared)
+            all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            ts.index_copy_(0, self.shared, t)
         if not self.recv_rows:
             return
         delta = cert - cert_before

@@ -100,18 +100,17 @@ def test_data_parallel_mapping_equals_single_process(case):
 
 
 # ------------------------------------------------------------------ spatially sharded mapping
-def _shard_setup():
-    """A small all-local oracle map (surface grid), the mapper fixture's decoder and two seeded
-    batches: surface points + N(0, 0.25^2) along z, label = -offset."""
+def _shard_setup(nx=120, ny=40):
+    """A small all-local oracle map (surface grid nx x ny at 0.3 m), the mapper fixture's decoder
+    and two seeded batches: surface points + N(0, 0.25^2) along z, label = -offset."""
     z = np.load(os.path.join(GOLDEN, "mapper_wf.npz"))
     mlp = O.mlp_from_fixture(z)
     res = 0.3
-    nx, ny = 120, 40
     xs, ys = np.meshgrid((np.arange(nx) + 0.5) * res, (np.arange(ny) + 0.5) * res, indexing="ij")
     pts = np.stack([xs.ravel(), ys.ravel(), 0.5 * np.sin(xs.ravel() / 7) * np.cos(ys.ravel() / 5) + 0.15], -1)
     st = O.empty_map(res, 1 << 20, np.zeros(1, np.float32), 1e9)
     O.map_update(st, pts.astype(np.float32), 0)
-    O.reset_local_map(st, np.array([18.0, 6.0, 0.0]), 0, 1e6)
+    O.reset_local_map(st, np.array([nx * res / 2, ny * res / 2, 0.0]), 0, 1e6)
     rng = np.random.default_rng(3)
     st.local_features[:-1] = rng.normal(0, 0.05, st.local_features[:-1].shape).astype(np.float32)
     batches = []
@@ -136,18 +135,18 @@ def _rank_grad(st, mlp, batch, mask, cfg, n_total):
     return out["feat_grad"].astype(np.float32) * np.float32(mask.sum() / n_total)
 
 
-def _shard_worker(rank, world, port, q):
+def _shard_worker(rank, world, port, q, grid, layout):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from pin_slam_amd.sharding import SlabPartition
-        st, mlp, batches, cfg = _shard_setup()
+        st, mlp, batches, cfg = _shard_setup(*grid)
         reach = float(np.sqrt(cfg["maxd2"])) * 1.001 + cfg["eps"] + 1e-3
-        part = SlabPartition(torch.from_numpy(st.local_points), reach)
+        part = SlabPartition(torch.from_numpy(st.local_points), reach, layout=layout)
         feats = torch.from_numpy(st.local_features)        # shares memory with the oracle state
         m, v = torch.zeros_like(feats), torch.zeros_like(feats)
         cert_before = torch.from_numpy(st.local_certainties.copy())
-        owned = part.owned.numpy()
+        owned = part.adam_rows.numpy()        # owned rows + the shared row (Adam by every rank)
         masks = []
         for it, batch in enumerate(batches):
             mask = part.sample_mask(torch.from_numpy(batch[0])).numpy()
@@ -164,21 +163,25 @@ def _shard_worker(rank, world, port, q):
         part.reconcile_side_effects(cert_before, cert, ts)
         part.gather_owned(feats, cert, ts)
         q.put((rank, feats.numpy().copy(), cert.numpy().copy(), ts.numpy().copy(), masks,
-               int(part.owned.numel()), int(part.halo.numel())))
+               int(part.owned.numel()), int(part.halo.numel()), part.shape))
     finally:
         dist.destroy_process_group()
 
 
-def test_slab_sharded_mapping_equals_dense_data_parallel():
-    """shard='space' (pin_slam_amd.sharding): halo gradients to owners, Adam on owned rows, halo
-    features refreshed, side effects reconciled, owned rows all-gathered -- equals the dense
-    data-parallel step on the same per-rank batches (sum of the ranks' gradients, Adam on every
-    row, summed certainty deltas, max ts) on every replica, over two iterations."""
-    world = 2
+@pytest.mark.parametrize("world,grid,layout,shape", [(2, (120, 40), "auto", (2, 1)),
+                                                    (4, (60, 60), "auto", (2, 2)),
+                                                    (4, (60, 60), "1d", (4, 1))])
+def test_slab_sharded_mapping_equals_dense_data_parallel(world, grid, layout, shape):
+    """shard='space' (pin_slam_amd.sharding): halo gradients to owners, Adam on owned rows (and
+    the shared row), halo features refreshed, side effects reconciled, owned rows all-gathered --
+    equals the dense data-parallel step on the same per-rank batches (sum of the ranks'
+    gradients, Adam on every row, summed certainty deltas, max ts) on every replica, over two
+    iterations.  1-D slabs on a corridor, 2 x 2 cells on a square map (layout auto) and 4 strips
+    on the same square map (layout 1d)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, grid, layout)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -187,9 +190,11 @@ def test_slab_sharded_mapping_equals_dense_data_parallel():
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    st, mlp, batches, cfg = _shard_setup()
+    st, mlp, batches, cfg = _shard_setup(*grid)
     L = st.local_points.shape[0]
-    assert sum(r[5] for r in res) == L and all(0 < r[6] < L // 4 for r in res)   # owners partition; small halos
+    assert all(r[7] == shape for r in res)
+    assert sum(r[5] for r in res) == L and all(0 < r[6] < L // 2 for r in res)   # owners partition; small halos
+    assert all(abs(r[5] - L / world) < 0.05 * L / world for r in res)            # equal-count cells
     m, v = np.zeros_like(st.local_features), np.zeros_like(st.local_features)
     cert0 = st.local_certainties.copy()
     cert_delta = np.zeros_like(cert0)

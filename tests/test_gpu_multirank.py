@@ -1,0 +1,174 @@
+"""Multi-rank Mapper.mapping on the GPU: two ranks share cuda:0 over gloo (as
+tools/rehearse_multi.sh does; the scaling run uses one rank per GPU over RCCL) and run the
+whole fused mapping() call end to end with shard="dense" (SUM all-reduce of the feature /
+decoder gradients) and shard="space" (slab ownership, halo exchange, shared row, Adam on owned
+rows, all-gather of the owned rows).
+
+Oracle: one process on the union of the same batches.  Every train_step of each rank is
+recorded (pool rows drawn, row scales); the single process replays, per iteration, both ranks'
+calls into one gradient accumulator with those scales and takes one Adam step over every row --
+the data-parallel step the collectives must implement.  The replicas must end bit-identical to
+each other; against the single process the features differ only by the float-atomic summation
+order amplified by fresh Adam (a near-zero gradient moves an element by +-lr on its sign):
+more than 1e-4 on at most 0.5 % of the elements and ||diff|| <= 3e-3 ||features moved|| (the
+tolerances of tests/test_gpu_mapper.py's whole-call test), decoder 1e-4 relative, certainties
+rel 1e-5 of their max, ts exact."""
+import os
+import socket
+import warnings
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+ITERS = 4
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _state(nm, dec):
+    return dict(feats=nm.local_geo_features.data.cpu().numpy().copy(),
+                cert=nm.local_point_certainties.cpu().numpy().copy(),
+                ts=nm.local_point_ts_update.cpu().numpy().copy(),
+                dec=[p.detach().cpu().numpy().copy() for p in dec.parameters()])
+
+
+def _worker(rank, world, port, case, shard, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from tests.replay import ReplayDraws
+        from tests.test_gpu_mapper import _mapping_call_setup
+        z = dict(np.load(os.path.join(GOLDEN, f"{case}.npz")))
+        nm, dec, mapper, _ = _mapping_call_setup(z, "cuda", "grid")
+        mapper.group = dist.group.WORLD
+        mapper.shard = shard
+        draws = ReplayDraws(7000 + 31 * rank)
+        mapper._randint = lambda high, k: torch.from_numpy(draws.randint(high, k)).to("cuda")
+        calls = []
+        step = mapper.train_step
+
+        def recorded(*a, **kw):
+            calls.append(dict(index=kw["index"].cpu().numpy(), scale=kw.get("scale"), n_tail=int(kw.get("n_tail", 0)),
+                              scale_tail=float(kw.get("scale_tail", 0.0)), world=int(a[5])))
+            return step(*a, **kw)
+        mapper.train_step = recorded
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            mapper.mapping(ITERS)
+        torch.cuda.synchronize()
+        part = getattr(mapper, "_partition", None)
+        out = _state(nm, dec)
+        out.update(calls=calls, warnings=[str(w.message) for w in caught],
+                   part=None if part is None else dict(shape=part.shape, owned=int(part.owned.numel()),
+                                                       halo=int(part.halo.numel()),
+                                                       shared=part.shared.cpu().tolist()))
+        q.put((rank, out))    # numpy only: tensors travel as shared-memory handles that die with this process
+    except BaseException as e:           # report instead of leaving the parent waiting on the queue
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _single_process(case, calls, dev):
+    """The union of the ranks' batches in one process: per iteration every rank's train_step into
+    one accumulator (reduce=False, the rank's scales), then one Adam step over all rows."""
+    from tests.test_gpu_mapper import _mapping_call_setup
+    from pin_slam_amd import _lib
+    z = dict(np.load(os.path.join(GOLDEN, f"{case}.npz")))
+    nm, dec, mapper, _ = _mapping_call_setup(z, dev, "grid")
+    fdata = nm.local_geo_features.data
+    feats0 = fdata.cpu().numpy().copy()
+    f_grad, f_m, f_v = (torch.zeros_like(fdata) for _ in range(3))
+    mlp_params = [p for p in dec.parameters() if p.requires_grad]
+    m_grad = m_m = m_v = None
+    if mlp_params:
+        m_grad = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+        m_m, m_v = torch.zeros_like(m_grad), torch.zeros_like(m_grad)
+    mapper._adam_t = 0
+    for it in range(ITERS):
+        for r in range(WORLD):
+            c = calls[r][it]
+            scale = c["scale"] if c["scale"] is not None else 1.0 / c["world"]
+            mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, f_grad, m_grad, 1,
+                              index=torch.from_numpy(c["index"]).to(dev), reduce=False, scale=scale, n_tail=c["n_tail"],
+                              scale_tail=c["scale_tail"], weight=mapper.weight_pool)
+        mapper._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
+    torch.cuda.synchronize()
+    return _state(nm, dec), feats0, mapper
+
+
+def _run(case, shard):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, case, shard, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(WORLD))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(WORLD):
+        assert isinstance(res[r], dict), f"rank {r}: {res[r]}"
+    assert all(p.exitcode == 0 for p in procs)
+    return res
+
+
+def _norm(a):
+    return float(np.linalg.norm(np.asarray(a, dtype=np.float64).ravel()))
+
+
+@pytest.mark.parametrize("case,shard", [("mapping_wf", "dense"), ("mapping_wf", "space"),
+                                        ("mapping_wf_frozen", "space"), ("mapping_nwf_weighted", "space")])
+def test_multirank_mapping_equals_union_of_batches(case, shard):
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    res = _run(case, shard)
+    r0, r1 = res[0], res[1]
+    calls = [r0["calls"], r1["calls"]]
+    assert all(len(c) == ITERS for c in calls)
+    if shard == "space":
+        assert r0["part"] is not None and not any("dense" in w for w in r0["warnings"]), r0["warnings"]
+        assert r0["part"]["shared"] == [1]
+        assert r0["part"]["owned"] + r1["part"]["owned"] == r0["feats"].shape[0] - 1
+    else:
+        assert r0["part"] is None
+    # replicas agree bit for bit
+    for key in ("feats", "cert", "ts"):
+        np.testing.assert_array_equal(r0[key], r1[key], err_msg=key)
+    for a, b in zip(r0["dec"], r1["dec"]):
+        np.testing.assert_array_equal(a, b)
+    ref, feats0, mapper = _single_process(case, calls, "cuda")
+    if shard == "space":
+        # the slab scales keep the union an unbiased estimate of one batch: sum_r scale_h,r bs_hist,r / bs_hist = 1
+        c = mapper.config
+        n_new = int(mapper.new_idx.numel())
+        bs_hist = int(c.bs) - min(n_new, int(c.bs_new_sample))
+        tot = sum(calls[r][0]["scale"] * (calls[r][0]["index"].size - calls[r][0]["n_tail"]) for r in range(WORLD))
+        assert tot / bs_hist == pytest.approx(1.0, rel=1e-9)
+    moved = _norm(ref["feats"] - feats0)
+    d = r0["feats"] - ref["feats"]
+    frac = float((np.abs(d) > 1e-4).mean())
+    assert frac <= 5e-3, frac
+    assert _norm(d) <= 3e-3 * moved, (_norm(d), moved)
+    for a, b in zip(r0["dec"], ref["dec"]):
+        assert _norm(a - b) <= 1e-4 * max(_norm(b), 1e-12)
+    np.testing.assert_allclose(r0["cert"], ref["cert"], rtol=1e-5, atol=1e-5 * float(np.abs(ref["cert"]).max()))
+    np.testing.assert_array_equal(r0["ts"], ref["ts"])

@@ -402,14 +402,16 @@ def test_tracking_loop_fixture(golden, dev, case):
     cfg.reg_iter_n = int(z["reg_iter_n"])
     tr = Tracker(cfg, nm, dec)
     hist = []
-    step = tr.registration_step
+    step = tr._register           # one registration step of the loop (query, normal equations, solve)
 
     def recording_step(*a, **kw):
         out = step(*a, **kw)
-        hist.append((_np(out[0]), float(out[5]), int(out[4].shape[0])))
+        st = out["status"]
+        solved = st[4] > 0
+        hist.append((_np(out["delta"]) if solved else np.eye(4), float(st[1]) if solved else 0.0, int(st[0])))
         return out
 
-    tr.registration_step = recording_step
+    tr._register = recording_step
     src = torch.as_tensor(z["source"], device=dev)
     T, cov, _, valid = tr.tracking(src, torch.eye(4, dtype=torch.float64, device=dev), cur_ts=9)
     assert len(hist) == z["tracking_delta_T"].shape[0]

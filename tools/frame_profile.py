@@ -45,10 +45,8 @@ def main(frames=8):
             return out
         return wrap
     TR.fused_query_sdf = timed("query_sdf", Q.query_sdf)
-    TR._reg_accumulate = timed("reg_accumulate", TR._reg_accumulate)
-    TR._solve = timed("solve", TR._solve)
-    tracker.registration_step = timed("registration_step", tracker.registration_step)
-    TR.transform_torch = timed("transform", TR.transform_torch)
+    tracker._register = timed("_register", tracker._register)
+    TR.transform_points = timed("transform", TR.transform_points)
     loop.read_and_preprocess(scans[frames - 1])
     src = loop.cur_source_points
     torch.cuda.synchronize()
