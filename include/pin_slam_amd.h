@@ -444,10 +444,14 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
                       const float* coord, const int64_t* ts, const PinTrainCfg* cfg, const PinTrainState* st,
                       void* stream);
 
+/* per-block decoder-gradient partial of pin_train_backward: the products T[64][16] and T'[64][16]
+ * over the block's rows, then sum so (see k_mlp_grad_final) */
+#define PIN_MLP_PART_FLOATS (2 * PIN_HIDDEN_DIM * 16 + 16)
+
 /* Workspace bytes of pin_train_backward for rows = n_main + 6 n_stencil. */
 static inline int64_t pin_train_workspace_bytes(int64_t rows) {
     const int64_t nblk = (rows + 255) / 256;
-    return nblk * 4 * 8 + nblk * PIN_MLP_GRAD_SIZE * 4;
+    return nblk * 4 * 8 + nblk * PIN_MLP_PART_FLOATS * 4;
 }
 
 /*
@@ -465,6 +469,13 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 /* pin_adam_step -- dense Adam over n floats in place (torch.optim.Adam, weight_decay 0). */
 int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
                   void* stream);
+
+/* pin_adam_segments -- the same Adam update over nseg (<= 8) separate parameter tensors params[k]
+ * of sizes[k] floats whose gradients and moments lie end to end in contiguous grad / exp_avg /
+ * exp_avg_sq (the decoder's W1, b1, W2, b2 against pin_train_backward's mlp_grad): one launch
+ * for what torch.optim.Adam does per parameter (utils/tools.py:89-116).  grad_stride must be 8. */
+int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, float* grad, float* exp_avg,
+                      float* exp_avg_sq, const PinAdamStep* a, void* stream);
 
 /* pin_adam_rows -- the same Adam update on the listed rows only of [rows, 8] contiguous arrays
  * (param, grad, exp_avg, exp_avg_sq; grad_stride must be 8); those rows' gradients are zeroed

@@ -100,6 +100,7 @@ class PinMapArrays(ctypes.Structure):
 
 
 MLP_GRAD_SIZE = HIDDEN_DIM * (FEATURE_DIM + 3) + 2 * HIDDEN_DIM + 1
+MLP_PART_FLOATS = 2 * HIDDEN_DIM * 16 + 16   # PIN_MLP_PART_FLOATS: per-block decoder-gradient partial
 
 _P = ctypes.POINTER
 # name -> (argtypes) ; every function returns int
@@ -151,6 +152,7 @@ _SIGS = {
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_adam_rows": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
+    "pin_adam_segments": [_P(c_void_p), _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
     "pin_map_workspace_bytes": [i64],
     "pin_voxel_down_sample": [c_void_p, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_map_insert": [c_void_p, c_void_p, i64, f32, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, i64, f32, f32,

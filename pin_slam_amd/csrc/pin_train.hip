@@ -578,10 +578,15 @@ k_train_forward_eik_grid(const PinGrid g, const PinPoints p, const PinMlp m, con
 
 // backward: one row per lane for the decoder; the row's k x 8 feature-gradient terms are staged
 // in LDS and scattered with 64 lanes covering 8 rows x 32 contiguous bytes per instruction.
-// Decoder-parameter gradients: wave shuffle sums -> per-block partials (fixed order, no
-// same-address atomics) -> k_mlp_grad_final.
+// Decoder-parameter gradients (a training decoder): GEMMs over the rows on the f32 matrix cores
+// (mlp_grad_mfma) -> per-block partials (fixed order, no same-address atomics) ->
+// k_mlp_grad_final, which also turns the reduced products into dW1, db1, dW2, db2.
 constexpr int kMlpGrad = PIN_MLP_GRAD_SIZE;
 constexpr int kWaves = kBlock / 64;
+constexpr int kTSize = kH * 16;                 // T[c][i], i < 16 (12 used)
+constexpr int kMlpPart = PIN_MLP_PART_FLOATS;   // per block: T, T' (analytic eikonal), sum so
+static_assert(kMlpPart >= 2 * kTSize + 1, "decoder-gradient partial layout");
+constexpr int kMgWave = 128 + 2 * 1024;         // per-wave LDS of mlp_grad_mfma: masks, B, E
 
 __device__ __forceinline__ float wave_sum_f(float v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -589,13 +594,11 @@ __device__ __forceinline__ float wave_sum_f(float v) {
 }
 
 // decoder backward of one input row x with upstream dL/d(out) = so (already times sdf_scale):
-// gf += sum_c delta_c W1[c][0:8]; decoder-parameter terms summed over the wave into mw (lane 0)
-// EXTRA (analytic eikonal): e = dL/d(gx) of the row (dsdf/dx through the mask-linear path,
-// gx = s W1^T (w2 o 1[pre > 0])): dW1[c][i] += s w2_c 1[pre_c > 0] e_i, dw2_c += s 1[pre_c > 0] W1[c] . e
-template <bool MLP_GRAD, bool EXTRA = false>
-__device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)[kD], float so, float (&gf)[kF],
-                                                 float* __restrict__ mw, bool accumulate,
-                                                 const float* __restrict__ e = nullptr) {
+// gf += sum_c delta_c W1[c][0:8], delta_c = so w2_c 1[pre_c > 0].  Returns the row's 64 ReLU
+// masks (bit c) for the decoder-parameter products (mlp_grad_mfma).
+__device__ __forceinline__ uint64_t decoder_backward_row(const MlpW& m, const float (&x)[kD], float so,
+                                                         float (&gf)[kF]) {
+    uint32_t lo = 0u, hi = 0u;
 #pragma unroll 2
     for (int cc = 0; cc < kH; ++cc) {
         float wr[kWRow];
@@ -608,29 +611,118 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
         const float delta = on ? so * m.w[kWW2 + cc] : 0.f;
 #pragma unroll
         for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
-        if (MLP_GRAD) {
-            float dw[kD + 2];
-            const float de = (EXTRA && on) ? m.sdf_scale * m.w[kWW2 + cc] : 0.f;
-            float ew = 0.f;
-            if (EXTRA) {
+        const uint32_t bit = on ? 1u << (cc & 31) : 0u;
+        if (cc < 32) lo |= bit; else hi |= bit;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// The decoder-parameter gradients of the wave's 64 rows (one lane per row) as products over the
+// rows, accumulated on v_mfma_f32_16x16x4_f32 (exact f32 products, f32 sums):
+//   T[c][i]  += sum_r 1[pre_c(r) > 0] so(r) [x(r), 1]_i        (i < 12)
+//   T'[c][i] += sum_r 1[pre_c(r) > 0] e_i(r)                    (EXTRA: the analytic eikonal's
+//                                                                dL/d(gx) of each row, gx = s W1^T (w2 o 1))
+// from which k_mlp_grad_final forms dW1[c][i] = w2_c (T + s T')[c][i], db1_c = w2_c T[c][11],
+// dW2_c = W1[c] . (T + s T')[c][0:11] + b1_c T[c][11].  A = the 0/1 masks (hidden c x row), B =
+// the rows' values (row x i), staged through the wave's LDS slice ws (kMgWave floats) transposed
+// so that a lane's 16 k-steps (rows 4 ks + g) are contiguous.  Every lane of the wave calls this.
+template <bool EXTRA>
+__device__ __forceinline__ void mlp_grad_mfma(float* ws, uint64_t mask, float so, const float (&x)[kD],
+                                              const float* e, f32x4 (&accT)[4], f32x4 (&accE)[4]) {
+    const int lane = threadIdx.x & 63;
+    const int slot = (lane & 3) * 16 + (lane >> 2);   // row r -> [g = r & 3][ks = r >> 2]
+    uint32_t* wm = (uint32_t*)ws;                      // [2 halves][64]
+    float* wb = ws + 128;                              // [16 i][64]
+    float* we = ws + 128 + 1024;                       // [16 i][64]
+    wave_lds_sync();   // the previous call's readers are done
+    wm[slot] = (uint32_t)mask;
+    wm[64 + slot] = (uint32_t)(mask >> 32);
 #pragma unroll
-                for (int i = 0; i < kD; ++i) ew = fmaf(wr[i], e[i], ew);
-            }
+    for (int i = 0; i < kD; ++i) wb[i * 64 + slot] = so * x[i];
+    wb[kD * 64 + slot] = so;
 #pragma unroll
-            for (int i = 0; i < kD; ++i) dw[i] = wave_sum_f(EXTRA ? fmaf(de, e[i], delta * x[i]) : delta * x[i]);
-            dw[kD] = wave_sum_f(delta);                       // b1
-            dw[kD + 1] = wave_sum_f(on ? (EXTRA ? fmaf(m.sdf_scale, ew, so * pre) : so * pre) : 0.f);   // W2
-            if ((threadIdx.x & 63) == 0) {
+    for (int i = kD + 1; i < 16; ++i) wb[i * 64 + slot] = 0.f;
+    if (EXTRA) {
 #pragma unroll
-                for (int i = 0; i < kD; ++i) mw[cc * kD + i] = (accumulate ? mw[cc * kD + i] : 0.f) + dw[i];
-                mw[kH * kD + cc] = (accumulate ? mw[kH * kD + cc] : 0.f) + dw[kD];
-                mw[kH * kD + kH + cc] = (accumulate ? mw[kH * kD + kH + cc] : 0.f) + dw[kD + 1];
+        for (int i = 0; i < kD; ++i) we[i * 64 + slot] = e[i];
+#pragma unroll
+        for (int i = kD; i < 16; ++i) we[i * 64 + slot] = 0.f;
+    }
+    wave_lds_sync();
+    const int n = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int kq = 0; kq < 4; ++kq) {
+        const float4 b4 = *(const float4*)(wb + n * 64 + g * 16 + 4 * kq);
+        const uint4 lo4 = *(const uint4*)(wm + g * 16 + 4 * kq);
+        const uint4 hi4 = *(const uint4*)(wm + 64 + g * 16 + 4 * kq);
+        float4 e4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (EXTRA) e4 = *(const float4*)(we + n * 64 + g * 16 + 4 * kq);
+        const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+        const float ev[4] = {e4.x, e4.y, e4.z, e4.w};
+        const uint32_t lv[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+        const uint32_t hv[4] = {hi4.x, hi4.y, hi4.z, hi4.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) {
+                const uint32_t w = ct < 2 ? lv[s] : hv[s];
+                const float a = (float)((w >> ((16 * ct + n) & 31)) & 1u);
+                accT[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[s], accT[ct], 0, 0, 0);
+                if (EXTRA) accE[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, ev[s], accE[ct], 0, 0, 0);
             }
         }
     }
-    if (MLP_GRAD) {
-        const float v = wave_sum_f(so);
-        if ((threadIdx.x & 63) == 0) mw[kMlpGrad - 1] = (accumulate ? mw[kMlpGrad - 1] : 0.f) + v;  // b2
+}
+
+// End of the block: the waves' T (T') and sum so into the block's partial (fixed order).
+// s_mg: [kWaves][kMgWave]; all threads call this.
+template <bool EXTRA>
+__device__ __forceinline__ void mlp_grad_flush(float (*s_mg)[kMgWave], float* s_so, const f32x4 (&accT)[4],
+                                               const f32x4 (&accE)[4], float so_sum, float* __restrict__ part) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n = lane & 15, g = lane >> 4;
+    const float s = wave_sum_f(so_sum);
+    wave_lds_sync();
+    float* tw = s_mg[wave] + 128;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = 16 * ct + 4 * g + j;   // accumulator row -> hidden unit, column -> i
+            tw[c * 16 + n] = accT[ct][j];
+            if (EXTRA) tw[kTSize + c * 16 + n] = accE[ct][j];
+        }
+    if (lane == 0) s_so[wave] = s;
+    __syncthreads();
+    constexpr int nval = EXTRA ? 2 * kTSize : kTSize;
+    for (int e = threadIdx.x; e < nval; e += kBlock) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += s_mg[w][128 + e];
+        part[e] = v;
+    }
+    if (threadIdx.x == 0) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v += s_so[w];
+        part[2 * kTSize] = v;
+    }
+}
+
+// decoder backward of one input row x with upstream dL/d(out) = so (already times sdf_scale),
+// frozen decoder: gf += sum_c delta_c W1[c][0:8]
+__device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)[kD], float so, float (&gf)[kF]) {
+#pragma unroll 2
+    for (int cc = 0; cc < kH; ++cc) {
+        float wr[kWRow];
+        load_row(m.w, cc, wr);
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kD; ++i) acc = fmaf(wr[i], x[i], acc);
+        const float pre = acc + m.w[kWB1 + cc];
+        const float delta = pre > 0.f ? so * m.w[kWW2 + cc] : 0.f;
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
     }
 }
 
@@ -651,7 +743,8 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
     constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
     __shared__ float gst[kBlock * kJ * kF];
-    __shared__ float mlds[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMlpGrad : 1];
+    __shared__ float s_mg[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMgWave : 1];
+    __shared__ float s_so[kWaves];
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[kDecode ? kPkBytes / 16 : 1];
     __shared__ float s_dsdf[WF && EIK ? kBlock : 1];
@@ -671,7 +764,12 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     loss *= (double)rs;
     if (EIK && live) loss += (double)st.eik_vec[r * (WF ? kEikWf : kEikNwf) + (WF ? 11 : 3)];   // (|g| - 1)^2 term
     const float so = dsdf * mlpw.sdf_scale;           // dL/d(lout output)
-    float* mw = MLP_GRAD ? mlds[wave] : nullptr;
+    // decoder-parameter products of the block's rows (MLP_GRAD): T, T' accumulators, sum so
+    f32x4 accT[4], accE[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) accT[ct] = accE[ct] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float so_sum = 0.f;
+    float* mws = MLP_GRAD ? s_mg[wave] : nullptr;
     if (WF && EIK) {
         // feature terms (w_j dsdf + alpha_j) gx[0:8] in the scatter; gx from the forward
         const float* ev = st.eik_vec + (live ? r : 0) * kEikWf;
@@ -685,7 +783,11 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                 x[d] = live ? st.x[r * kD + d] : 0.f;
                 e[d] = live ? ev[d] : 0.f;
             }
-            decoder_backward<MLP_GRAD, true>(mlpw, x, so, gf, mw, false, e);
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gf[d] = 0.f;
+            const uint64_t mk = decoder_backward_row(mlpw, x, so, gf);   // gf unused: gx came from the forward
+            mlp_grad_mfma<true>(mws, mk, so, x, e, accT, accE);
+            so_sum += so;
         }
     } else if (WF && MF) {
 #pragma unroll
@@ -697,7 +799,13 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         float gf[kF];
 #pragma unroll
         for (int d = 0; d < kF; ++d) gf[d] = 0.f;
-        decoder_backward<MLP_GRAD>(mlpw, x, so, gf, mw, false);
+        if (MLP_GRAD) {
+            const uint64_t mk = decoder_backward_row(mlpw, x, so, gf);
+            mlp_grad_mfma<false>(mws, mk, so, x, nullptr, accT, accE);
+            so_sum += so;
+        } else {
+            decoder_backward(mlpw, x, so, gf);
+        }
 #pragma unroll
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = gf[d];
     } else {
@@ -747,9 +855,17 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                 e[kF] = w * u0;
                 e[kF + 1] = w * u1;
                 e[kF + 2] = w * u2;
-                decoder_backward<true, true>(mlpw, x, coef * mlpw.sdf_scale, gf, mw, j > 0, e);
-            } else if (__any(ok) || MLP_GRAD) {
-                decoder_backward<MLP_GRAD>(mlpw, x, coef * mlpw.sdf_scale, gf, mw, j > 0);
+                const float soj = coef * mlpw.sdf_scale;
+                const uint64_t mk = decoder_backward_row(mlpw, x, soj, gf);
+                mlp_grad_mfma<true>(mws, mk, soj, x, e, accT, accE);
+                so_sum += soj;
+            } else if (MLP_GRAD) {
+                const float soj = coef * mlpw.sdf_scale;
+                const uint64_t mk = decoder_backward_row(mlpw, x, soj, gf);
+                mlp_grad_mfma<false>(mws, mk, soj, x, nullptr, accT, accE);
+                so_sum += soj;
+            } else if (__any(ok)) {
+                decoder_backward(mlpw, x, coef * mlpw.sdf_scale, gf);
             }
 #pragma unroll
             for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
@@ -763,15 +879,8 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         }();
         if ((threadIdx.x & 63) == 0 && loss_part) loss_part[(int64_t)blockIdx.x * kWaves + wave] = v;
     }
+    if constexpr (MLP_GRAD) mlp_grad_flush<EIK>(s_mg, s_so, accT, accE, so_sum, mlp_part + (int64_t)blockIdx.x * kMlpPart);
     __syncthreads();
-    if (MLP_GRAD) {
-        for (int e = threadIdx.x; e < kMlpGrad; e += kBlock) {
-            float v = 0.f;
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) v += mlds[w][e];
-            mlp_part[(int64_t)blockIdx.x * kMlpGrad + e] = v;
-        }
-    }
     if (!grad_features) return;
     // scatter: element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour)
     // pairs x 32 contiguous bytes, one memory-side request each -- the cheapest atomic shape
@@ -819,14 +928,59 @@ __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ 
     }
 }
 
-// mlp_grad[e] += sum_b part[b][e], fixed order
-__global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk,
-                                                           float* __restrict__ out) {
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    if (e >= kMlpGrad) return;
-    float v = 0.f;
-    for (int64_t b = 0; b < nblk; ++b) v += part[b * kMlpGrad + e];
-    out[e] += v;
+// Decoder-parameter gradients from the blocks' partials (fixed order): block b reduces hidden
+// units 4b..4b+3 (64 products of T, and of T' with the analytic eikonal), 4 waves over interleaved
+// block ranges, then mlp_grad += dW1 = w2 o (T + s T')[:, 0:11], db1 = w2 o T[:, 11],
+// dW2 = rowwise W1 . (T + s T')[:, 0:11] + b1 o T[:, 11]; block 0 also adds db2 = sum so.
+__global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk, int extra,
+                                                           PinMlp m, float* __restrict__ out) {
+    __shared__ float red[kWaves][2][64];
+    __shared__ float s_b2[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = 4 * blockIdx.x + (lane >> 4), i = lane & 15;
+    const int e = c * 16 + i;
+    float t = 0.f, te = 0.f, b2 = 0.f;
+#pragma unroll 8
+    for (int64_t b = wave; b < nblk; b += kWaves) {
+        const float* pb = part + b * kMlpPart;
+        t += pb[e];
+        if (extra) te += pb[kTSize + e];
+    }
+    if (blockIdx.x == 0) {
+        for (int64_t b = threadIdx.x; b < nblk; b += kBlock) b2 += part[b * kMlpPart + 2 * kTSize];
+        b2 = wave_sum_f(b2);
+        if (lane == 0) s_b2[wave] = b2;
+    }
+    red[wave][0][lane] = t;
+    red[wave][1][lane] = te;
+    __syncthreads();
+    if (wave != 0) return;
+    t = 0.f;
+    te = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        t += red[w][0][lane];
+        te += red[w][1][lane];
+    }
+    const float w2 = m.W2[c];
+    const float v = fmaf(m.sdf_scale, te, t);
+    float d2 = 0.f;
+    if (i < kD) {
+        out[c * kD + i] += w2 * v;
+        d2 = m.W1[c * kD + i] * v;
+    } else if (i == kD) {
+        out[kH * kD + c] += w2 * t;
+        d2 = m.b1[c] * t;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) d2 += __shfl_xor(d2, off);   // the 16 lanes of hidden unit c
+    if (i == 0) out[kH * kD + kH + c] += d2;
+    if (blockIdx.x == 0 && lane == 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) s += s_b2[w];
+        out[kMlpGrad - 1] += s;
+    }
 }
 
 // torch.optim.Adam (single-tensor form, weight_decay 0), four elements per thread:
@@ -889,9 +1043,52 @@ k_adam_rows(float* __restrict__ prm, float* __restrict__ grad, float* __restrict
     if (a.zero_grad) *(float4*)(grad + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// Adam over up to kMaxSeg separate parameter tensors whose gradients / moments lie end to end in
+// contiguous grad / m / v (the decoder's W1, b1, W2, b2 after one backward): one launch for all.
+constexpr int kMaxSeg = 8;
+struct AdamSegs {
+    float* p[kMaxSeg];
+    int64_t off[kMaxSeg + 1];
+    int n;
+};
+
+__global__ void __launch_bounds__(kBlock)
+k_adam_segments(AdamSegs sg, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, PinAdamStep a) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= sg.off[sg.n]) return;
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxSeg; ++k) s += (k < sg.n && t >= sg.off[k]) ? 1 : 0;
+    float* prm = sg.p[s] + (t - sg.off[s]);
+    float p = *prm, m = m_[t], v = v_[t];
+    adam_one(p, grad[t], m, v, a);
+    *prm = p;
+    m_[t] = m;
+    v_[t] = v;
+    if (a.zero_grad) grad[t] = 0.f;
+}
+
 }  // namespace
 
 extern "C" {
+
+int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, float* grad, float* exp_avg,
+                      float* exp_avg_sq, const PinAdamStep* a, void* stream) {
+    if (!a || !params || !sizes || nseg < 1 || nseg > kMaxSeg || !grad || !exp_avg || !exp_avg_sq) return PIN_ERR_ARG;
+    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
+    AdamSegs sg{};
+    sg.n = nseg;
+    sg.off[0] = 0;
+    for (int k = 0; k < nseg; ++k) {
+        if (sizes[k] < 0 || (sizes[k] > 0 && !params[k])) return PIN_ERR_ARG;
+        sg.p[k] = params[k];
+        sg.off[k + 1] = sg.off[k] + sizes[k];
+    }
+    if (sg.off[nseg] == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_adam_segments, grid_for(sg.off[nseg]), dim3(kBlock), 0, as_stream(stream), sg, grad, exp_avg,
+                       exp_avg_sq, *a);
+    return launch_status();
+}
 
 int pin_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, const int64_t* rows, int64_t nrows,
                   const PinAdamStep* a, void* stream) {
@@ -988,6 +1185,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     const int64_t nblk = g.x;
     double* lpart = loss_out ? (double*)workspace : nullptr;
     float* mpart = mlp_grad ? (float*)((char*)workspace + nblk * kWaves * sizeof(double)) : nullptr;
+    const int extra = (cfg->flags & PIN_TRAIN_EIK) ? 1 : 0;
 #define PIN_LAUNCH_BWD(WF, MG)                                                                               \
     hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
@@ -1019,9 +1217,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
     if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
-    if (mlp_grad)
-        hipLaunchKernelGGL(k_mlp_grad_final, dim3((kMlpGrad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, mpart, nblk,
-                           mlp_grad);
+    if (mlp_grad) hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4), dim3(kBlock), 0, s, mpart, nblk, extra, *mlp, mlp_grad);
     return launch_status();
 }
 

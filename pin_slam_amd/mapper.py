@@ -79,7 +79,7 @@ class _TrainBuffers:
             self.label = torch.empty((rows,), dtype=torch.float32, device=device)
             self.ts = torch.empty((rows,), dtype=torch.int64, device=device)
             nblk = (rows + 255) // 256
-            self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_GRAD_SIZE * 4,), dtype=torch.uint8,
+            self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_PART_FLOATS * 4,), dtype=torch.uint8,
                                          device=device)
             self.loss = torch.zeros((1,), dtype=torch.float64, device=device)
             self.wrow = torch.empty((rows,), dtype=torch.float32, device=device)
@@ -642,15 +642,17 @@ class Mapper:
         feats = self.neural_points.local_geo_features
         self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
         if m_grad is not None:
-            off = 0
+            # the decoder's parameters in one launch: their gradients / moments lie end to end
             for p in mlp_params:
-                k = p.numel()
-                pd = p.data
-                if not (pd.is_contiguous() and pd.dtype == torch.float32):
+                if not (p.data.is_contiguous() and p.data.dtype == torch.float32):
                     raise RuntimeError("decoder parameters must be contiguous float32")
-                _lib.call("pin_adam_step", _lib.ptr(pd), _lib.ptr(m_grad[off:off + k]), _lib.ptr(m_m[off:off + k]),
-                          _lib.ptr(m_v[off:off + k]), k, ctypes.byref(st), s)
-                off += k
+            n = len(mlp_params)
+            ptrs = (ctypes.c_void_p * n)(*[p.data.data_ptr() for p in mlp_params])
+            sizes = (ctypes.c_int64 * n)(*[p.numel() for p in mlp_params])
+            if sum(sizes) != m_grad.numel():
+                raise RuntimeError("decoder parameters do not match the gradient layout")
+            _lib.call("pin_adam_segments", ptrs, sizes, n, _lib.ptr(m_grad), _lib.ptr(m_m), _lib.ptr(m_v),
+                      ctypes.byref(st), s)
             # the step wrote through raw pointers: bump the versions so views built on the
             # parameters (the matrix-core operand image of mlp_view) are rebuilt before the next use
             for p in mlp_params:
