@@ -5,8 +5,11 @@ Workload (BASELINE.json configs[1]): synthetic 1M-point
 surface map (1000 x 1000 voxels of 0.3 m, hash table B = 5e7), 262,144 queries
 per step = map points + N(0, 0.25^2), Kc = 33 cells (num_nei_cells 2, alpha 0.2),
 k = 8, F = 8, decoder 11 -> 64 -> 1, weighted_first, fp32, query_locally=False.
-One step = Tracker/Mesher's fused query over the batch (pin_query_sort: the queries
-counting-sorted into spatial tiles, then one pin_query_sdf_grid_sorted launch), inputs resident in HBM.  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
+One step = the Tracker's fused query over the batch (pin_query_sort: the queries counting-sorted
+into spatial tiles, then one pin_query_sdf_grid_sorted launch whose outputs stay in tile order,
+PIN_QUERY_OUT_TILE, as the registration's normal equations consume them), inputs resident in HBM;
+the same step with the outputs scattered back to input order (what a generic query_sdf caller
+gets) is reported beside it as "input_order".  Multi-GPU: one process per GPU, each rank queries its own 262,144-point
 batch against its replica of the map ("weak" scaling, no data-path collective);
 the barrier + max-over-ranks timing is the only collective.
 
@@ -194,10 +197,11 @@ def cpu_baseline(nm, dec, q, wf):
                       f"({t:.3f} s each)"}
 
 
-def time_kernel(nm, dec, q, wf, backend, steps):
+def time_kernel(nm, dec, q, wf, backend, steps, flags=1):
     """Mean duration (ms) of the headline kernel alone -- HIP events on the launch stream around
-    each pin_query_sdf(_grid) launch, with the tile order precomputed -- and of the ordering pass
-    (pin_query_sort) that each step also runs."""
+    each pin_query_sdf(_grid) launch, with the tile order precomputed; flags 1: outputs in tile
+    order (PIN_QUERY_OUT_TILE), 0: in input order -- and of the ordering pass (pin_query_sort) that
+    each step also runs."""
     import ctypes  # noqa: F401
     from pin_slam_amd import _lib
     from pin_slam_amd.query import mlp_view, query_sort
@@ -213,8 +217,8 @@ def time_kernel(nm, dec, q, wf, backend, steps):
         q4 = query_sort(gv, q)
 
         def launch():
-            _lib.call("pin_query_sdf_grid_sorted", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, 8, int(wf), 0,
-                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
+            _lib.call("pin_query_sdf_grid_sorted_ex", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, 8, int(wf), 0,
+                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), int(flags), _lib.stream())
 
         def order_pass():
             query_sort(gv, q, out=q4)
@@ -547,24 +551,26 @@ def slam_frame_leg(args, dev, world, rank):
     compact records) as a part of its own."""
     from pin_slam_amd.synthetic import FrameLoop, Q_SCALE, lidar_scan, slam_poses, street_scene
     nsteps = SLAM_FRAMES
+    cfg = P.Config(device=dev, reg_iter_n=20, track_on=True)     # config/lidar_slam/run_demo.yaml
+    warm = int(cfg.pool_filter_freq)     # untimed: frame 0's 15 x 40 iterations .. the first pool filter
     rng = np.random.default_rng(21 + 1000 * rank)
     scene = street_scene(rng)
-    poses = slam_poses(1 + nsteps)
+    poses = slam_poses(warm + nsteps)
     scans = [torch.from_numpy(lidar_scan(T, scene, rng).astype(np.float32) / np.float32(Q_SCALE)).to(dev)
              for T in poses]
-    cfg = P.Config(device=dev, reg_iter_n=20, track_on=True)     # config/lidar_slam/run_demo.yaml
     nm = P.NeuralPoints(cfg)
     torch.manual_seed(42)
     dec = P.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(dev)
     tracker = P.Tracker(cfg, nm, dec)
     mapper = P.Mapper(cfg, None, nm, dec)
     loop = FrameLoop(cfg, nm, dec, tracker, mapper, build_index=True)
-    loop.frame(scans[0])
+    for k in range(warm):
+        loop.frame(scans[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     parts, frame_s, valid = {}, [], 0
-    for k in range(1, 1 + nsteps):
+    for k in range(warm, warm + nsteps):
         stamps = []
 
         def mark(name):
@@ -580,7 +586,7 @@ def slam_frame_leg(args, dev, world, rank):
         frame_s.append(prev - t0)
     el, med = _frames_el(frame_s, nsteps, world, dev)
     err = max(float(np.linalg.norm(np.asarray(loop.odom_poses[k])[:3, 3] - poses[k][:3, 3]))
-              for k in range(1 + nsteps))
+              for k in range(warm + nsteps))
     return {"metric": "SLAM frames/sec (pin_slam.py frame loop)", "value": nsteps * world / el, "unit": "frames/s",
             "ms_per_frame": el / nsteps * 1e3, "median_ms_per_frame": med * 1e3,
             "parts_mean_ms": {k: round(statistics.mean(v) * 1e3, 4) for k, v in parts.items()},
@@ -589,7 +595,10 @@ def slam_frame_leg(args, dev, world, rank):
             "config": {"workload": "configs[0]: synthetic 64-beam street sequence (64K points/scan), run_demo.yaml "
                                    "settings (voxel 0.3, k 6, weighted_first, tracker iter_n 20, bs 16384, iters "
                                    "15, decoder trained), deskew off",
-                       "note": "frame 0 (15 x 40 mapping iterations on the empty map) is not timed"}}
+                       "timed_frames": f"{warm}..{warm + nsteps - 1}",
+                       "note": f"frames 0..{warm - 1} are not timed (frame 0: 15 x 40 mapping iterations on the "
+                               f"empty map; frame {warm - 1}: the first pool window filter, pool_filter_freq "
+                               f"{warm}); the timed frames include the filter of frame {2 * warm - 1}"}}
 
 
 def mapper_cpu_baseline(nm, dec, coord, label):
@@ -726,28 +735,32 @@ def main():
     torch.cuda.synchronize()
     build_ms = (time.perf_counter() - tb) * 1e3
 
-    def step():
+    def step(order="tile"):
         return P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False,
-                           want_std=not wf)
+                           want_std=not wf, out_order=order)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps)
-    t = torch.tensor([elapsed, kern_ms, order_ms], dtype=torch.float64, device=dev)
+    def window(order):
+        for _ in range(args.warmup):
+            step(order)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(order)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+    elapsed = window("tile")
+    kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps, flags=1)
+    elapsed_in = window("input")
+    kern_in_ms, _ = time_kernel(nm, dec, q, wf, backend, args.steps, flags=0)
+    t = torch.tensor([elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms, order_ms = float(t[0]), float(t[1]), float(t[2])
+    elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms = (float(v) for v in t)
     total_q = N_QUERY * args.steps * world
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
@@ -794,6 +807,10 @@ def main():
                      "frac_step": (value / world) * BYTES_PER_QUERY / HBM_PEAK,
                      "frac_pmc_traffic": (traffic / (kern_ms * 1e-3) / HBM_PEAK) if traffic else None},
         "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
+        # the same step with the outputs scattered to each query's own index (query_sdf's default
+        # for callers that index the outputs by query): same work, uncoalesced stores
+        "input_order": {"value": total_q / elapsed_in, "unit": "queries/s", "ms_per_step": elapsed_in / args.steps * 1e3,
+                        "kernel_ms": kern_in_ms, "frac_kernel": BYTES_PER_QUERY * N_QUERY / (kern_in_ms * 1e-3) / HBM_PEAK},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)

@@ -210,6 +210,9 @@ typedef struct PinRegParams {
     float gm_dist;               /* reg_GM_dist_m, <= 0: no residual weight */
     float gm_grad;               /* reg_GM_grad, <= 0: no gradient weight */
     int32_t div_grad_norm;       /* reg_dist_div_grad_norm: r = sdf / |g| - label (:335-336) */
+    int32_t q4_points;           /* 1: points are pin_query_sort rows {x, y, z, bits(i)} with sdf / grad /
+                                    nn_count / sdf_std in the same (tile) order (PIN_QUERY_OUT_TILE);
+                                    sdf_label and valid_out stay indexed by the original i */
 } PinRegParams;
 
 /* accumulator layout of pin_reg_normal_eq's output */
@@ -336,6 +339,23 @@ int pin_query_sdf_grid_tiled(const PinGrid* grid, const PinPoints* pts, const Pi
                              int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
                              float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
                              void* workspace, void* stream);
+
+/* flags of the _ex forms: outputs in tile order -- element k of sdf / grad / nn_count / certainty /
+ * sdf_std belongs to the query q4[k] (original index bits(q4[4k+3])) -- instead of at each query's
+ * own index: coalesced stores, for consumers that reduce over the queries (the tracker's normal
+ * equations, pin_reg_normal_eq with PinRegParams.q4_points) or read the index from q4 */
+#define PIN_QUERY_OUT_TILE 1
+
+/* pin_query_sdf_grid_tiled / pin_query_sdf_grid_sorted with flags (PIN_QUERY_OUT_TILE); every
+ * argument is checked before the sort is launched. */
+int pin_query_sdf_grid_tiled_ex(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                                int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                                float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
+                                void* workspace, int32_t flags, void* stream);
+int pin_query_sdf_grid_sorted_ex(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
+                                 int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                                 float* grad, int32_t* nn_count, float* certainty, float* sdf_std, int32_t flags,
+                                 void* stream);
 
 /* pin_query_feature_fwd_grid -- pin_query_feature_fwd with candidates from the occupancy grid
  * (features always read live from pts->features; gids from grid->cgid). */

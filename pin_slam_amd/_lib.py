@@ -17,6 +17,7 @@ PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
 PIN_TRAIN_DX = 2     # PinTrainCfg.flags: forward saves s dsdf/dx (matrix-core decoder), backward applies it
 PIN_TRAIN_EIK = 4    # PinTrainCfg.flags: analytic-gradient eikonal (double backward in closed form)
 PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
+PIN_QUERY_OUT_TILE = 1   # outputs in tile order (pin_query_sdf_grid_*_ex)
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 
 FEATURE_DIM = 8
@@ -60,7 +61,7 @@ class PinGrid(ctypes.Structure):
 
 class PinRegParams(ctypes.Structure):
     _fields_ = [("min_nn_count", i32), ("min_grad_norm", f32), ("max_grad_norm", f32), ("max_sdf_std", f32),
-                ("gm_dist", f32), ("gm_grad", f32), ("div_grad_norm", i32)]
+                ("gm_dist", f32), ("gm_grad", f32), ("div_grad_norm", i32), ("q4_points", i32)]
 
 
 REG_NACC = 31
@@ -135,6 +136,10 @@ _SIGS = {
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_sorted": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_sdf_grid_tiled_ex": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i32, c_void_p],
+    "pin_query_sdf_grid_sorted_ex": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, i32, c_void_p],
     "pin_mc_workspace_bytes": [i64, i64, i64],
     "pin_mc_count": [c_void_p, c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p],
     "pin_mc_emit": [c_void_p, i64, i64, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p],

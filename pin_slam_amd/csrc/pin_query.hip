@@ -412,7 +412,7 @@ __attribute__((amdgpu_waves_per_eu(PGO ? 1 : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q,
                  const float4* __restrict__ q4, int64_t n, int nn_k, int zero_empty, float* __restrict__ sdf_out,
                  float* __restrict__ grad_out, int* __restrict__ nn_out, float* __restrict__ cert_out,
-                 float* __restrict__ std_out, const int* __restrict__ order) {
+                 float* __restrict__ std_out, const int* __restrict__ order, int out_slot) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
     MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
@@ -441,6 +441,9 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
         const int64_t iq = i >= 0 ? i : 0;
         qx = q[3 * iq]; qy = q[3 * iq + 1]; qz = q[3 * iq + 2];
     }
+    // out_slot: outputs at the processing position (tile order, coalesced stores) instead of the
+    // query's own index -- for consumers that reduce over the queries (the tracker) or read q4
+    if (out_slot && i >= 0) i = t;
     const GridSource<FAT> src(g, p);
     query_sdf_body<WF, PGO, GRAD, GridSource<FAT>, MF>(src, p, mw, qx, qy, qz, i, nn_k, zero_empty, sdf_out, grad_out,
                                                        nn_out, cert_out, std_out);
@@ -1073,18 +1076,29 @@ int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, in
     return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
 }
 
-static int query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
-                          const float* q4, int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty,
-                          float* sdf, float* grad, int32_t* nn_count, float* certainty, float* sdf_std,
-                          const int32_t* order, void* stream) {
+// argument checks of the grid SDF query, before anything is launched (the tiled entry sorts first)
+static int query_sdf_grid_args(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, int64_t n,
+                               int32_t nn_k) {
     if (!grid_ok(grid) || !points_ok(pts) || !mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0)
         return PIN_ERR_ARG;
     const bool fat = grid->fat != 0;
     if ((!fat && (!pts->features || !pts->certainties)) || (pts->after_pgo && !pts->orientations))
         return PIN_ERR_ARG;
     if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n > INT32_MAX) return PIN_ERR_ARG;
+    return PIN_OK;
+}
+
+static int query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                          const float* q4, int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty,
+                          float* sdf, float* grad, int32_t* nn_count, float* certainty, float* sdf_std,
+                          const int32_t* order, void* stream, int out_slot = 0) {
+    const int rc = query_sdf_grid_args(grid, pts, mlp, n, nn_k);
+    if (rc != PIN_OK) return rc;
     if (n == 0) return PIN_OK;
-    if ((!q && !q4) || n > INT32_MAX) return PIN_ERR_ARG;
+    if (!q && !q4) return PIN_ERR_ARG;
+    if (out_slot && !q4) return PIN_ERR_ARG;   // tile-order outputs are read against q4
+    const bool fat = grid->fat != 0;
     const bool g = grad != nullptr;
     const bool pgo = pts->after_pgo != 0;
     // the matrix-core decoder pays off where the decoder carries the input gradient (262K queries:
@@ -1095,7 +1109,7 @@ static int query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMl
 #define PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT, MF)                                                                   \
     hipLaunchKernelGGL((k_query_sdf_grid<WF, PGO, GRAD, FAT, MF>), grid_for(n), dim3(kBlock), 0, s, *grid, *pts, \
                        *mlp, q, (const float4*)q4, n, nn_k, zero_empty, sdf, grad, nn_count, certainty, sdf_std,   \
-                       (const int*)order)
+                       (const int*)order, out_slot)
 #define PIN_SDFG_MF(WF, PGO, GRAD, FAT) \
     do { if (mf && GRAD) PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT, GRAD); else PIN_LAUNCH_SDFG(WF, PGO, GRAD, FAT, false); } while (0)
 #define PIN_SDFG_FAT(WF, PGO, GRAD) \
@@ -1113,26 +1127,44 @@ static int query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMl
     return launch_status();
 }
 
+int pin_query_sdf_grid_sorted_ex(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
+                                 int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                                 float* grad, int32_t* nn_count, float* certainty, float* sdf_std, int32_t flags,
+                                 void* stream) {
+    if ((n > 0 && !q4) || (flags & ~PIN_QUERY_OUT_TILE)) return PIN_ERR_ARG;
+    return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                          certainty, sdf_std, nullptr, stream, (flags & PIN_QUERY_OUT_TILE) ? 1 : 0);
+}
+
 int pin_query_sdf_grid_sorted(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q4,
                               int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
                               float* grad, int32_t* nn_count, float* certainty, float* sdf_std, void* stream) {
-    if (n > 0 && !q4) return PIN_ERR_ARG;
+    return pin_query_sdf_grid_sorted_ex(grid, pts, mlp, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                                        certainty, sdf_std, 0, stream);
+}
+
+int pin_query_sdf_grid_tiled_ex(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
+                                int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
+                                float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
+                                void* workspace, int32_t flags, void* stream) {
+    if (n < 0 || (n > 0 && (!q || !q4 || !workspace)) || (flags & ~PIN_QUERY_OUT_TILE)) return PIN_ERR_ARG;
+    const int rc = query_sdf_grid_args(grid, pts, mlp, n, nn_k);   // every check before the sort launches
+    if (rc != PIN_OK) return rc;
+    if (n == 0) return PIN_OK;
+    // the three launches leave the host back to back: the query kernel is queued before the
+    // sort has finished, so the GPU does not wait for the host between them
+    const int rs = sort_queries(*grid, q, n, (float4*)q4, nullptr, workspace, as_stream(stream));
+    if (rs != PIN_OK) return rs;
     return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
-                          certainty, sdf_std, nullptr, stream);
+                          certainty, sdf_std, nullptr, stream, (flags & PIN_QUERY_OUT_TILE) ? 1 : 0);
 }
 
 int pin_query_sdf_grid_tiled(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q,
                              int64_t n, int32_t nn_k, int32_t weighted_first, int32_t zero_empty, float* sdf,
                              float* grad, int32_t* nn_count, float* certainty, float* sdf_std, float* q4,
                              void* workspace, void* stream) {
-    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !q4 || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
-    if (n == 0) return PIN_OK;
-    // the three launches leave the host back to back: the query kernel is queued before the
-    // sort has finished, so the GPU does not wait for the host between them
-    const int rc = sort_queries(*grid, q, n, (float4*)q4, nullptr, workspace, as_stream(stream));
-    if (rc != PIN_OK) return rc;
-    return query_sdf_grid(grid, pts, mlp, nullptr, q4, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
-                          certainty, sdf_std, nullptr, stream);
+    return pin_query_sdf_grid_tiled_ex(grid, pts, mlp, q, n, nn_k, weighted_first, zero_empty, sdf, grad, nn_count,
+                                       certainty, sdf_std, q4, workspace, 0, stream);
 }
 
 int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* mlp, const float* q, int64_t n,

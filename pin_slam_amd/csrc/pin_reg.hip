@@ -44,10 +44,19 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
             valid = nn[i] >= prm.min_nn_count && gn < prm.max_grad_norm && gn > prm.min_grad_norm;
             if (std_) valid = valid && std_[i] < prm.max_sdf_std;
         }
-        if (valid_out) valid_out[i] = valid ? 1 : 0;
+        float px, py, pz;
+        int64_t src = i;   // the query's own index (labels, valid mask)
+        if (prm.q4_points) {
+            const float4 v = ((const float4*)pts)[i];
+            px = v.x; py = v.y; pz = v.z;
+            src = __float_as_int(v.w);
+        } else {
+            px = pts[3 * i]; py = pts[3 * i + 1]; pz = pts[3 * i + 2];
+        }
+        if (valid_out) valid_out[src] = valid ? 1 : 0;
         if (!valid) continue;
         const float sd = prm.div_grad_norm ? sdf[i] / gn : sdf[i];   // :335-336, "fix the overshot"
-        const float r = sd - (label ? label[i] : 0.f);
+        const float r = sd - (label ? label[src] : 0.f);
         float w = 1.f;
         if (weight) {
             w = weight[i];
@@ -60,7 +69,6 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
             const float t = prm.gm_dist / (prm.gm_dist * prm.gm_dist + r * r);
             w = (t * t) * w;
         }
-        const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
         const double J[6] = {(double)(py * gz - pz * gy), (double)(pz * gx - px * gz), (double)(px * gy - py * gx),
                              (double)gx, (double)gy, (double)gz};
         const double wd = w, rd = r;

@@ -291,6 +291,12 @@ class Mapper:
             nb = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
             nb[:n] = cur
             buf = nb
+            # the window filter's compaction target, sized alike now rather than at the first
+            # filter (a first-time allocation of every pool there stalled that frame ~150 ms)
+            spares = self.__dict__.setdefault("_pool_spare", {})
+            sp = spares.get(name)
+            if sp is None or sp.shape[0] < rows or sp.dtype != dt or sp.shape[1:] != nb.shape[1:]:
+                spares[name] = torch.empty_like(nb)
         buf[n:n + m] = new
         bufs[name] = (buf, n + m)
         return buf[:n + m]

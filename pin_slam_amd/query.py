@@ -196,13 +196,18 @@ def query_sort(gv, q, out=None):
 
 
 def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
-              want_certainty=True, nn_k=None, weighted_first=None, sorted_rows=None):
+              want_certainty=True, nn_k=None, weighted_first=None, sorted_rows=None, out_order="input"):
     """Fused query_feature + Decoder.sdf (+ analytic dSDF/dq) in one kernel.
 
     Returns (sdf [N], grad [N,3] or None, nn_count [N] int32, certainty [N] or None,
     sdf_std [N] or None).  Semantics: utils/tracker.py:176-260 (query_locally=True) and
     utils/mesher.py:41-136 (query_locally=False, zero_empty=True).  sorted_rows: q already sorted
-    by query_sort."""
+    by query_sort.  out_order "tile": where the batch is tile-sorted (grid backend, N >= _TILE_MIN)
+    the outputs stay in tile order (coalesced stores) and a sixth value, the sorted rows q4 [N,4]
+    {x, y, z, bits(index)}, says which query each output row belongs to; otherwise (and with
+    "input") the outputs are in input order and the sixth value is None."""
+    if out_order not in ("input", "tile"):
+        raise ValueError("out_order must be 'input' or 'tile'")
     _lib.require_device(points)
     q = points.detach().to(torch.float32).contiguous()
     n = q.shape[0]
@@ -217,6 +222,7 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
     nn_count = torch.empty(n, dtype=torch.int32, device=dev)
     cert = torch.empty(n, dtype=torch.float32, device=dev) if want_certainty else None
     std = torch.empty(n, dtype=torch.float32, device=dev) if (want_std and not wf) else None
+    tile_out = False
     if nm.backend() == "grid":
         gv = nm.grid_view(mode, True)
         if sorted_rows is not None:
@@ -224,12 +230,14 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
                       int(wf), int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
                       _lib.ptr(std), _lib.stream(dev))
         elif _TILE_QUERIES and n >= _TILE_MIN:
-            # tile sort + sorted query in one call (pin_query_sdf_grid_tiled)
+            # tile sort + sorted query in one call (pin_query_sdf_grid_tiled_ex)
             q4 = torch.empty((n, 4), dtype=torch.float32, device=dev)
             ws = order_workspace(n, dev)
-            _lib.call("pin_query_sdf_grid_tiled", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
+            tile_out = out_order == "tile"
+            _lib.call("pin_query_sdf_grid_tiled_ex", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
                       int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
-                      _lib.ptr(std), _lib.ptr(q4), _lib.ptr(ws), _lib.stream(dev))
+                      _lib.ptr(std), _lib.ptr(q4), _lib.ptr(ws), _lib.PIN_QUERY_OUT_TILE if tile_out else 0,
+                      _lib.stream(dev))
         else:
             _lib.call("pin_query_sdf_grid", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf),
                       int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert),
@@ -239,4 +247,6 @@ def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empt
                   _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn_count), _lib.ptr(cert), _lib.ptr(std), _lib.stream())
     if want_std and wf:
         std = torch.zeros(n, dtype=torch.float32, device=dev)
+    if out_order == "tile":
+        return sdf, grad, nn_count, cert, std, (q4 if tile_out else None)
     return sdf, grad, nn_count, cert, std

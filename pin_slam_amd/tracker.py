@@ -295,19 +295,24 @@ class Tracker:
         if normals is not None:
             raise NotImplementedError("normal-consistency weights are not used by any reference config")
         cfg = self.config
-        sdf, grad, nn, _, std = fused_query_sdf(self.neural_points, self.geo_decoder, pts, query_locally=True,
-                                                want_grad=True, want_std=not cfg.weighted_first, want_certainty=False)
+        # outputs in tile order where the batch is tile-sorted: the normal equations are a sum over the
+        # points, so they read the sorted rows (q4) instead of un-permuting (PIN_QUERY_OUT_TILE)
+        sdf, grad, nn, _, std, q4 = fused_query_sdf(self.neural_points, self.geo_decoder, pts, query_locally=True,
+                                                    want_grad=True, want_std=not cfg.weighted_first,
+                                                    want_certainty=False, out_order="tile")
         max_sdf_std = cfg.surface_sample_range_m * cfg.max_sdf_std_ratio
         prm = _lib.PinRegParams(min_nn_count=int(cfg.query_nn_k), min_grad_norm=float(min_grad_norm),
                                 max_grad_norm=float(max_grad_norm), max_sdf_std=float(max_sdf_std),
                                 gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
                                 gm_grad=float(GM_grad) if GM_grad is not None else 0.0,
-                                div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))))
+                                div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))),
+                                q4_points=int(q4 is not None))
         if cfg.weighted_first:
             std = None  # reference: sdf_std stays 0 < max_sdf_std
         b = _reg_buffers(pts.device)
         s = _lib.stream()
-        _lib.call("pin_reg_normal_eq", _lib.ptr(pts), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), _lib.ptr(std),
+        _lib.call("pin_reg_normal_eq", _lib.ptr(pts if q4 is None else q4), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn),
+                  _lib.ptr(std),
                   _lib.ptr(labels), None, pts.shape[0], ctypes.byref(prm), _lib.ptr(b["ws"]), _lib.ptr(b["acc"]),
                   _lib.ptr(valid_out), s)
         pose_out = None
