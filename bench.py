@@ -121,6 +121,8 @@ def parse():
     ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
     ap.add_argument("--no-nwf-leg", action="store_true", help="skip the per-neighbour-decoding leg")
     ap.add_argument("--no-slam", action="store_true", help="skip the whole-frame leg (configs[0])")
+    ap.add_argument("--no-input-order", action="store_true",
+                    help="skip the input-order headline variant (profiles of the tile-order kernel alone)")
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--mapper-shard", default="space", choices=["space", "dense"],
                     help="N > 1 mapper data parallelism: owner-partitioned slabs with halo exchange (space) or "
@@ -755,8 +757,10 @@ def main():
         return time.perf_counter() - t0
     elapsed = window("tile")
     kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps, flags=1)
-    elapsed_in = window("input")
-    kern_in_ms, _ = time_kernel(nm, dec, q, wf, backend, args.steps, flags=0)
+    elapsed_in = kern_in_ms = float("nan")
+    if not args.no_input_order:
+        elapsed_in = window("input")
+        kern_in_ms, _ = time_kernel(nm, dec, q, wf, backend, args.steps, flags=0)
     t = torch.tensor([elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -809,8 +813,9 @@ def main():
         "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
         # the same step with the outputs scattered to each query's own index (query_sdf's default
         # for callers that index the outputs by query): same work, uncoalesced stores
-        "input_order": {"value": total_q / elapsed_in, "unit": "queries/s", "ms_per_step": elapsed_in / args.steps * 1e3,
-                        "kernel_ms": kern_in_ms, "frac_kernel": BYTES_PER_QUERY * N_QUERY / (kern_in_ms * 1e-3) / HBM_PEAK},
+        "input_order": None if args.no_input_order else {
+            "value": total_q / elapsed_in, "unit": "queries/s", "ms_per_step": elapsed_in / args.steps * 1e3,
+            "kernel_ms": kern_in_ms, "frac_kernel": BYTES_PER_QUERY * N_QUERY / (kern_in_ms * 1e-3) / HBM_PEAK},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)

@@ -9,5 +9,5 @@ timeout -k 10 180 rocprofv3 --kernel-trace \
     --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
     --output-format csv -d $OUT/p -o run -- \
     python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-mapper --no-tracker --no-mesher \
-    --no-map-update --no-process-frame ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || exit $?
+    --no-map-update --no-process-frame --no-slam --no-input-order ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || exit $?
 python3 tools/mfma_pmc.py $OUT > gpurun_out/mfma.json

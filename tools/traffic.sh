@@ -9,6 +9,6 @@ OUT=gpurun_out/traffic
 rm -rf $OUT; mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/$c -o run -- \
-        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:---no-mapper --no-tracker --no-mesher --no-map-update --no-process-frame --no-nwf-leg --no-slam} > $OUT/$c.log 2>&1 || exit $?
+        python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:---no-mapper --no-tracker --no-mesher --no-map-update --no-process-frame --no-nwf-leg --no-slam --no-input-order} > $OUT/$c.log 2>&1 || exit $?
 done
 python3 tools/traffic.py $OUT > gpurun_out/traffic.json
