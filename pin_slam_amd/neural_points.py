@@ -352,26 +352,61 @@ class NeuralPoints(nn.Module):
         return self._cached("occupancy", (self.neural_points, self.buffer_pt_index),
                             (float(self.resolution), self.buffer_size), self._build_occupancy)
 
+    # margin of the brick box kept between builds (bricks per side, x/y and z): a moving sensor
+    # grows the map by a few cells per frame, so most rebuilds fit the previous box
+    GRID_BOX_MARGIN = (8, 8, 2)
+
     def _build_occupancy(self):
+        """Occupancy bricks of the current points.  One host read per build in the common case:
+        the cell bounds and the mark kernel's two counters land in one device buffer, the marking
+        runs in the box kept from the previous build (exact bounds + GRID_BOX_MARGIN), and the box
+        is re-sized (a second read) only when the points have left it."""
         pts = self.neural_points.contiguous()
         _lib.require_device(pts)
         res = float(np.float32(self.resolution))
-        bounds = torch.empty(6, dtype=torch.int64, device=pts.device)
-        _lib.call("pin_cell_bounds", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(bounds), _lib.stream())
-        b = bounds.cpu().tolist()
-        lo, hi = b[:3], b[3:]
-        ext = [(h - l + 1 + 3) // 4 for l, h in zip(lo, hi)]
-        nb = ext[0] * ext[1] * ext[2]
-        if nb > self.MAX_GRID_BRICKS:
-            return None
-        dims = _lib.PinGridDims(ox=lo[0], oy=lo[1], oz=lo[2], nbx=ext[0], nby=ext[1], nbz=ext[2], reserved=0)
+        state = torch.empty(8, dtype=torch.int64, device=pts.device)    # bounds [6], marked, occupied
+        _lib.call("pin_cell_bounds", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(state), _lib.stream())
+        box = self.__dict__.get("_grid_box")
+        if box is not None:
+            bricks, dims, ws = self._grid_mark(pts, res, box, state)
+            b = state.cpu().tolist()
+            if self._box_fits(box, b[:3], b[3:6]):
+                return self._occupancy_result(bricks, dims, b[6], b[7])
+        else:
+            b = state.cpu().tolist()
+        lo, hi = b[:3], b[3:6]
+        m = self.GRID_BOX_MARGIN
+        box_lo = [lo[a] - 4 * m[a] for a in range(3)]
+        ext = [(hi[a] + 4 * m[a] - box_lo[a] + 1 + 3) // 4 for a in range(3)]
+        if ext[0] * ext[1] * ext[2] > self.MAX_GRID_BRICKS:
+            box_lo = list(lo)
+            ext = [(h - l + 1 + 3) // 4 for l, h in zip(lo, hi)]
+            if ext[0] * ext[1] * ext[2] > self.MAX_GRID_BRICKS:
+                return None
+        box = (tuple(box_lo), tuple(ext))
+        self._grid_box = box
+        bricks, dims, ws = self._grid_mark(pts, res, box, state)
+        marked, occupied = state[6:8].cpu().tolist()
+        return self._occupancy_result(bricks, dims, marked, occupied)
+
+    @staticmethod
+    def _box_fits(box, lo, hi):
+        (ox, oy, oz), (ex, ey, ez) = box
+        return all(lo[a] >= o and hi[a] < o + 4 * e for a, o, e in zip(range(3), (ox, oy, oz), (ex, ey, ez)))
+
+    def _grid_mark(self, pts, res, box, state):
+        (ox, oy, oz), (ex, ey, ez) = box
+        nb = ex * ey * ez
+        dims = _lib.PinGridDims(ox=ox, oy=oy, oz=oz, nbx=ex, nby=ey, nbz=ez, reserved=0)
         bricks = torch.empty((nb, 4), dtype=torch.int32, device=pts.device)
-        counters = torch.empty(2, dtype=torch.int64, device=pts.device)
         ws = torch.empty(((nb + 4095) // 4096 * 4 + 16,), dtype=torch.uint8, device=pts.device)
         _lib.call("pin_grid_mark", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(self.buffer_pt_index), self.buffer_size,
-                  ctypes.byref(dims), _lib.ptr(bricks), _lib.ptr(counters), _lib.ptr(ws), _lib.stream())
-        marked, occupied = counters.cpu().tolist()
-        if marked != occupied:
+                  ctypes.byref(dims), _lib.ptr(bricks), _lib.ptr(state[6:8]), _lib.ptr(ws), _lib.stream())
+        return bricks, dims, ws
+
+    @staticmethod
+    def _occupancy_result(bricks, dims, marked, occupied):
+        if marked != occupied:   # table entries away from their point's own slot: hash path only
             return None
         return bricks, dims, int(marked)
 
