@@ -837,9 +837,12 @@ __device__ __forceinline__ uint32_t mask_f16x2(float a, float b) {
 }
 
 // All 64 lanes of the wave must call this together (lanes without a query pass zeros).
-// Returns sdf; gx = the NOUT input gradients from input OFF on (GRAD).
+// Returns sdf; gx = the NOUT input gradients from input OFF on (GRAD); mask (may be NULL): the
+// lane's query's 64 ReLU masks, bit c = [pre_c > 0] (the decoder-parameter products of the
+// training backward).
 template <bool GRAD, int OFF, int NOUT>
-__device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+__device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT],
+                                                uint64_t* mask = nullptr) {
     static_assert(OFF + NOUT <= kD, "decoder input range");
     float* xs = m.xs;
     const unsigned char* pk = m.pk;
@@ -921,6 +924,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     f32x4 acc[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    uint32_t mbits[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};   // [query tile][hidden half]
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t mk[4][4];
@@ -939,6 +943,11 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
                 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bl[nt], d, 0, 0, 0);
                 mk[nt][2 * h] = mask_f16x2(d[0], d[1]);
                 mk[nt][2 * h + 1] = mask_f16x2(d[2], d[3]);
+                if (mask) {   // hidden 16 mt + 4 grp + j of query 16 nt + col: bits of half mt / 2
+                    const uint32_t b4 = (d[0] > 0.f ? 1u : 0u) | (d[1] > 0.f ? 2u : 0u) | (d[2] > 0.f ? 4u : 0u) |
+                                        (d[3] > 0.f ? 8u : 0u);
+                    mbits[nt][ch] |= b4 << (16 * h + 4 * grp);
+                }
             }
         }
         const f16x8 a2h = ((const f16x8*)(pk + kPkA2))[(2 * ch) * 64 + lane];
@@ -949,6 +958,22 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
             acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h, b, acc[nt], 0, 0, 0);
             acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l, b, acc[nt], 0, 0, 0);
         }
+    }
+    if (mask) {
+        // OR over the four lane groups (grp) holding a query's hidden rows; lane q = col + 16 grp
+        // then holds query 16 nt + col's whole mask for every nt -- its own query at nt = grp
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            uint32_t a = mbits[nt][0], b = mbits[nt][1];
+            a |= __shfl_xor(a, 16);
+            a |= __shfl_xor(a, 32);
+            b |= __shfl_xor(b, 16);
+            b |= __shfl_xor(b, 32);
+            lo = nt == grp ? a : lo;
+            hi = nt == grp ? b : hi;
+        }
+        *mask = ((uint64_t)hi << 32) | lo;
     }
     // ---- g back to the query's lane: lane (col, grp) holds rows 4grp..4grp+3 of query 16nt+col
     wave_lds_sync();   // every lane has read its B operands

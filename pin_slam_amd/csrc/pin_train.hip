@@ -738,18 +738,27 @@ __global__ void __launch_bounds__(kBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
                  double* __restrict__ loss_part) {
-    static_assert(!MF || !MLP_GRAD, "matrix-core backward: frozen decoder");
+    static_assert(!MF || !MLP_GRAD || (WF && !EIK), "matrix-core backward with a training decoder: weighted_first");
     static_assert(!EIK || !(WF && MF), "analytic eikonal, weighted_first: gx from the forward");
     constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
+    constexpr bool kRowDecode = MF && WF && MLP_GRAD; // weighted_first, training decoder: one decode per row
     constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
     __shared__ float gst[kBlock * kJ * kF];
     __shared__ float s_mg[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMgWave : 1];
     __shared__ float s_so[kWaves];
     __shared__ float s_mlp[MF ? 1 : kWSize];
-    __shared__ uint4 s_pk[kDecode ? kPkBytes / 16 : 1];
+    __shared__ uint4 s_pk[kDecode || kRowDecode ? kPkBytes / 16 : 1];
     __shared__ float s_dsdf[WF && EIK ? kBlock : 1];
-    const MlpW mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk)
-                              : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
+    MlpW mlpw;
+    if constexpr (kRowDecode) {   // the decoder scratch is the wave's slice of s_mg (used in turn)
+        const uint4* src = (const uint4*)m.packed;
+        for (int e = threadIdx.x; e < kPkBytes / 16; e += kBlock) s_pk[e] = src[e];
+        __syncthreads();
+        mlpw = MlpW{nullptr, m.sdf_scale, s_mg[threadIdx.x >> 6], (const unsigned char*)s_pk};
+    } else {
+        mlpw = kDecode ? stage_decoder<true>(m, s_mlp, s_pk)
+                       : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
+    }
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
@@ -789,6 +798,18 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             mlp_grad_mfma<true>(mws, mk, so, x, e, accT, accE);
             so_sum += so;
         }
+    } else if (kRowDecode) {
+        // training decoder on the matrix cores: each row's input gradient and 64 ReLU masks from
+        // one decode of the wave's rows, then the decoder-parameter products
+        float x[kD], gx[kD];
+#pragma unroll
+        for (int d = 0; d < kD; ++d) x[d] = live ? st.x[r * kD + d] : 0.f;
+        uint64_t mk = 0;
+        mlp_sdf_mfma16<true, 0, kD>(mlpw, x, gx, &mk);
+#pragma unroll
+        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = dsdf * gx[d];
+        mlp_grad_mfma<false>(mws, mk, so, x, nullptr, accT, accE);
+        so_sum += so;
     } else if (WF && MF) {
 #pragma unroll
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? dsdf * st.x[r * kD + d] : 0.f;
@@ -1206,7 +1227,11 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st,
                            grad_features, mpart, lpart);
     } else if (cfg->weighted_first) {
-        if (mlp_grad) PIN_LAUNCH_BWD(true, true); else PIN_LAUNCH_BWD(true, false);
+        if (mlp_grad && mlp->packed)   // a training decoder decoded on the matrix cores
+            hipLaunchKernelGGL((k_train_backward<true, true, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg,
+                               *st, grad_features, mpart, lpart);
+        else if (mlp_grad) PIN_LAUNCH_BWD(true, true);
+        else PIN_LAUNCH_BWD(true, false);
     } else {
         if (mlp_grad) PIN_LAUNCH_BWD(false, true);
         else if (mlp->packed)

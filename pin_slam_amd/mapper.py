@@ -21,6 +21,7 @@ mapping(): nothing inside an iteration reads them.
 drop-in query_feature for callers outside the fused loop.
 """
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -31,6 +32,10 @@ from . import _lib
 from .data_sampler import DataSampler
 from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
 from .sharding import all_reduce
+
+# weighted_first with a training decoder: decode each row in the backward on the matrix cores
+# (PIN_TRAIN_ROW_DECODE=0: the f32 VALU decoder backward, for A/B runs)
+_ROW_DECODE = os.environ.get("PIN_TRAIN_ROW_DECODE", "1") != "0"
 
 
 def _viewed_elsewhere(t: torch.Tensor) -> bool:
@@ -605,8 +610,10 @@ class Mapper:
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK and not analytic
-        # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores
-        mv = mlp_view(self.geo_mlp, packed=mlp_grad is None and _MLP_PACK)
+        # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores;
+        # weighted_first with a training decoder: the backward decodes each row there once (input
+        # gradient + ReLU masks of the decoder-parameter products)
+        mv = mlp_view(self.geo_mlp, packed=_MLP_PACK and (mlp_grad is None or (wf and not analytic and _ROW_DECODE)))
         if dx:
             cfg.flags |= _lib.PIN_TRAIN_DX
         if analytic:

@@ -1,0 +1,56 @@
+"""Host cost of the SLAM leg's mapping(15) calls: wall time of the call (its one closing sync
+included) against the GPU time of its kernels, and a cProfile of the host side."""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pin_slam_amd as P  # noqa: E402
+from pin_slam_amd.synthetic import FrameLoop, Q_SCALE, lidar_scan, slam_poses, street_scene  # noqa: E402
+
+
+def main(frames=12):
+    dev = "cuda"
+    rng = np.random.default_rng(21)
+    scene = street_scene(rng)
+    poses = slam_poses(frames)
+    scans = [torch.from_numpy(lidar_scan(T, scene, rng).astype(np.float32) / np.float32(Q_SCALE)).to(dev)
+             for T in poses]
+    cfg = P.Config(device=dev, reg_iter_n=20, track_on=True)
+    nm = P.NeuralPoints(cfg)
+    torch.manual_seed(42)
+    dec = P.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(dev)
+    tracker = P.Tracker(cfg, nm, dec)
+    mapper = P.Mapper(cfg, None, nm, dec)
+    loop = FrameLoop(cfg, nm, dec, tracker, mapper, build_index=True)
+    for k in range(frames):
+        loop.frame(scans[k])
+    torch.cuda.synchronize()
+    walls = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mapper.mapping(15)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+    print("mapping(15) wall ms:", [round(w * 1e3, 3) for w in walls])
+    # host-side only: the same call with the GPU work already queued behind a long sleep kernel
+    pr = cProfile.Profile()
+    torch.cuda.synchronize()
+    pr.enable()
+    t0 = time.perf_counter()
+    mapper.mapping(15)
+    t1 = time.perf_counter()
+    pr.disable()
+    torch.cuda.synchronize()
+    print(f"profiled call wall {1e3 * (t1 - t0):.3f} ms")
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+
+
+if __name__ == "__main__":
+    main()
