@@ -39,7 +39,7 @@ MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world"
                   "_used_poses", "_pool_append", "_pool_compact", "_pool_rows_hint", "set_pool")
 # utils/tracker.py:Tracker -- the fused query and the registration step; the reference's
 # tracking() loop (:39-174) drives them unchanged
-TRACKER_METHODS = ("query_source_points", "registration_step", "_register")
+TRACKER_METHODS = ("query_source_points", "registration_step", "_register", "_shard_range")
 # utils/mesher.py:Mesher -- grid queries (:41-136) and marching cubes (:310-337)
 MESHER_METHODS = ("query_points", "mc_mesh")
 

@@ -22,9 +22,11 @@ import math
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib
 from .query import query_sdf as fused_query_sdf
+from .sharding import all_reduce
 
 
 def transform_torch(points: torch.Tensor, transformation: torch.Tensor) -> torch.Tensor:
@@ -176,7 +178,12 @@ def transform_points(points: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
 
 class Tracker:
 
-    def __init__(self, config, neural_points, geo_decoder, sem_decoder=None, color_decoder=None):
+    def __init__(self, config, neural_points, geo_decoder, sem_decoder=None, color_decoder=None, group=None):
+        """group (a torch.distributed group of W > 1 ranks, optional): every registration step
+        splits the source points into W contiguous chunks, each rank queries its chunk and the
+        31 normal-equation accumulators are SUM all-reduced before the solve (one
+        exchange step); every rank then takes the same pose."""
+        self.group = group
         self.config = config
         self.silence = config.silence
         self.neural_points = neural_points
@@ -287,6 +294,14 @@ class Tracker:
         return sdf, grad, None, None, None, mc_mask, cert, std
 
     # ------------------------------------------------------------------ utils/tracker.py:277-452
+    def _shard_range(self, n):
+        """(lo, hi, world) of this rank's chunk of n source points; (0, n, 1) unsharded."""
+        group = getattr(self, "group", None)
+        if group is None or not dist.is_available() or not dist.is_initialized():
+            return 0, n, 1
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        return n * rank // world, n * (rank + 1) // world, world
+
     def _register(self, pts, normals, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda,
                   want_stats, pose_in=None, valid_out=None):
         """query + normal equations + solve of one registration step, all stream-ordered, then one
@@ -295,6 +310,11 @@ class Tracker:
         if normals is not None:
             raise NotImplementedError("normal-consistency weights are not used by any reference config")
         cfg = self.config
+        lo, hi, world = self._shard_range(pts.shape[0])
+        if world > 1:   # this rank's chunk; the accumulators are summed over the ranks below
+            pts = pts[lo:hi]
+            labels = labels[lo:hi] if labels is not None else None
+            valid_out = valid_out[lo:hi] if valid_out is not None else None
         # outputs in tile order where the batch is tile-sorted: the normal equations are a sum over the
         # points, so they read the sorted rows (q4) instead of un-permuting (PIN_QUERY_OUT_TILE)
         sdf, grad, nn, _, std, q4 = fused_query_sdf(self.neural_points, self.geo_decoder, pts, query_locally=True,
@@ -315,6 +335,8 @@ class Tracker:
                   _lib.ptr(std),
                   _lib.ptr(labels), None, pts.shape[0], ctypes.byref(prm), _lib.ptr(b["ws"]), _lib.ptr(b["acc"]),
                   _lib.ptr(valid_out), s)
+        if world > 1:
+            all_reduce(b["acc"], group=getattr(self, "group", None))   # 31 doubles: a sharded step's one exchange
         pose_out = None
         if pose_in is not None:
             b["flip"] ^= 1
@@ -342,6 +364,20 @@ class Tracker:
         valid = torch.empty(pts.shape[0], dtype=torch.uint8, device=pts.device)
         r = self._register(pts, normals, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda,
                            vis_weight_pc, valid_out=valid)
+        lo, hi, world = self._shard_range(pts.shape[0])
+        if world > 1:   # every rank's chunk of the validity mask, for the valid points of the whole cloud
+            n = pts.shape[0]
+            m = max(n * (k + 1) // world - n * k // world for k in range(world))
+            mine = torch.zeros(m, dtype=torch.uint8, device=pts.device)
+            mine[:hi - lo] = valid[lo:hi]
+            group = getattr(self, "group", None)
+            host = dist.get_backend(group) == "gloo" and mine.is_cuda
+            src = mine.cpu() if host else mine
+            parts = [torch.empty_like(src) for _ in range(world)]
+            dist.all_gather(parts, src, group=group)
+            for k, part in enumerate(parts):
+                a, z = n * k // world, n * (k + 1) // world
+                valid[a:z] = part[:z - a].to(valid.device)
         cnt = int(r["status"][0])
         # the count is on the host already: gather the valid rows without another sync
         valid_points = points[torch.nonzero_static(valid, size=cnt).squeeze(1)]

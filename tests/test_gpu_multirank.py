@@ -172,3 +172,72 @@ def test_multirank_mapping_equals_union_of_batches(case, shard):
         assert _norm(a - b) <= 1e-4 * max(_norm(b), 1e-12)
     np.testing.assert_allclose(r0["cert"], ref["cert"], rtol=1e-5, atol=1e-5 * float(np.abs(ref["cert"]).max()))
     np.testing.assert_array_equal(r0["ts"], ref["ts"])
+
+
+# ------------------------------------------------------------------ point-sharded registration
+def _reg_worker(rank, world, port, case, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        out = _registration(case, "cuda", dist.group.WORLD)
+        q.put((rank, out))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _registration(case, dev, group):
+    """One registration_step and a whole tracking loop on the tracker fixture (group: shard the
+    source points over the group's ranks)."""
+    from tests import helpers as H
+    from pin_slam_amd.tracker import Tracker
+    z = dict(np.load(os.path.join(GOLDEN, f"{case}.npz")))
+    nm = H.neural_points_from_fixture(z, dev)
+    nm.local_geo_features = torch.nn.Parameter(torch.as_tensor(z["local_features"], device=dev))
+    dec = H.decoder_from_fixture(z, nm.config)
+    cfg = nm.config
+    cfg.surface_sample_range_m = float(z["surface_sample_range_m"])
+    cfg.max_sdf_std_ratio = float(z["max_sdf_std_ratio"])
+    cfg.reg_iter_n = int(z["reg_iter_n"])
+    tr = Tracker(cfg, nm, dec, group=group)
+    src = torch.as_tensor(z["source"], device=dev)
+    T, _, _, _, valid, resid, _ = tr.registration_step(
+        src, None, torch.zeros(src.shape[0], device=dev), None, 9, float(z["reg_min_grad_norm"]),
+        float(z["reg_max_grad_norm"]), float(z["reg_GM_dist_m"]), float(z["reg_GM_grad"]), float(z["reg_lm_lambda"]))
+    Tt, _, _, ok = tr.tracking(src, torch.eye(4, dtype=torch.float64, device=dev), cur_ts=9)
+    return dict(T=T.cpu().numpy(), valid=valid.cpu().numpy(), resid=float(resid), Tt=Tt.cpu().numpy(), ok=bool(ok))
+
+
+@pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
+def test_point_sharded_registration_equals_single_process(case):
+    """Tracker(group=...) (the tracker's one exchange step): two ranks on cuda:0
+    (gloo) each query half of the source points and SUM all-reduce the 31 normal-equation
+    accumulators; the step's increment, residual and valid points, and the whole tracking loop's
+    pose, equal the single-process ones (f64 sums in another order: 1e-9)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reg_worker, args=(r, WORLD, port, case, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(WORLD))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(WORLD):
+        assert isinstance(res[r], dict), f"rank {r}: {res[r]}"
+    ref = _registration(case, "cuda", None)
+    for r in range(WORLD):
+        np.testing.assert_allclose(res[r]["T"], ref["T"], rtol=0, atol=1e-9)
+        assert np.array_equal(res[r]["valid"], ref["valid"])
+        assert res[r]["resid"] == pytest.approx(ref["resid"], rel=1e-9)
+        np.testing.assert_allclose(res[r]["Tt"], ref["Tt"], rtol=0, atol=1e-7)
+        assert res[r]["ok"] == ref["ok"]
