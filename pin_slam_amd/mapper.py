@@ -403,8 +403,11 @@ class Mapper:
             raise NotImplementedError("fused mapping implements Adam with weight_decay 0")
 
     def _world(self):
+        """Ranks of the data-parallel group; 1 without an explicit group (an initialised default
+        group alone does not make a mapper data-parallel: replicas mapping their own data, like
+        bench.py's whole-frame leg, must not exchange gradients)."""
         group = getattr(self, "group", None)
-        if group is False or not dist.is_available() or not dist.is_initialized():
+        if group is None or group is False or not dist.is_available() or not dist.is_initialized():
             return 1
         return dist.get_world_size(group)
 

@@ -212,3 +212,41 @@ def test_slab_sharded_mapping_equals_dense_data_parallel(world, grid, layout, sh
         np.testing.assert_allclose(res[r][1], st.local_features, rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(res[r][2], cert0 + cert_delta, rtol=1e-5, atol=1e-5)
         np.testing.assert_array_equal(res[r][3], ts)
+
+
+def _world_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import types
+        from pin_slam_amd.mapper import Mapper
+        from pin_slam_amd.tracker import Tracker
+        q.put((rank, Mapper._world(types.SimpleNamespace()), Mapper._world(types.SimpleNamespace(group=None)),
+               Mapper._world(types.SimpleNamespace(group=dist.group.WORLD)),
+               Tracker._shard_range(types.SimpleNamespace(), 10), Tracker._shard_range(
+                   types.SimpleNamespace(group=dist.group.WORLD), 10)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_only_with_an_explicit_group():
+    """An initialised default process group alone does not make a Mapper / Tracker data-parallel
+    (bench.py's whole-frame leg runs one independent SLAM per rank: its mappers must not exchange
+    gradients of differently sized maps); an explicit group does."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, w_none, w_none2, w_group, sh_none, sh_group in res:
+        assert (w_none, w_none2, w_group) == (1, 1, 2)
+        assert sh_none == (0, 10, 1)
+        assert sh_group == ((0, 5, 2) if rank == 0 else (5, 10, 2))
