@@ -643,8 +643,10 @@ def _shard_info(mapper):
         return None
     halo = int(p.halo.numel())
     sent = sum(int(r.numel()) for r in p.send_rows.values())
-    return {"mode": "space (owner-partitioned slabs, halo exchange)", "owned_rows": int(p.owned.numel()),
-            "halo_rows": halo, "exchange_bytes_per_iter": 2 * 32 * (halo + sent)}
+    return {"mode": "space (owner-partitioned cells, halo exchange, shared quirk row)", "cells": list(p.shape),
+            "owned_rows": int(p.owned.numel()), "halo_rows": halo, "exchange_bytes_per_iter": 2 * 32 * (halo + sent),
+            "batch": "each rank draws its batch from its cell's pool samples, rows weighted so that the union is an "
+                     "unbiased estimate of one reference batch (DESIGN.md section 6)"}
 
 
 def mapper_leg(args, dev, world, rank):
