@@ -277,6 +277,15 @@ int pin_grid_mark(const float* positions, int64_t num_points, float resolution, 
                   int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks, unsigned long long* counters,
                   void* workspace, void* stream);
 
+/* pin_grid_mark with flags: PIN_GRID_TABLE_TRUSTED -- the caller vouches that every occupied table
+ * slot holds a point at its own cell's slot (the table was written from the current positions by
+ * pin_map_insert / pin_hash_assign / pin_hash_rebuild and nothing moved since), so counters[1] =
+ * counters[0] without the pass over the B-slot table. */
+#define PIN_GRID_TABLE_TRUSTED 1
+int pin_grid_mark_ex(const float* positions, int64_t num_points, float resolution, const int32_t* table,
+                     int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks, unsigned long long* counters,
+                     void* workspace, int32_t flags, void* stream);
+
 /*
  * pin_grid_fill -- compact arrays in brick order for one query mode, for every own-cell point g
  * at rank r = rank(cell_g): crec[r] = record_g, cgid[r] = g and, when cfeat / ccert are

@@ -18,6 +18,7 @@ PIN_TRAIN_DX = 2     # PinTrainCfg.flags: forward saves s dsdf/dx (matrix-core d
 PIN_TRAIN_EIK = 4    # PinTrainCfg.flags: analytic-gradient eikonal (double backward in closed form)
 PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
 PIN_QUERY_OUT_TILE = 1   # outputs in tile order (pin_query_sdf_grid_*_ex)
+PIN_GRID_TABLE_TRUSTED = 1   # pin_grid_mark_ex: skip the table count
 _ERRORS = {-1: "invalid argument", -2: "HIP launch/runtime failure", -3: "unsupported configuration"}
 
 FEATURE_DIM = 8
@@ -125,6 +126,8 @@ _SIGS = {
     "pin_reg_solve": [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_transform_points": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_grid_mark_ex": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, i32,
+                         c_void_p],
     "pin_grid_fill": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p, c_void_p,

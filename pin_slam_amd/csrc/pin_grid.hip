@@ -270,9 +270,10 @@ int pin_cell_bounds(const float* positions, int64_t num_points, float resolution
 }
 
 
-int pin_grid_mark(const float* positions, int64_t num_points, float resolution, const int32_t* table,
-                  int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks,
-                  unsigned long long* counters, void* workspace, void* stream) {
+int pin_grid_mark_ex(const float* positions, int64_t num_points, float resolution, const int32_t* table,
+                     int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks, unsigned long long* counters,
+                     void* workspace, int32_t flags, void* stream) {
+    if (flags & ~PIN_GRID_TABLE_TRUSTED) return PIN_ERR_ARG;
     if (!dims_ok(dims) || !table || !bricks || !counters || !workspace || num_points < 0 || buffer_size <= 0 ||
         buffer_size >= (1ll << 31))
         return PIN_ERR_ARG;
@@ -286,8 +287,16 @@ int pin_grid_mark(const float* positions, int64_t num_points, float resolution, 
         hipLaunchKernelGGL(k_grid_mark, dim3((unsigned)mb), dim3(kBlock), 0, s, positions, num_points, resolution,
                            table, buffer_size, *dims, bricks, counters);
     }
-    const int64_t tb = std::min<int64_t>(std::max<int64_t>((buffer_size / 4 + kBlock - 1) / kBlock, 1), 2048);
-    hipLaunchKernelGGL(k_table_count, dim3((unsigned)tb), dim3(kBlock), 0, s, table, buffer_size, counters + 1);
+    if (flags & PIN_GRID_TABLE_TRUSTED) {
+        // the caller vouches that every occupied slot holds a point of its own cell: occupied =
+        // marked, no pass over the table
+        if (hipMemcpyAsync(counters + 1, counters, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s) !=
+            hipSuccess)
+            return PIN_ERR_HIP;
+    } else {
+        const int64_t tb = std::min<int64_t>(std::max<int64_t>((buffer_size / 4 + kBlock - 1) / kBlock, 1), 2048);
+        hipLaunchKernelGGL(k_table_count, dim3((unsigned)tb), dim3(kBlock), 0, s, table, buffer_size, counters + 1);
+    }
     if (launch_status() != PIN_OK) return PIN_ERR_HIP;
     // brick prefix counts
     const int64_t per = (int64_t)kBlock * kScanItems;
@@ -297,6 +306,13 @@ int pin_grid_mark(const float* positions, int64_t num_points, float resolution, 
     hipLaunchKernelGGL(k_scan_block_sums, dim3(1), dim3(1024), 0, s, part, np);
     hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)np), dim3(kBlock), 0, s, bricks, nb, part);
     return launch_status();
+}
+
+int pin_grid_mark(const float* positions, int64_t num_points, float resolution, const int32_t* table,
+                  int64_t buffer_size, const PinGridDims* dims, uint32_t* bricks,
+                  unsigned long long* counters, void* workspace, void* stream) {
+    return pin_grid_mark_ex(positions, num_points, resolution, table, buffer_size, dims, bricks, counters, workspace,
+                            0, stream);
 }
 
 int pin_grid_fill(const float* positions, int64_t num_points, float resolution, const int32_t* table,

@@ -176,6 +176,7 @@ class NeuralPoints(nn.Module):
         self.point_ts_create = torch.empty((0,), device=self.device, dtype=torch.long)
         self.point_ts_update = torch.empty((0,), device=self.device, dtype=torch.long)
         self.point_certainties = torch.empty((0,), dtype=self.dtype, device=self.device)
+        self._trust_table()   # an empty table over no points
 
         self.local_neural_points = torch.empty((0, 3), dtype=self.dtype, device=self.device)
         self.local_point_orientations = torch.empty((0, 4), dtype=self.dtype, device=self.device)
@@ -389,6 +390,21 @@ class NeuralPoints(nn.Module):
         marked, occupied = state[6:8].cpu().tolist()
         return self._occupancy_result(bricks, dims, marked, occupied)
 
+    # The table is "trusted" when this object wrote it from the current positions (insert,
+    # kept-points re-hash, rebuild) and neither tensor changed since: every occupied slot then
+    # holds a point of its own cell, and the exactness check needs no pass over the B slots.
+    def _trust_table(self):
+        pts, tab = self.neural_points, self.buffer_pt_index
+        self._table_trust = None if tab is None else (weakref.ref(pts), pts._version, weakref.ref(tab), tab._version)
+
+    def _table_trusted(self):
+        t = self.__dict__.get("_table_trust")
+        if t is None:
+            return False
+        pr, pv, tr, tv = t
+        return pr() is self.neural_points and pv == self.neural_points._version and \
+            tr() is self.buffer_pt_index and tv == self.buffer_pt_index._version
+
     @staticmethod
     def _box_fits(box, lo, hi):
         (ox, oy, oz), (ex, ey, ez) = box
@@ -400,8 +416,10 @@ class NeuralPoints(nn.Module):
         dims = _lib.PinGridDims(ox=ox, oy=oy, oz=oz, nbx=ex, nby=ey, nbz=ez, reserved=0)
         bricks = torch.empty((nb, 4), dtype=torch.int32, device=pts.device)
         ws = torch.empty(((nb + 4095) // 4096 * 4 + 16,), dtype=torch.uint8, device=pts.device)
-        _lib.call("pin_grid_mark", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(self.buffer_pt_index), self.buffer_size,
-                  ctypes.byref(dims), _lib.ptr(bricks), _lib.ptr(state[6:8]), _lib.ptr(ws), _lib.stream())
+        flags = _lib.PIN_GRID_TABLE_TRUSTED if self._table_trusted() else 0
+        _lib.call("pin_grid_mark_ex", _lib.ptr(pts), pts.shape[0], res, _lib.ptr(self.buffer_pt_index),
+                  self.buffer_size, ctypes.byref(dims), _lib.ptr(bricks), _lib.ptr(state[6:8]), _lib.ptr(ws), flags,
+                  _lib.stream())
         return bricks, dims, ws
 
     @staticmethod
@@ -524,6 +542,7 @@ class NeuralPoints(nn.Module):
             raise IndexError("travel_dist has no entry for cur_ts=%d" % int(cur_ts))
         new_rows = torch.empty((max(n, 1),), dtype=torch.int64, device=dev)
         n_new = torch.empty((1,), dtype=torch.int64, device=dev)
+        was_trusted = self._table_trusted()   # an insert keeps an exact table exact
         _lib.call("pin_map_insert", _lib.ptr(pts), _lib.ptr(sidx), n, float(np.float32(res)),
                   _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.ptr(self.neural_points) if M else None,
                   _lib.ptr(self.point_ts_update) if M else None, M, _lib.ptr(td), int(cur_ts),
@@ -533,6 +552,8 @@ class NeuralPoints(nn.Module):
         k = int(n_new.item())
         added = pts[new_rows[:k]]
         self.neural_points = torch.cat((self.neural_points, added), 0)
+        if was_trusted:
+            self._trust_table()
         quat = torch.zeros((k, 4), dtype=self.dtype, device=dev)
         quat[:, 0] = 1.0
         self.point_orientations = torch.cat((self.point_orientations, quat), 0)
@@ -712,6 +733,7 @@ class NeuralPoints(nn.Module):
                       _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.ptr(map_workspace(n, dev)),
                       _lib.stream())
             torch.autograd.graph.increment_version(self.buffer_pt_index)
+            self._trust_table()
         else:
             self._select_global(sample_idx, n)
             self.rebuild_hash()
@@ -727,6 +749,7 @@ class NeuralPoints(nn.Module):
         _lib.call("pin_hash_rebuild", _lib.ptr(pts), pts.shape[0], float(np.float32(self.resolution)),
                   _lib.ptr(self.buffer_pt_index), self.buffer_size, _lib.stream())
         torch.autograd.graph.increment_version(self.buffer_pt_index)
+        self._trust_table()
 
     def clear_temp(self, clean_more: bool = False):
         """model/neural_points.py:678-693."""
