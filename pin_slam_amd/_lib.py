@@ -125,6 +125,7 @@ _SIGS = {
     "pin_cell_bounds": [c_void_p, i64, f32, c_void_p, c_void_p],
     "pin_reg_solve": [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_transform_points": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_transform_points_sorted": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark_ex": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, i32,
                          c_void_p],
@@ -135,6 +136,7 @@ _SIGS = {
     "pin_mlp_pack": [_P(PinMlp), c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_sort": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_sort_ex": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, i32, c_void_p],
     "pin_query_sdf_grid_tiled": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_sorted": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,

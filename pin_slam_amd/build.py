@@ -5,8 +5,10 @@ container; the resulting .so travels to the GPU box with the repo snapshot.
 """
 import glob
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -39,11 +41,25 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = None)
     out = out or LIB
     if out == LIB and not force and not _stale():
         return LIB
-    cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"),
-           *sources(), "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    # one object per source, compiled in parallel (objects outside the tree), then one link
+    objdir = tempfile.mkdtemp(prefix="pin_slam_amd_obj_")
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
+    try:
+        procs = []
+        objs = []
+        for src in sources():
+            obj = os.path.join(objdir, os.path.basename(src) + ".o")
+            cmd = [HIPCC, *FLAGS, *extra, *inc, "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            procs.append((cmd, subprocess.Popen(cmd)))
+            objs.append(obj)
+        for cmd, p in procs:
+            if p.wait() != 0:
+                raise subprocess.CalledProcessError(p.returncode, cmd)
+        subprocess.run([HIPCC, *FLAGS, *objs, "-o", out + ".tmp"], check=True)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -128,6 +128,27 @@ k_transform_points(const float* __restrict__ src, int64_t n, const double* __res
     for (int a = 0; a < 3; ++a) out[3 * i + a] = fmaf(pz, t[4 * a + 2], fmaf(py, t[4 * a + 1], px * t[4 * a])) + t[4 * a + 3];
 }
 
+// The same transform written into tile-sorted query rows in place: row k = {T src[i], bits(i)}
+// with i = bits(q4[k].w) kept.  The tracking loop sorts its source cloud once (pin_query_sort) and
+// re-poses the sorted rows every later iteration: the points move by the pose increment only, the
+// order is a locality hint (results do not depend on it), and the two sort launches are saved.
+__global__ void __launch_bounds__(kRegBlock)
+k_transform_sorted(const float* __restrict__ src, int64_t n, const double* __restrict__ T, float4* __restrict__ q4) {
+    const int64_t k = (int64_t)blockIdx.x * kRegBlock + threadIdx.x;
+    if (k >= n) return;
+    float t[12];
+#pragma unroll
+    for (int e = 0; e < 12; ++e) t[e] = (float)T[e];
+    const float w = q4[k].w;
+    int i = __float_as_int(w);
+    i = i < 0 || i >= n ? 0 : i;   // rows always come from pin_query_sort; never read outside src
+    const float px = src[3 * (int64_t)i], py = src[3 * (int64_t)i + 1], pz = src[3 * (int64_t)i + 2];
+    float o[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) o[a] = fmaf(pz, t[4 * a + 2], fmaf(py, t[4 * a + 1], px * t[4 * a])) + t[4 * a + 3];
+    q4[k] = make_float4(o[0], o[1], o[2], w);
+}
+
 // implicit_reg's solve on the device (utils/tracker.py:483-496, expmap :580-589) and the tracking
 // loop's bookkeeping of one iteration (:115, :132-133): from the accumulators of
 // pin_reg_normal_eq, N = s sum w J^T J, g = -s sum w r J with s = n / (2 sum w) (the w /= 2 mean(w)
@@ -215,6 +236,14 @@ int pin_transform_points(const float* points, int64_t n, const double* pose, flo
     if (n == 0) return PIN_OK;
     hipLaunchKernelGGL(k_transform_points, dim3((unsigned)((n + kRegBlock - 1) / kRegBlock)), dim3(kRegBlock), 0,
                        reinterpret_cast<hipStream_t>(stream), points, n, pose, out);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}
+
+int pin_transform_points_sorted(const float* points, int64_t n, const double* pose, float* q4, void* stream) {
+    if (n < 0 || n > INT32_MAX || (n > 0 && (!points || !pose || !q4))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_transform_sorted, dim3((unsigned)((n + kRegBlock - 1) / kRegBlock)), dim3(kRegBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), points, n, pose, (float4*)q4);
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

@@ -12,7 +12,7 @@
 * transplants the hot-path methods onto the reference's ``utils.mapper.Mapper``,
   ``utils.tracker.Tracker`` and ``utils.mesher.Mesher`` classes, together with every helper
   method they call, keeping everything else of those classes as it is.  The reference's own
-  control flow (``Tracker.tracking``, ``Mapper.get_batch`` / ``sdf`` /
+  control flow (``Mapper.get_batch`` / ``sdf`` /
   ``get_numerical_gradient``, bundle adjustment, ...) stays: it calls the transplanted
   hot-path methods and the drop-in ``NeuralPoints`` / ``Decoder``.
 
@@ -37,9 +37,11 @@ from .tracker import Tracker
 MAPPER_METHODS = ("mapping", "train_step", "_adam", "_check_supported", "_world", "_pools_fusable",
                   "_slab_partition", "_batch_index", "_randint", "_new_sample_mode", "process_frame", "dynamic_filter",
                   "_used_poses", "_pool_append", "_pool_compact", "_pool_rows_hint", "set_pool")
-# utils/tracker.py:Tracker -- the fused query and the registration step; the reference's
-# tracking() loop (:39-174) drives them unchanged
-TRACKER_METHODS = ("query_source_points", "registration_step", "_register", "_shard_range")
+# utils/tracker.py:Tracker -- the fused query, the registration step and the tracking loop
+# (:39-174) with the pose kept on the device and each iteration enqueued one ahead of the host's
+# read of the previous one (tracker._RegLoop), instead of the reference's per-iteration host syncs
+TRACKER_METHODS = ("tracking", "_iteration_done", "query_source_points", "registration_step", "_register",
+                   "_shard_range")
 # utils/mesher.py:Mesher -- grid queries (:41-136) and marching cubes (:310-337)
 MESHER_METHODS = ("query_points", "mc_mesh")
 

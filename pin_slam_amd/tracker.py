@@ -9,23 +9,27 @@ with torch ops (:176-496).  Here one iteration is:
 2. ``pin_reg_normal_eq``: validity mask, Geman-McClure weights and the f64 normal equations
    in one deterministic reduction;
 3. ``pin_reg_solve``: the 6x6 f64 solve, expmap, T = dT T and the convergence measures of dT on
-   the device; one host read of a 39-double record per iteration drives the control flow
-   (the reference syncs on ``.item()``-style reads several times per iteration).
+   the device; one asynchronous copy of a 55-double record (accumulators, status, dT) per
+   iteration drives the control flow (the reference syncs on ``.item()``-style reads several
+   times per iteration).
 
-The control flow of ``tracking`` (convergence, validity checks, fall-back to the initial
-guess) follows :39-174.  When ``install()`` puts registration_step on the reference class, the
-reference's own tracking loop drives it.  Colour / photometric registration is out of scope
-(off in every lidar config).
+``tracking`` (:39-174: convergence, validity checks, fall-back to the initial guess) keeps the
+pose on the device and runs the iterations through ``_RegLoop``: iteration i+1 is enqueued
+before the host reads iteration i (stream order carries the pose), the cloud is tile-sorted once
+per call and re-posed in tile order afterwards.  ``install()`` transplants it onto the reference
+class.  Colour / photometric registration is out of scope (off in every lidar config).
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import _lib
-from .query import query_sdf as fused_query_sdf
+from . import query as _query
+from .query import mlp_view, order_workspace, query_sdf as fused_query_sdf
 from .sharding import all_reduce
 
 
@@ -147,10 +151,12 @@ def _reg_buffers(dev):
         n = W + _lib.REG_NACC + _lib.REG_NSTATUS + 16 * 3
         buf = torch.empty(n, dtype=torch.float64, device=dev)
         host = torch.empty(_lib.REG_NACC + _lib.REG_NSTATUS, dtype=torch.float64, pin_memory=buf.is_cuda)
+        host2 = torch.empty((2, _lib.REG_NACC + _lib.REG_NSTATUS + 16), dtype=torch.float64, pin_memory=buf.is_cuda)
         o = W + _lib.REG_NACC + _lib.REG_NSTATUS
-        _REG_BUF[key] = dict(ws=buf[:W], acc_status=buf[W:o], acc=buf[W:W + _lib.REG_NACC],
+        _REG_BUF[key] = dict(ws=buf[:W], acc_status=buf[W:o], acc_status_dT=buf[W:o + 16], acc=buf[W:W + _lib.REG_NACC],
                              status=buf[W + _lib.REG_NACC:o], dT=buf[o:o + 16].view(4, 4),
-                             poses=(buf[o + 16:o + 32].view(4, 4), buf[o + 32:o + 48].view(4, 4)), host=host, flip=0)
+                             poses=(buf[o + 16:o + 32].view(4, 4), buf[o + 32:o + 48].view(4, 4)), host=host,
+                             host2=host2, flip=0)
     return _REG_BUF[key]
 
 
@@ -163,6 +169,104 @@ def _reg_accumulate(points, sdf, grad, nn_count, sdf_std, label, weight, prm, va
     h = b["host"][:_lib.REG_NACC]
     h.copy_(b["acc"])
     return h.numpy().copy()
+
+
+_LOOP_SORT_MIN = 16384   # tracking loops over at least this many points process them tile-sorted
+_PIPELINE = os.environ.get("PIN_TRACK_PIPELINE", "1") != "0"   # 0: one _register call (and host read) per iteration
+
+
+class _RegLoop:
+    """One ``tracking`` call's registration iterations, bound once: the views, the outputs and the
+    launch arguments are built in the constructor, so an iteration is six ctypes launches.
+
+    - Tile order: where the grid backend serves the query and the cloud is large enough, iteration
+      0 tile-sorts the posed cloud (pin_query_sdf_grid_tiled_ex, outputs in tile order) and later
+      iterations re-pose the SORTED rows in place (pin_transform_points_sorted): the points move by
+      the pose increment only, so the order stays a good locality order, and the sort's two
+      launches are paid once per call.  The normal equations read the sorted rows (q4_points).
+    - Lookahead: ``enqueue(i)`` ends with an asynchronous copy of the iteration's accumulators and
+      status into pinned host slot i % 2 and an event; the loop enqueues iteration i + 1 (its pose
+      is iteration i's device output) before it waits for iteration i, so the GPU does not idle
+      through the host's read and decision.  Poses ping-pong between two device slots and status
+      between two host slots: iteration i + 1 writes neither of iteration i's."""
+
+    def __init__(self, tracker, src, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda, init_pose):
+        nm, cfg = tracker.neural_points, tracker.config
+        self.n = n = src.shape[0]
+        dev = src.device
+        self.src, self.labels, self.lm = src, labels, float(lm_lambda)
+        self.wf = bool(cfg.weighted_first)
+        self.nn_k = int(cfg.query_nn_k)
+        self.hv, self.pv = nm._views("local", True)
+        self.mv = mlp_view(tracker.geo_decoder, packed=True)
+        self.gv = nm.grid_view("local", True) if nm.backend() == "grid" else None
+        self.sorted = self.gv is not None and n >= _LOOP_SORT_MIN and _query._TILE_QUERIES
+        self.sdf = torch.empty(n, dtype=torch.float32, device=dev)
+        self.grad = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        self.nn = torch.empty(n, dtype=torch.int32, device=dev)
+        self.std = None if self.wf else torch.empty(n, dtype=torch.float32, device=dev)
+        self.cur = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        self.q4 = torch.empty((n, 4), dtype=torch.float32, device=dev) if self.sorted else None
+        self.ws = order_workspace(n, dev) if self.sorted else None
+        self.prm = _lib.PinRegParams(min_nn_count=self.nn_k, min_grad_norm=float(min_grad_norm),
+                                     max_grad_norm=float(max_grad_norm),
+                                     max_sdf_std=float(cfg.surface_sample_range_m * cfg.max_sdf_std_ratio),
+                                     gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
+                                     gm_grad=float(GM_grad) if GM_grad is not None else 0.0,
+                                     div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))),
+                                     q4_points=int(self.sorted))
+        b = self.b = _reg_buffers(dev)
+        self.pose0 = init_pose.contiguous()
+        self.events = (torch.cuda.Event(), torch.cuda.Event())
+        P = _lib.ptr
+        self.a_src, self.a_cur, self.a_q4 = P(src), P(self.cur), P(self.q4)
+        self.a_out = (P(self.sdf), P(self.grad), P(self.nn), None, P(self.std))
+        self.a_label = P(labels)
+        self.a_ws, self.a_acc, self.a_status, self.a_dT = P(b["ws"]), P(b["acc"]), P(b["status"]), P(b["dT"])
+        self.a_pose = (P(b["poses"][0]), P(b["poses"][1]))
+        self.a_pose0 = P(self.pose0)
+
+    def pose(self, i):
+        """The device pose after iteration i."""
+        return self.b["poses"][i % 2]
+
+    def enqueue(self, i):
+        s = _lib.stream()
+        call = _lib.call
+        pose_in = self.a_pose0 if i == 0 else self.a_pose[(i - 1) % 2]
+        n, g, p, m = self.n, self.gv, self.pv, self.mv
+        if self.sorted:
+            if i == 0:
+                call("pin_transform_points", self.a_src, n, pose_in, self.a_cur, s)
+                call("pin_query_sdf_grid_tiled_ex", g.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
+                     *self.a_out, self.a_q4, _lib.ptr(self.ws), _lib.PIN_QUERY_OUT_TILE, s)
+            else:
+                call("pin_transform_points_sorted", self.a_src, n, pose_in, self.a_q4, s)
+                call("pin_query_sdf_grid_sorted_ex", g.ref(), p.ref(), m.ref(), self.a_q4, n, self.nn_k, int(self.wf),
+                     0, *self.a_out, _lib.PIN_QUERY_OUT_TILE, s)
+            pts = self.a_q4
+        else:
+            call("pin_transform_points", self.a_src, n, pose_in, self.a_cur, s)
+            if g is not None:
+                call("pin_query_sdf_grid", g.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
+                     *self.a_out, None, s)
+            else:
+                call("pin_query_sdf", self.hv.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
+                     *self.a_out, s)
+            pts = self.a_cur
+        sdf, grad, nn, _, std = self.a_out
+        call("pin_reg_normal_eq", pts, sdf, grad, nn, None if self.wf else std, self.a_label, None, n,
+             ctypes.byref(self.prm), self.a_ws, self.a_acc, None, s)
+        call("pin_reg_solve", self.a_acc, self.lm, pose_in, self.a_dT, self.a_pose[i % 2], self.a_status, s)
+        self.b["host2"][i % 2].copy_(self.b["acc_status_dT"], non_blocking=True)
+        self.events[i % 2].record()
+
+    def result(self, i):
+        """(accumulators [31], status [8], delta pose [4,4]) of iteration i, on the host (waits for it)."""
+        self.events[i % 2].synchronize()
+        h = self.b["host2"][i % 2].numpy()
+        o = _lib.REG_NACC + _lib.REG_NSTATUS
+        return h[:_lib.REG_NACC].copy(), h[_lib.REG_NACC:o].copy(), h[o:].reshape(4, 4).copy()
 
 
 def transform_points(points: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
@@ -233,13 +337,35 @@ class Tracker:
         eigenvalues = None
         sdf_residual_cm = 0.0
         valid_point_count = 0
+        loop = None
+        if _PIPELINE and self._shard_range(source_point_count)[2] == 1 and dev.type == "cuda" and source_normals is None:
+            loop = _RegLoop(self, src, labels, min_grad_norm, max_grad_norm, cur_GM_dist_m, cur_GM_grad, lm_lambda, T)
+            loop.enqueue(0)
+        launched = 0
+        self.last_iterations = 0
+        self.last_status = "ok"   # or the reference's failure message (its prints stay under silence)
         for i in range(iter_n):
-            cur_points = transform_points(src, T)
             want_stats = vis_result and converged
-            r = self._register(cur_points, source_normals, labels, min_grad_norm, max_grad_norm, cur_GM_dist_m,
-                               cur_GM_grad, lm_lambda, want_stats, pose_in=T)
-            T = r["pose"]                                                     # :115, T = dT @ T
-            st = r["status"]
+            if loop is not None:
+                # one iteration ahead of the host: i + 1 runs while the host reads i, unless i is
+                # known to be the last (converged at i - 1, or the iteration budget)
+                if i + 1 < iter_n and not converged and launched < i + 1:
+                    loop.enqueue(i + 1)
+                    launched = i + 1
+                acc, st, dT = loop.result(i)
+                T = loop.pose(i)                                              # :115, T = dT @ T
+                r = dict(eig=None, cov=None)
+                if want_stats and st[4] > 0:
+                    _, r["cov"], r["eig"] = _solve(acc, lm_lambda, True, True, dev)
+            else:
+                cur_points = transform_points(src, T)
+                r = self._register(cur_points, source_normals, labels, min_grad_norm, max_grad_norm, cur_GM_dist_m,
+                                   cur_GM_grad, lm_lambda, want_stats, pose_in=T)
+                T = r["pose"]                                                 # :115, T = dT @ T
+                st = r["status"]
+                dT = r["delta"]
+            self.last_iterations = i + 1
+            self._iteration_done(i, dT, st)
             valid_point_count = int(st[0])
             sdf_residual_cm = float(st[1]) if st[4] > 0 else 0.0
             eigenvalues = r["eig"]
@@ -248,12 +374,14 @@ class Tracker:
                 if not self.silence:
                     print("(Warning) registration failed: wrong optimization")
                 valid_flag = False
+                self.last_status = "wrong optimization"
             else:
                 last_sdf_residual_cm = sdf_residual_cm
             if valid_point_count < min_valid_points or 1.0 * valid_point_count / source_point_count < min_valid_ratio:
                 if not self.silence:
                     print("(Warning) registration failed: not enough valid points")
                 valid_flag = False
+                self.last_status = "not enough valid points"
             if not valid_flag or converged:
                 break
             rot_angle_deg, tran_m = float(st[2]), float(st[3])                # :132-133, from the solve
@@ -264,18 +392,24 @@ class Tracker:
             if not self.silence:
                 print("(Warning) registration failed: too large final residual")
             valid_flag = False
+            self.last_status = "too large final residual"
         if eigenvalues is not None:
             min_eigenvalue = torch.min(eigenvalues).item()
             if cfg.eigenvalue_check and min_eigenvalue < valid_point_count * eigenvalue_ratio_thre:
                 if not self.silence:
                     print("(Warning) registration failed: eigenvalue check failed")
                 valid_flag = False
+                self.last_status = "eigenvalue check failed"
         if cov_mat is not None:
             cov_mat = cov_mat.detach().cpu().numpy()
         if not valid_flag:
             T = init_pose
             cov_mat = None
         return T, cov_mat, weight_point_cloud, valid_flag
+
+    def _iteration_done(self, i, delta, status):
+        """Called once per registration iteration of ``tracking`` with its delta pose (host
+        ndarray or device tensor [4,4]) and status record; a no-op (a hook for tests/tools)."""
 
     # ------------------------------------------------------------------ utils/tracker.py:176-275
     def query_source_points(self, coord, ts, bs, query_sdf=True, query_sdf_grad=True, query_color=False,

@@ -383,15 +383,24 @@ def test_registration_step_fixture(golden, dev, backend, case):
     np.testing.assert_allclose(_np(T), z["divnorm_delta_T"], atol=5e-6)
 
 
-@pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
-def test_tracking_loop_fixture(golden, dev, case):
+@pytest.mark.parametrize("case,mode", [("tracker_wf", "loop"), ("tracker_nwf", "loop"), ("tracker_wf", "sorted"),
+                                       ("tracker_wf", "stepwise")])
+def test_tracking_loop_fixture(golden, dev, case, mode, monkeypatch):
     """The whole Tracker.tracking loop (utils/tracker.py:39-174: iterations, convergence,
     validity checks, fall-back) from the identity guess vs the reference's own run on a
     well-conditioned room scene: same number of iterations, per-iteration increments within
     5e-5 (f32 reductions in a different order feed the next iteration), residuals within
     1e-3 relative, valid-point counts within 3 (points at the gradient-norm thresholds), the
-    final pose within 1e-4 and the same validity verdict."""
+    final pose within 1e-4 and the same validity verdict.  Modes: "loop" = the pipelined
+    loop (_RegLoop: one iteration enqueued ahead of the host's read); "sorted" = the same with the
+    cloud tile-sorted once and re-posed in tile order on later iterations (forced on for this
+    small cloud); "stepwise" = one _register call per iteration (the sharded path's form)."""
+    from pin_slam_amd import tracker as trk
     from pin_slam_amd.tracker import Tracker
+    if mode == "sorted":
+        monkeypatch.setattr(trk, "_LOOP_SORT_MIN", 0)
+    if mode == "stepwise":
+        monkeypatch.setattr(trk, "_PIPELINE", False)
     z = golden(case)
     nm = H.neural_points_from_fixture(z, dev)
     nm.local_geo_features = torch.nn.Parameter(torch.as_tensor(z["local_features"], device=dev))
@@ -402,18 +411,18 @@ def test_tracking_loop_fixture(golden, dev, case):
     cfg.reg_iter_n = int(z["reg_iter_n"])
     tr = Tracker(cfg, nm, dec)
     hist = []
-    step = tr._register           # one registration step of the loop (query, normal equations, solve)
 
-    def recording_step(*a, **kw):
-        out = step(*a, **kw)
-        st = out["status"]
+    def recording_step(i, delta, st):   # every registration iteration the loop ran
         solved = st[4] > 0
-        hist.append((_np(out["delta"]) if solved else np.eye(4), float(st[1]) if solved else 0.0, int(st[0])))
-        return out
+        d = delta if isinstance(delta, np.ndarray) else _np(delta)
+        hist.append((d if solved else np.eye(4), float(st[1]) if solved else 0.0, int(st[0])))
 
-    tr._register = recording_step
+    tr._iteration_done = recording_step
     src = torch.as_tensor(z["source"], device=dev)
+    if mode == "sorted":
+        assert nm.backend() == "grid"
     T, cov, _, valid = tr.tracking(src, torch.eye(4, dtype=torch.float64, device=dev), cur_ts=9)
+    assert tr.last_iterations == len(hist)
     assert len(hist) == z["tracking_delta_T"].shape[0]
     for i, (dT, res, cnt) in enumerate(hist):
         np.testing.assert_allclose(dT, z["tracking_delta_T"][i], atol=5e-5, err_msg=f"iteration {i}")

@@ -108,7 +108,7 @@ def test_every_self_attribute_resolves_on_the_reference_classes(installed):
 
 
 def test_reference_control_flow_is_kept(installed):
-    """tracking / get_batch / sdf / bundle_adjustment stay the reference's: they reach the
-    accelerated path through the transplanted registration_step and the drop-in classes."""
-    assert installed["kept"] == {"tracking": "utils.tracker", "get_batch": "utils.mapper", "sdf": "utils.mapper",
-                                 "bundle_adjustment": "utils.mapper"}
+    """get_batch / sdf / bundle_adjustment stay the reference's: they reach the accelerated path
+    through the drop-in classes.  tracking is transplanted (the device-pipelined loop)."""
+    assert installed["kept"] == {"tracking": "pin_slam_amd.tracker", "get_batch": "utils.mapper",
+                                 "sdf": "utils.mapper", "bundle_adjustment": "utils.mapper"}
