@@ -121,7 +121,6 @@ def parse():
     ap.add_argument("--no-process-frame", action="store_true", help="skip the process_frame leg (8f rank 4)")
     ap.add_argument("--no-nwf-leg", action="store_true", help="skip the per-neighbour-decoding leg")
     ap.add_argument("--no-slam", action="store_true", help="skip the whole-frame leg (configs[0])")
-    ap.add_argument("--no-streamed", action="store_true", help="skip the streamed-batches view (QueryPipeline)")
     ap.add_argument("--no-input-order", action="store_true",
                     help="skip the input-order headline variant (profiles of the tile-order kernel alone)")
     ap.add_argument("--mapper-steps", type=int, default=10)
@@ -792,38 +791,14 @@ def main():
         return time.perf_counter() - t0
     elapsed = window("tile")
     kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps, flags=1)
-    # a stream of batches (QueryPipeline): the lean tile sort of batch k+1 on a second stream
-    # beside the query of batch k; every batch is still sorted and queried in full
-    elapsed_st = float("nan")
-    if backend == "grid" and not args.no_streamed:
-        pipe = P.QueryPipeline(nm, dec, N_QUERY, query_locally=False, want_grad=True)
-
-        def run(k):
-            pipe.sort(q)
-            for i in range(k):
-                if i + 1 < k:
-                    pipe.sort(q)
-                pipe.query()
-        run(args.warmup)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        run(args.steps)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed_st = time.perf_counter() - t0
     elapsed_in = kern_in_ms = float("nan")
     if not args.no_input_order:
         elapsed_in = window("input")
         kern_in_ms, _ = time_kernel(nm, dec, q, wf, backend, args.steps, flags=0)
-    t = torch.tensor([elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms, elapsed_st], dtype=torch.float64,
-                     device=dev)
+    t = torch.tensor([elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms, elapsed_st = (float(v) for v in t)
+    elapsed, kern_ms, order_ms, elapsed_in, kern_in_ms = (float(v) for v in t)
     total_q = N_QUERY * args.steps * world
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
@@ -873,11 +848,6 @@ def main():
         "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
         # the same step with the outputs scattered to each query's own index (query_sdf's default
         # for callers that index the outputs by query): same work, uncoalesced stores
-        "streamed": None if elapsed_st != elapsed_st else {
-            "value": total_q / elapsed_st, "unit": "queries/s", "ms_per_step": elapsed_st / args.steps * 1e3,
-            "frac_step": (total_q / elapsed_st / world) * BYTES_PER_QUERY / HBM_PEAK,
-            "how": "QueryPipeline: lean tile sort of batch k+1 (pin_query_sort_ex PIN_SORT_LEAN, second stream) "
-                   "beside the query of batch k; every batch sorted and queried in full"},
         "input_order": None if args.no_input_order else {
             "value": total_q / elapsed_in, "unit": "queries/s", "ms_per_step": elapsed_in / args.steps * 1e3,
             "kernel_ms": kern_in_ms, "frac_kernel": BYTES_PER_QUERY * N_QUERY / (kern_in_ms * 1e-3) / HBM_PEAK},

@@ -306,8 +306,7 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
  * totals and a done counter) that must be ZERO before the first call on a workspace and that
  * every call leaves zero again (calls sharing one workspace must be ordered on one stream), then
  * 8 bytes per query. */
-#define PIN_ORDER_STATE_BYTES 33024
-#define PIN_ORDER_BASE_OFFSET 16640   /* tile bases of the lean sort, inside the state bytes */
+#define PIN_ORDER_STATE_BYTES 16640
 static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
     return PIN_ORDER_STATE_BYTES + 8 * n;
 }
@@ -328,15 +327,6 @@ int pin_query_order(const PinGrid* grid, const float* q, int64_t n, int32_t* ord
  */
 int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
                    void* stream);
-
-/* pin_query_sort with flags.  PIN_SORT_LEAN: the same sort as three small kernels of 256 threads
- * and <= 16 VGPRs (one returning atomic per query, a one-block scan, the placement), shaped to run
- * on a second stream BESIDE a running query kernel (whose 2 waves per SIMD leave 16 registers per
- * lane free) rather than between two: the sort of batch k+1 then overlaps the query of batch k.
- * Same workspace; its state is left zero as by pin_query_sort. */
-#define PIN_SORT_LEAN 1
-int pin_query_sort_ex(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
-                      int32_t flags, void* stream);
 
 /*
  * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  order (n ints,

@@ -16,9 +16,9 @@ from .decoder import Decoder
 from .mapper import Mapper
 from .mesher import Mesher
 from .neural_points import NeuralPoints
-from .query import QueryPipeline, query_sdf
+from .query import query_sdf
 from .tracker import Tracker
 from .mapio import load_pin_map, save_implicit_map
 
-__all__ = ["Config", "Decoder", "Mapper", "Mesher", "NeuralPoints", "Tracker", "QueryPipeline", "query_sdf", "load_pin_map",
+__all__ = ["Config", "Decoder", "Mapper", "Mesher", "NeuralPoints", "Tracker", "query_sdf", "load_pin_map",
            "save_implicit_map"]

@@ -136,7 +136,6 @@ _SIGS = {
     "pin_mlp_pack": [_P(PinMlp), c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_sort": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
-    "pin_query_sort_ex": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, i32, c_void_p],
     "pin_query_sdf_grid_tiled": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_sorted": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,

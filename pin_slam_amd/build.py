@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False, extra=(), out: str = None)
         objs = []
         for src in sources():
             obj = os.path.join(objdir, os.path.basename(src) + ".o")
-            cmd = [HIPCC, *FLAGS, *extra, *inc, "-c", src, "-o", obj]
+            cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], *extra, *inc, "-c", src, "-o", obj]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             procs.append((cmd, subprocess.Popen(cmd)))

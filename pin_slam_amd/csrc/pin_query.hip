@@ -649,131 +649,6 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 
-// Lean tile sort (PIN_SORT_LEAN): the same output, shaped to run on a second stream BESIDE a query
-// kernel instead of between two.  The fused query kernel holds 2 waves per SIMD at 242 VGPRs (248
-// allocated): 16 of the 512 registers per SIMD lane stay free, no LDS pressure.  Every lean kernel
-// is 256 threads (one wave per SIMD) in <= 16 VGPRs, so the dispatcher can place its blocks on CUs
-// that are running query blocks; the latency of the sort then hides behind the previous batch's
-// query (a stream of batches: tile-sort batch k+1 while batch k is queried).
-//   k_lean_rank   LDS tile histogram per block, one coalesced returning global atomic per
-//                 (block, tile): the query's rank inside its tile
-//   k_lean_scan   one block: exclusive scan of the tile totals -> bases; totals re-zeroed
-//   k_lean_place  q4[base[tile] + rank] = {x, y, z, bits(i)}
-constexpr int kLean = 256;
-
-// tile_of in 32-bit integer math (a lean kernel's register budget): the cell index is clamped
-// in float before the conversion, so any coordinate lands in a valid tile
-__device__ __forceinline__ int tile_of_lean(float x, float y, float z, const TileMap& t) {
-    auto axis = [&](float v, int64_t o, int nt) -> int {
-        const float c = fminf(fmaxf(floorf(v * t.inv_res) - (float)o, -1.f), (float)(nt << t.shift));
-        const int a = (int)c >> t.shift;
-        return a < 0 ? 0 : (a >= nt ? nt - 1 : a);
-    };
-    return (axis(z, t.oz, t.ntz) * t.nty + axis(y, t.oy, t.nty)) * t.ntx + axis(x, t.ox, t.ntx);
-}
-
-// Per block: an LDS tile histogram (the returning LDS atomic is the query's rank among the block's
-// queries of its tile), then the block's run inside each tile reserved by one returning global
-// atomic per (block, tile) -- issued as coalesced wave instructions, thread k on tiles k, k + 256,
-// ... (64 lanes on 64 different lines, one atomic per query, measured 8x slower and congesting the
-// memory side under the running query kernel) -- and the run added to the ranks.  Queries are
-// processed one per loop trip (registers), kLeanPer per thread.
-constexpr int kLeanPer = 4;
-
-__global__ void __launch_bounds__(kLean)
-k_lean_rank(const float* __restrict__ q, int n, TileMap t, int* __restrict__ tot, int2* __restrict__ tk) {
-    __shared__ int h[kMaxTiles];
-    const int k = threadIdx.x;
-#pragma unroll 1
-    for (int j = 0; j < kMaxTiles / kLean; ++j) h[k + j * kLean] = 0;
-    __syncthreads();
-    const int lo = blockIdx.x * (kLean * kLeanPer) + k;
-#pragma unroll 1
-    for (int u = 0; u < kLeanPer; ++u) {
-        const int i = lo + u * kLean;
-        if (i < n) {
-            const float* p = q + 3 * i;
-            const int tile = tile_of_lean(p[0], p[1], p[2], t);
-            tk[i] = make_int2(tile, atomicAdd(h + tile, 1));
-        }
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int j = 0; j < kMaxTiles / kLean; ++j) {
-        const int b = k + j * kLean;
-        const int c = h[b];
-        h[b] = c ? atomicAdd(tot + b, c) : 0;
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int u = 0; u < kLeanPer; ++u) {   // this thread's own tk writes: visible to it
-        const int i = lo + u * kLean;
-        if (i < n) {
-            const int2 e = tk[i];
-            tk[i].y = e.y + h[e.x];
-        }
-    }
-}
-
-__global__ void __launch_bounds__(kLean)
-k_lean_scan(int* __restrict__ tot, int* __restrict__ base, int ntiles) {
-    __shared__ int wsum[kLean / 64];
-    constexpr int kPer = kMaxTiles / kLean;   // consecutive tiles per thread
-    const int k = threadIdx.x;
-    int sum = 0;
-#pragma unroll 1
-    for (int j = 0; j < kPer; ++j) sum += kPer * k + j < ntiles ? tot[kPer * k + j] : 0;
-    int incl = sum;
-#pragma unroll 1
-    for (int o = 1; o < 64; o <<= 1) {
-        const int w = __shfl_up(incl, o);
-        if ((k & 63) >= o) incl += w;
-    }
-    if ((k & 63) == 63) wsum[k >> 6] = incl;
-    __syncthreads();
-    int run = incl - sum;
-#pragma unroll 1
-    for (int w = 0; w < (k >> 6); ++w) run += wsum[w];
-#pragma unroll 1
-    for (int j = 0; j < kPer; ++j) {
-        const int e = kPer * k + j;
-        const int v = e < ntiles ? tot[e] : 0;
-        base[e] = run;
-        tot[e] = 0;   // state back to zero for the next call on this workspace
-        run += v;
-    }
-}
-
-__global__ void __launch_bounds__(kLean)
-k_lean_place(const float* __restrict__ q, int n, const int* __restrict__ base, const int2* __restrict__ tk,
-             float4* __restrict__ q4, int* __restrict__ order) {
-    const int i = blockIdx.x * kLean + threadIdx.x;
-    if (i >= n) return;
-    const int2 e = tk[i];
-    const int pos = base[e.x & (kMaxTiles - 1)] + e.y;
-    if (pos < 0 || pos >= n) return;   // only a workspace whose state was not zeroed
-    const float* p = q + 3 * i;
-    if (q4) q4[pos] = make_float4(p[0], p[1], p[2], __int_as_float(i));
-    if (order) order[pos] = i;
-}
-
-int sort_queries_lean(const PinGrid& g, const float* q, int64_t n, float4* q4, int* order, void* workspace,
-                      hipStream_t s) {
-    const TileMap t = tile_map(g);
-    char* ws = (char*)workspace;
-    int* tot = (int*)ws;
-    int* base = (int*)(ws + PIN_ORDER_BASE_OFFSET);
-    static_assert(PIN_ORDER_BASE_OFFSET >= 4 * kMaxTiles + 64 &&
-                  PIN_ORDER_BASE_OFFSET + 4 * kMaxTiles <= PIN_ORDER_STATE_BYTES, "order workspace layout");
-    int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
-    const dim3 grid_rank((unsigned)((n + kLean * kLeanPer - 1) / (kLean * kLeanPer)));
-    const dim3 grid((unsigned)((n + kLean - 1) / kLean));
-    hipLaunchKernelGGL(k_lean_rank, grid_rank, dim3(kLean), 0, s, q, (int)n, t, tot, tk);
-    hipLaunchKernelGGL(k_lean_scan, dim3(1), dim3(kLean), 0, s, tot, base, t.ntiles);
-    hipLaunchKernelGGL(k_lean_place, grid, dim3(kLean), 0, s, q, (int)n, base, tk, q4, order);
-    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
-}
-
 // ------------------------------------------------------------------ drop-in query_feature
 template <bool WF, bool PGO, class Src>
 __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoints& p, const float* __restrict__ q,
@@ -1198,16 +1073,6 @@ int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, in
                    void* stream) {
     if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !q4 || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
-    return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
-}
-
-int pin_query_sort_ex(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
-                      int32_t flags, void* stream) {
-    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || (!q4 && !order) || !workspace)) || n > INT32_MAX ||
-        (flags & ~PIN_SORT_LEAN))
-        return PIN_ERR_ARG;
-    if (n == 0) return PIN_OK;
-    if (flags & PIN_SORT_LEAN) return sort_queries_lean(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
     return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
 }
 

@@ -160,8 +160,7 @@ class QueryFeatureFn(torch.autograd.Function):
         return grad_q, grad_f, None, None, None, None, None
 
 
-ORDER_STATE_BYTES = 33024   # PIN_ORDER_STATE_BYTES
-SORT_LEAN = 1   # PIN_SORT_LEAN
+ORDER_STATE_BYTES = 16640   # PIN_ORDER_STATE_BYTES
 _order_ws = {}
 
 
@@ -194,88 +193,6 @@ def query_sort(gv, q, out=None):
     ws = order_workspace(n, q.device)
     _lib.call("pin_query_sort", gv.ref(), _lib.ptr(q), n, _lib.ptr(q4), None, _lib.ptr(ws), _lib.stream(q.device))
     return q4
-
-
-class QueryPipeline:
-    """SDF (+gradient) queries over a stream of random batches, with the tile sort of batch k+1
-    running on a second stream BESIDE the query of batch k.
-
-    The lean sort (pin_query_sort_ex, PIN_SORT_LEAN: 256-thread kernels in <= 16 VGPRs) fits in the
-    registers the 2-waves/SIMD query kernel leaves free, so its latency hides behind the running
-    query instead of sitting between two.  Sorted rows are double-buffered: the sort of batch k+1
-    waits only for the query of batch k-1 (the reader of its buffer); the query of batch k waits
-    for its own sort.  Outputs are in tile order (PIN_QUERY_OUT_TILE) with the sorted rows naming
-    each row's query, as ``query_sdf(..., out_order="tile")`` returns them.
-
-        pipe = QueryPipeline(nm, decoder, n)
-        pipe.sort(batches[0])
-        for k, b in enumerate(batches):
-            if k + 1 < len(batches):
-                pipe.sort(batches[k + 1])      # side stream, overlaps the query below
-            sdf, grad, nn, q4 = pipe.query()    # batch k, on the current stream
-    """
-
-    def __init__(self, nm, decoder, n, query_locally=False, want_grad=True):
-        if nm.backend() != "grid":
-            raise RuntimeError("QueryPipeline needs the occupancy-grid backend")
-        dev = torch.device(nm.device) if not isinstance(nm.device, torch.device) else nm.device
-        if dev.type != "cuda":
-            raise RuntimeError("QueryPipeline needs a ROCm device")
-        self.nm, self.n = nm, int(n)
-        self.mode = "local" if query_locally else "global"
-        self.query_locally = bool(query_locally)
-        self.want_grad = bool(want_grad)
-        self.wf = bool(nm.config.weighted_first)
-        self.nn_k = int(nm.config.query_nn_k)
-        self.mv = mlp_view(decoder, packed=want_grad)
-        self.side = torch.cuda.Stream(device=dev, priority=-1)
-        self.side_h = c_void_p(self.side.cuda_stream)
-        self.q4 = [torch.empty((self.n, 4), dtype=torch.float32, device=dev) for _ in range(2)]
-        self.ws = order_workspace(self.n, dev, stream_handle=self.side_h.value)
-        self.sorted_ev = [torch.cuda.Event(), torch.cuda.Event()]
-        self.free_ev = [torch.cuda.Event(), torch.cuda.Event()]
-        self.out = [(torch.empty(self.n, dtype=torch.float32, device=dev),
-                     torch.empty((self.n, 3), dtype=torch.float32, device=dev) if want_grad else None,
-                     torch.empty(self.n, dtype=torch.int32, device=dev)) for _ in range(2)]
-        self.n_sorted = self.n_queried = 0
-        self.src = [None, None]   # the batch tensors, alive until their sort has run
-
-    def sort(self, points):
-        """Enqueue the lean tile sort of the next batch on the side stream."""
-        if self.n_sorted - self.n_queried >= 2:
-            raise RuntimeError("QueryPipeline: two batches are already sorted and not yet queried")
-        q = points.detach().to(torch.float32).contiguous()
-        if q.shape[0] != self.n:
-            raise ValueError(f"QueryPipeline was built for batches of {self.n} points")
-        slot = self.n_sorted % 2
-        main = torch.cuda.current_stream(q.device)
-        self.side.wait_stream(main)                 # the batch was produced on the current stream
-        self.side.wait_event(self.free_ev[slot])    # the query of batch k-2 read this buffer
-        gv = self.nm.grid_view(self.mode, True)
-        _lib.call("pin_query_sort_ex", gv.ref(), _lib.ptr(q), self.n, _lib.ptr(self.q4[slot]), None,
-                  _lib.ptr(self.ws), SORT_LEAN, self.side_h)
-        self.sorted_ev[slot].record(self.side)
-        q.record_stream(self.side)
-        self.src[slot] = q
-        self.n_sorted += 1
-
-    def query(self):
-        """Query the oldest sorted batch on the current stream -> (sdf, grad, nn_count, q4), tile
-        order.  The tensors are reused two batches later."""
-        if self.n_queried >= self.n_sorted:
-            raise RuntimeError("QueryPipeline: no sorted batch to query")
-        slot = self.n_queried % 2
-        main = torch.cuda.current_stream(self.q4[slot].device)
-        main.wait_event(self.sorted_ev[slot])
-        gv = self.nm.grid_view(self.mode, True)
-        _, pv = self.nm._views(self.mode, self.query_locally)
-        sdf, grad, nn = self.out[slot]
-        _lib.call("pin_query_sdf_grid_sorted_ex", gv.ref(), pv.ref(), self.mv.ref(), _lib.ptr(self.q4[slot]), self.n,
-                  self.nn_k, int(self.wf), 0, _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, None,
-                  _lib.PIN_QUERY_OUT_TILE, _lib.stream())
-        self.free_ev[slot].record(main)
-        self.n_queried += 1
-        return sdf, grad, nn, self.q4[slot]
 
 
 def query_sdf(nm, decoder, points, query_locally=True, want_grad=True, zero_empty=False, want_std=False,
