@@ -259,6 +259,40 @@ int pin_transform_points(const float* points, int64_t n, const double* pose, flo
 int pin_transform_points_sorted(const float* points, int64_t n, const double* pose, float* q4, void* stream);
 
 /*
+ * pin_reg_iteration -- one iteration of Tracker.tracking (utils/tracker.py:92-159) in one call,
+ * stream-ordered, no host synchronisation:
+ *   1. the source cloud under pose_in: first iteration with q4 != NULL (grid only) -> posed into
+ *      cur and tile-sorted into q4 (order_ws as pin_query_sort); later ones -> q4 re-posed in place
+ *      (pin_transform_points_sorted); q4 == NULL -> posed into cur;
+ *   2. the fused SDF + dSDF/dq query (grid or hash; outputs in tile order when sorted);
+ *   3. pin_reg_normal_eq (prm.q4_points is set from the sorted flag) into acc_status_dt[0..30];
+ *   4. pin_reg_solve: status into acc_status_dt[31..38], dT into [39..54], pose_out = dT pose_in;
+ *   5. host_out != NULL (pinned host, 55 doubles): an asynchronous copy of the 55 doubles.
+ * Exactly one of grid / hash is non-NULL.  pose_in / pose_out: [4,4] f64 device, distinct.
+ */
+typedef struct PinRegIter {
+    const float* src;            /* [n,3] source points (f32) */
+    int64_t n;
+    const float* labels;         /* [n] sdf labels by source index, or NULL (zeros) */
+    float* cur;                  /* [n,3] scratch: the posed cloud */
+    float* q4;                   /* [n,4] tile-sorted rows (grid, sorted mode) or NULL */
+    void* order_ws;              /* pin_query_order_workspace_bytes(n), zeroed state (first sorted iteration) */
+    float* sdf;                  /* [n] */
+    float* grad;                 /* [n,3] */
+    int32_t* nn_count;           /* [n] */
+    float* sdf_std;              /* [n], read when weighted_first == 0 */
+    double* reg_ws;              /* PIN_REG_WORKSPACE_DOUBLES */
+    double* acc_status_dt;       /* device: PIN_REG_NACC + PIN_REG_NSTATUS + 16 doubles */
+    double* host_out;            /* pinned host copy target (55 doubles) or NULL */
+    int32_t nn_k;
+    int32_t weighted_first;
+    double lm_lambda;
+    PinRegParams prm;
+} PinRegIter;
+int pin_reg_iteration(const PinGrid* grid, const PinHash* hash, const PinPoints* pts, const PinMlp* mlp,
+                      const PinRegIter* it, int32_t first, const double* pose_in, double* pose_out, void* stream);
+
+/*
  * pin_cell_bounds -- out[0..2] = min, out[3..5] = max over the points of floor(p / resolution)
  * (f32 division, the reference's voxel rule, neural_points.py:214); the occupancy-grid box.
  * Empty input leaves out = {INT64_MAX x3, INT64_MIN x3}.

@@ -65,6 +65,13 @@ class PinRegParams(ctypes.Structure):
                 ("gm_dist", f32), ("gm_grad", f32), ("div_grad_norm", i32), ("q4_points", i32)]
 
 
+class PinRegIter(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("n", i64), ("labels", c_void_p), ("cur", c_void_p), ("q4", c_void_p),
+                ("order_ws", c_void_p), ("sdf", c_void_p), ("grad", c_void_p), ("nn_count", c_void_p),
+                ("sdf_std", c_void_p), ("reg_ws", c_void_p), ("acc_status_dt", c_void_p), ("host_out", c_void_p),
+                ("nn_k", i32), ("weighted_first", i32), ("lm_lambda", ctypes.c_double), ("prm", PinRegParams)]
+
+
 REG_NACC = 31
 REG_NSTATUS = 8
 REG_WORKSPACE_DOUBLES = 256 * REG_NACC
@@ -126,6 +133,8 @@ _SIGS = {
     "pin_reg_solve": [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_transform_points": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_transform_points_sorted": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
+    "pin_reg_iteration": [_P(PinGrid), _P(PinHash), _P(PinPoints), _P(PinMlp), _P(PinRegIter), i32, c_void_p, c_void_p,
+                          c_void_p],
     "pin_grid_mark": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_grid_mark_ex": [c_void_p, i64, f32, c_void_p, i64, _P(PinGridDims), c_void_p, c_void_p, c_void_p, i32,
                          c_void_p],

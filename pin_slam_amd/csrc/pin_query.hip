@@ -1175,6 +1175,58 @@ int pin_query_sdf_grid(const PinGrid* grid, const PinPoints* pts, const PinMlp* 
                           certainty, sdf_std, order, stream);
 }
 
+// One iteration of the tracking loop in one call (utils/tracker.py:92-159 body): pose the source
+// cloud (or re-pose its tile-sorted rows), the fused SDF + gradient query, the normal equations,
+// the device solve (T = dT T) and an asynchronous copy of accumulators + status + dT to the host.
+int pin_reg_iteration(const PinGrid* grid, const PinHash* hash, const PinPoints* pts, const PinMlp* mlp,
+                      const PinRegIter* it, int32_t first, const double* pose_in, double* pose_out, void* stream) {
+    if (!it || !pts || !mlp || !pose_in || !pose_out || it->n < 0 || !it->reg_ws || !it->acc_status_dt) return PIN_ERR_ARG;
+    if ((grid == nullptr) == (hash == nullptr)) return PIN_ERR_ARG;
+    const int64_t n = it->n;
+    const bool sorted = it->q4 != nullptr;
+    if (sorted && (!grid || (first && !it->order_ws))) return PIN_ERR_ARG;
+    if (n > 0 && (!it->src || !it->sdf || !it->grad || !it->nn_count || (!sorted && !it->cur))) return PIN_ERR_ARG;
+    const int rc = grid ? query_sdf_grid_args(grid, pts, mlp, n, it->nn_k) : PIN_OK;
+    if (rc != PIN_OK) return rc;
+    auto s = as_stream(stream);
+    float* std_out = it->weighted_first ? nullptr : it->sdf_std;
+    int r = PIN_OK;
+    if (n > 0) {
+        if (sorted && first) {
+            r = pin_transform_points(it->src, n, pose_in, it->cur, stream);
+            if (r == PIN_OK) r = sort_queries(*grid, it->cur, n, (float4*)it->q4, nullptr, it->order_ws, s);
+        } else if (sorted) {
+            r = pin_transform_points_sorted(it->src, n, pose_in, it->q4, stream);
+        } else {
+            r = pin_transform_points(it->src, n, pose_in, it->cur, stream);
+        }
+        if (r != PIN_OK) return r;
+        if (grid)
+            r = query_sdf_grid(grid, pts, mlp, sorted ? nullptr : it->cur, sorted ? it->q4 : nullptr, n, it->nn_k,
+                               it->weighted_first, 0, it->sdf, it->grad, it->nn_count, nullptr, std_out, nullptr, stream,
+                               sorted ? 1 : 0);
+        else
+            r = pin_query_sdf(hash, pts, mlp, it->cur, n, it->nn_k, it->weighted_first, 0, it->sdf, it->grad,
+                              it->nn_count, nullptr, std_out, stream);
+        if (r != PIN_OK) return r;
+    }
+    PinRegParams prm = it->prm;
+    prm.q4_points = sorted ? 1 : 0;
+    double* acc = it->acc_status_dt;
+    double* status = acc + PIN_REG_NACC;
+    double* dT = status + PIN_REG_NSTATUS;
+    r = pin_reg_normal_eq(sorted ? it->q4 : it->cur, it->sdf, it->grad, it->nn_count, std_out, it->labels, nullptr, n,
+                          &prm, it->reg_ws, acc, nullptr, stream);
+    if (r != PIN_OK) return r;
+    r = pin_reg_solve(acc, it->lm_lambda, pose_in, dT, pose_out, status, stream);
+    if (r != PIN_OK) return r;
+    if (it->host_out &&
+        hipMemcpyAsync(it->host_out, acc, sizeof(double) * (PIN_REG_NACC + PIN_REG_NSTATUS + 16), hipMemcpyDeviceToHost,
+                       s) != hipSuccess)
+        return PIN_ERR_HIP;
+    return PIN_OK;
+}
+
 int pin_query_feature_fwd_grid(const PinGrid* grid, const PinPoints* pts, const float* q, int64_t n, int32_t nn_k,
                                int32_t weighted_first, float* feat, float* weights, int64_t* nn_counts,
                                float* certainty, int32_t* ids, int32_t* gids, void* stream) {

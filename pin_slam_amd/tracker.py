@@ -177,88 +177,66 @@ _PIPELINE = os.environ.get("PIN_TRACK_PIPELINE", "1") != "0"   # 0: one _registe
 
 class _RegLoop:
     """One ``tracking`` call's registration iterations, bound once: the views, the outputs and the
-    launch arguments are built in the constructor, so an iteration is six ctypes launches.
+    launch record (PinRegIter) are built in the constructor, so an iteration is ONE native call
+    (pin_reg_iteration: pose, query, normal equations, solve, asynchronous copy of the 55-double
+    record to pinned host memory) and one event record.
 
     - Tile order: where the grid backend serves the query and the cloud is large enough, iteration
-      0 tile-sorts the posed cloud (pin_query_sdf_grid_tiled_ex, outputs in tile order) and later
-      iterations re-pose the SORTED rows in place (pin_transform_points_sorted): the points move by
-      the pose increment only, so the order stays a good locality order, and the sort's two
-      launches are paid once per call.  The normal equations read the sorted rows (q4_points).
-    - Lookahead: ``enqueue(i)`` ends with an asynchronous copy of the iteration's accumulators and
-      status into pinned host slot i % 2 and an event; the loop enqueues iteration i + 1 (its pose
-      is iteration i's device output) before it waits for iteration i, so the GPU does not idle
-      through the host's read and decision.  Poses ping-pong between two device slots and status
-      between two host slots: iteration i + 1 writes neither of iteration i's."""
+      0 tile-sorts the posed cloud and later iterations re-pose the SORTED rows in place: the
+      points move by the pose increment only, so the order stays a good locality order, and the
+      sort's two launches are paid once per call.  The normal equations read the sorted rows.
+    - Lookahead: iteration i + 1 is enqueued before the host waits for iteration i (its pose is
+      iteration i's device output), so the GPU does not idle through the host's read and
+      decision.  Poses ping-pong between two device slots and records between two pinned host
+      slots: iteration i + 1 writes neither of iteration i's."""
 
     def __init__(self, tracker, src, labels, min_grad_norm, max_grad_norm, GM_dist, GM_grad, lm_lambda, init_pose):
         nm, cfg = tracker.neural_points, tracker.config
         self.n = n = src.shape[0]
         dev = src.device
-        self.src, self.labels, self.lm = src, labels, float(lm_lambda)
-        self.wf = bool(cfg.weighted_first)
-        self.nn_k = int(cfg.query_nn_k)
+        wf = bool(cfg.weighted_first)
+        nn_k = int(cfg.query_nn_k)
         self.hv, self.pv = nm._views("local", True)
         self.mv = mlp_view(tracker.geo_decoder, packed=True)
         self.gv = nm.grid_view("local", True) if nm.backend() == "grid" else None
-        self.sorted = self.gv is not None and n >= _LOOP_SORT_MIN and _query._TILE_QUERIES
+        sorted_ = self.gv is not None and n >= _LOOP_SORT_MIN and _query._TILE_QUERIES
         self.sdf = torch.empty(n, dtype=torch.float32, device=dev)
         self.grad = torch.empty((n, 3), dtype=torch.float32, device=dev)
         self.nn = torch.empty(n, dtype=torch.int32, device=dev)
-        self.std = None if self.wf else torch.empty(n, dtype=torch.float32, device=dev)
+        self.std = None if wf else torch.empty(n, dtype=torch.float32, device=dev)
         self.cur = torch.empty((n, 3), dtype=torch.float32, device=dev)
-        self.q4 = torch.empty((n, 4), dtype=torch.float32, device=dev) if self.sorted else None
-        self.ws = order_workspace(n, dev) if self.sorted else None
-        self.prm = _lib.PinRegParams(min_nn_count=self.nn_k, min_grad_norm=float(min_grad_norm),
-                                     max_grad_norm=float(max_grad_norm),
-                                     max_sdf_std=float(cfg.surface_sample_range_m * cfg.max_sdf_std_ratio),
-                                     gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
-                                     gm_grad=float(GM_grad) if GM_grad is not None else 0.0,
-                                     div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))),
-                                     q4_points=int(self.sorted))
+        self.q4 = torch.empty((n, 4), dtype=torch.float32, device=dev) if sorted_ else None
+        self.ws = order_workspace(n, dev) if sorted_ else None
+        self.src, self.labels = src, labels   # kept alive with the launch record
+        prm = _lib.PinRegParams(min_nn_count=nn_k, min_grad_norm=float(min_grad_norm),
+                                max_grad_norm=float(max_grad_norm),
+                                max_sdf_std=float(cfg.surface_sample_range_m * cfg.max_sdf_std_ratio),
+                                gm_dist=float(GM_dist) if GM_dist is not None else 0.0,
+                                gm_grad=float(GM_grad) if GM_grad is not None else 0.0,
+                                div_grad_norm=int(bool(getattr(cfg, "reg_dist_div_grad_norm", False))),
+                                q4_points=int(sorted_))
         b = self.b = _reg_buffers(dev)
         self.pose0 = init_pose.contiguous()
         self.events = (torch.cuda.Event(), torch.cuda.Event())
-        P = _lib.ptr
-        self.a_src, self.a_cur, self.a_q4 = P(src), P(self.cur), P(self.q4)
-        self.a_out = (P(self.sdf), P(self.grad), P(self.nn), None, P(self.std))
-        self.a_label = P(labels)
-        self.a_ws, self.a_acc, self.a_status, self.a_dT = P(b["ws"]), P(b["acc"]), P(b["status"]), P(b["dT"])
-        self.a_pose = (P(b["poses"][0]), P(b["poses"][1]))
-        self.a_pose0 = P(self.pose0)
+        d = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+        self.rec = [_lib.PinRegIter(src=d(src), n=n, labels=d(labels), cur=d(self.cur), q4=d(self.q4),
+                                    order_ws=d(self.ws), sdf=d(self.sdf), grad=d(self.grad), nn_count=d(self.nn),
+                                    sdf_std=d(self.std), reg_ws=d(b["ws"]), acc_status_dt=d(b["acc_status_dT"]),
+                                    host_out=b["host2"][k].data_ptr(), nn_k=nn_k, weighted_first=int(wf),
+                                    lm_lambda=float(lm_lambda), prm=prm) for k in range(2)]
+        self.a_grid = self.gv.ref() if self.gv is not None else None
+        self.a_hash = None if self.gv is not None else self.hv.ref()
+        self.a_pose = (_lib.ptr(b["poses"][0]), _lib.ptr(b["poses"][1]))
+        self.a_pose0 = _lib.ptr(self.pose0)
 
     def pose(self, i):
         """The device pose after iteration i."""
         return self.b["poses"][i % 2]
 
     def enqueue(self, i):
-        s = _lib.stream()
-        call = _lib.call
         pose_in = self.a_pose0 if i == 0 else self.a_pose[(i - 1) % 2]
-        n, g, p, m = self.n, self.gv, self.pv, self.mv
-        if self.sorted:
-            if i == 0:
-                call("pin_transform_points", self.a_src, n, pose_in, self.a_cur, s)
-                call("pin_query_sdf_grid_tiled_ex", g.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
-                     *self.a_out, self.a_q4, _lib.ptr(self.ws), _lib.PIN_QUERY_OUT_TILE, s)
-            else:
-                call("pin_transform_points_sorted", self.a_src, n, pose_in, self.a_q4, s)
-                call("pin_query_sdf_grid_sorted_ex", g.ref(), p.ref(), m.ref(), self.a_q4, n, self.nn_k, int(self.wf),
-                     0, *self.a_out, _lib.PIN_QUERY_OUT_TILE, s)
-            pts = self.a_q4
-        else:
-            call("pin_transform_points", self.a_src, n, pose_in, self.a_cur, s)
-            if g is not None:
-                call("pin_query_sdf_grid", g.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
-                     *self.a_out, None, s)
-            else:
-                call("pin_query_sdf", self.hv.ref(), p.ref(), m.ref(), self.a_cur, n, self.nn_k, int(self.wf), 0,
-                     *self.a_out, s)
-            pts = self.a_cur
-        sdf, grad, nn, _, std = self.a_out
-        call("pin_reg_normal_eq", pts, sdf, grad, nn, None if self.wf else std, self.a_label, None, n,
-             ctypes.byref(self.prm), self.a_ws, self.a_acc, None, s)
-        call("pin_reg_solve", self.a_acc, self.lm, pose_in, self.a_dT, self.a_pose[i % 2], self.a_status, s)
-        self.b["host2"][i % 2].copy_(self.b["acc_status_dT"], non_blocking=True)
+        _lib.call("pin_reg_iteration", self.a_grid, self.a_hash, self.pv.ref(), self.mv.ref(),
+                  ctypes.byref(self.rec[i % 2]), int(i == 0), pose_in, self.a_pose[i % 2], _lib.stream())
         self.events[i % 2].record()
 
     def result(self, i):
