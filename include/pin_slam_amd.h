@@ -219,7 +219,9 @@ typedef struct PinRegParams {
 #define PIN_REG_NACC 31          /* [0] sum w, [1] sum |r|, [2] sum w r^2, [3] n_valid,
                                     [4..24] sum w J^T J (upper triangle, row major),
                                     [25..30] sum w r J,  J = [p x g, g] */
-#define PIN_REG_WORKSPACE_DOUBLES (256 * PIN_REG_NACC)
+#define PIN_REG_WORKSPACE_DOUBLES (256 * PIN_REG_NACC + 8)   /* block partials, then pin_reg_step's counter
+                                                             (one word that must be ZERO before the first
+                                                             pin_reg_step on a workspace; it is left zero) */
 
 /*
  * pin_reg_normal_eq -- fused validity mask + Geman-McClure weights + f64 normal-equation
@@ -248,6 +250,18 @@ int pin_reg_normal_eq(const float* points, const float* sdf, const float* grad, 
 int pin_reg_solve(const double* acc, double lm_lambda, const double* pose_in, double* delta_pose, double* pose_out,
                   double* status, void* stream);
 
+/*
+ * pin_reg_step -- pin_reg_normal_eq (sdf_label / sdf_std may be NULL; no weights, no valid_out)
+ * followed by pin_reg_solve in ONE launch: the last block to finish sums the block partials in
+ * pin_reg_normal_eq's fixed order (bitwise the same acc) and solves.  acc [PIN_REG_NACC], status,
+ * delta_pose, pose_in / pose_out as pin_reg_solve; workspace PIN_REG_WORKSPACE_DOUBLES doubles whose
+ * counter word is zero before the first call.
+ */
+int pin_reg_step(const float* points, const float* sdf, const float* grad, const int32_t* nn_count,
+                 const float* sdf_std, const float* sdf_label, int64_t n, const PinRegParams* prm, double* workspace,
+                 double* acc, double lm_lambda, const double* pose_in, double* delta_pose, double* pose_out,
+                 double* status, void* stream);
+
 /* pin_transform_points -- transform_torch (utils/tools.py:386-399): out [n,3] f32 = the points
  * under pose [4,4] (row-major f64 on the device, cast to f32), one fma chain per coordinate. */
 int pin_transform_points(const float* points, int64_t n, const double* pose, float* out, void* stream);
@@ -265,8 +279,8 @@ int pin_transform_points_sorted(const float* points, int64_t n, const double* po
  *      cur and tile-sorted into q4 (order_ws as pin_query_sort); later ones -> q4 re-posed in place
  *      (pin_transform_points_sorted); q4 == NULL -> posed into cur;
  *   2. the fused SDF + dSDF/dq query (grid or hash; outputs in tile order when sorted);
- *   3. pin_reg_normal_eq (prm.q4_points is set from the sorted flag) into acc_status_dt[0..30];
- *   4. pin_reg_solve: status into acc_status_dt[31..38], dT into [39..54], pose_out = dT pose_in;
+ *   3.+4. pin_reg_step (prm.q4_points is set from the sorted flag): the accumulators into
+ *      acc_status_dt[0..30], status into [31..38], dT into [39..54], pose_out = dT pose_in;
  *   5. host_out != NULL (pinned host, 55 doubles): an asynchronous copy of the 55 doubles.
  * Exactly one of grid / hash is non-NULL.  pose_in / pose_out: [4,4] f64 device, distinct.
  */
@@ -281,7 +295,7 @@ typedef struct PinRegIter {
     float* grad;                 /* [n,3] */
     int32_t* nn_count;           /* [n] */
     float* sdf_std;              /* [n], read when weighted_first == 0 */
-    double* reg_ws;              /* PIN_REG_WORKSPACE_DOUBLES */
+    double* reg_ws;              /* PIN_REG_WORKSPACE_DOUBLES, counter word zeroed (pin_reg_step) */
     double* acc_status_dt;       /* device: PIN_REG_NACC + PIN_REG_NSTATUS + 16 doubles */
     double* host_out;            /* pinned host copy target (55 doubles) or NULL */
     int32_t nn_k;

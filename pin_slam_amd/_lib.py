@@ -74,7 +74,7 @@ class PinRegIter(ctypes.Structure):
 
 REG_NACC = 31
 REG_NSTATUS = 8
-REG_WORKSPACE_DOUBLES = 256 * REG_NACC
+REG_WORKSPACE_DOUBLES = 256 * REG_NACC + 8   # block partials + pin_reg_step's counter word
 
 
 class PinMlp(ctypes.Structure):
@@ -131,6 +131,8 @@ _SIGS = {
                           _P(PinRegParams), c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_cell_bounds": [c_void_p, i64, f32, c_void_p, c_void_p],
     "pin_reg_solve": [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_reg_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinRegParams), c_void_p,
+                     c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_transform_points": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_transform_points_sorted": [c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_reg_iteration": [_P(PinGrid), _P(PinHash), _P(PinPoints), _P(PinMlp), _P(PinRegIter), i32, c_void_p, c_void_p,

@@ -1215,10 +1215,8 @@ int pin_reg_iteration(const PinGrid* grid, const PinHash* hash, const PinPoints*
     double* acc = it->acc_status_dt;
     double* status = acc + PIN_REG_NACC;
     double* dT = status + PIN_REG_NSTATUS;
-    r = pin_reg_normal_eq(sorted ? it->q4 : it->cur, it->sdf, it->grad, it->nn_count, std_out, it->labels, nullptr, n,
-                          &prm, it->reg_ws, acc, nullptr, stream);
-    if (r != PIN_OK) return r;
-    r = pin_reg_solve(acc, it->lm_lambda, pose_in, dT, pose_out, status, stream);
+    r = pin_reg_step(sorted ? it->q4 : it->cur, it->sdf, it->grad, it->nn_count, std_out, it->labels, n, &prm,
+                     it->reg_ws, acc, it->lm_lambda, pose_in, dT, pose_out, status, stream);
     if (r != PIN_OK) return r;
     if (it->host_out &&
         hipMemcpyAsync(it->host_out, acc, sizeof(double) * (PIN_REG_NACC + PIN_REG_NSTATUS + 16), hipMemcpyDeviceToHost,

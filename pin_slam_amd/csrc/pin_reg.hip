@@ -27,11 +27,12 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-__global__ void __launch_bounds__(kRegBlock)
-k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, const float* __restrict__ grad,
-               const int32_t* __restrict__ nn, const float* __restrict__ std_, const float* __restrict__ label,
-               const float* __restrict__ weight, int64_t n, PinRegParams prm, double* __restrict__ partials,
-               uint8_t* __restrict__ valid_out) {
+// one block's partial accumulators -> partials[blockIdx.x * PIN_REG_NACC ..]
+__device__ __forceinline__ void reg_block_partials(const float* __restrict__ pts, const float* __restrict__ sdf,
+                                                   const float* __restrict__ grad, const int32_t* __restrict__ nn,
+                                                   const float* __restrict__ std_, const float* __restrict__ label,
+                                                   const float* __restrict__ weight, int64_t n, const PinRegParams& prm,
+                                                   double* __restrict__ partials, uint8_t* __restrict__ valid_out) {
     double acc[PIN_REG_NACC];
 #pragma unroll
     for (int k = 0; k < PIN_REG_NACC; ++k) acc[k] = 0.0;
@@ -99,18 +100,36 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
     }
 }
 
+__global__ void __launch_bounds__(kRegBlock)
+k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, const float* __restrict__ grad,
+               const int32_t* __restrict__ nn, const float* __restrict__ std_, const float* __restrict__ label,
+               const float* __restrict__ weight, int64_t n, PinRegParams prm, double* __restrict__ partials,
+               uint8_t* __restrict__ valid_out) {
+    reg_block_partials(pts, sdf, grad, nn, std_, label, weight, n, prm, partials, valid_out);
+}
+
 // out[k] = sum of the block partials in a fixed order: thread t serves accumulator t / 8
 // (31 x 8 = 248 threads), strided partial sums over the blocks, then a shuffle tree over
 // the 8 lanes of each accumulator
-__global__ void __launch_bounds__(256) k_reg_final(const double* __restrict__ partials, int nblk,
-                                                   double* __restrict__ out) {
-    const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
+// COHERENT: the partials were written by other blocks of the SAME launch (read at device scope)
+template <bool COHERENT>
+__device__ __forceinline__ double reg_final_sum(const double* __restrict__ partials, int nblk, int k, int l) {
     double v = 0.0;
     if (k < PIN_REG_NACC)
-        for (int b = l; b < nblk; b += 8) v += partials[(int64_t)b * PIN_REG_NACC + k];
+        for (int b = l; b < nblk; b += 8) {
+            const double* a = partials + (int64_t)b * PIN_REG_NACC + k;
+            v += COHERENT ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *a;
+        }
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);
     v += __shfl_xor(v, 4);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_reg_final(const double* __restrict__ partials, int nblk,
+                                                   double* __restrict__ out) {
+    const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
+    const double v = reg_final_sum<false>(partials, nblk, k, l);
     if (k < PIN_REG_NACC && l == 0) out[k] = v;
 }
 
@@ -154,9 +173,8 @@ k_transform_sorted(const float* __restrict__ src, int64_t n, const double* __res
 // pin_reg_normal_eq, N = s sum w J^T J, g = -s sum w r J with s = n / (2 sum w) (the w /= 2 mean(w)
 // of :394), N += lambda diag(N), t = N^-1 g (f64 Gaussian elimination, partial pivoting),
 // dT = [expmap(t[0:3]) | t[3:6]], pose_out = dT pose_in.  One thread.
-__global__ void k_reg_solve(const double* __restrict__ acc, double lm_lambda, const double* __restrict__ pose_in,
-                            double* __restrict__ dT, double* __restrict__ pose_out, double* __restrict__ status) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void reg_solve_body(const double* __restrict__ acc, double lm_lambda, const double* __restrict__ pose_in,
+                               double* __restrict__ dT, double* __restrict__ pose_out, double* __restrict__ status) {
     const double s_w = acc[0], s_r = acc[1], cnt = acc[3];
     status[0] = cnt;
     status[1] = cnt > 0.0 ? s_r / cnt * 100.0 : 0.0;
@@ -227,6 +245,41 @@ __global__ void k_reg_solve(const double* __restrict__ acc, double lm_lambda, co
     status[4] = solve ? 1.0 : 0.0;
 }
 
+__global__ void k_reg_solve(const double* __restrict__ acc, double lm_lambda, const double* __restrict__ pose_in,
+                            double* __restrict__ dT, double* __restrict__ pose_out, double* __restrict__ status) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    reg_solve_body(acc, lm_lambda, pose_in, dT, pose_out, status);
+}
+
+// The registration step's reductions and solve in ONE launch: every block writes its partials, the
+// last block to finish (ticket on a counter that wraps back to zero) sums them in the fixed order of
+// k_reg_final (bitwise the same accumulators) and runs the solve -- two launches fewer per
+// iteration of the tracking loop.
+__global__ void __launch_bounds__(kRegBlock)
+k_reg_step(const float* __restrict__ pts, const float* __restrict__ sdf, const float* __restrict__ grad,
+           const int32_t* __restrict__ nn, const float* __restrict__ std_, const float* __restrict__ label,
+           int64_t n, PinRegParams prm, double* __restrict__ partials, unsigned* __restrict__ counter,
+           double* __restrict__ acc, double lm_lambda, const double* __restrict__ pose_in, double* __restrict__ dT,
+           double* __restrict__ pose_out, double* __restrict__ status) {
+    reg_block_partials(pts, sdf, grad, nn, std_, label, nullptr, n, prm, partials, nullptr);
+    __shared__ int last;
+    __shared__ double s_acc[PIN_REG_NACC];
+    __threadfence();   // this block's partials before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicInc(counter, gridDim.x - 1) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
+    const double v = reg_final_sum<true>(partials, gridDim.x, k, l);
+    if (k < PIN_REG_NACC && l == 0) {
+        acc[k] = v;
+        s_acc[k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) reg_solve_body(s_acc, lm_lambda, pose_in, dT, pose_out, status);
+}
+
 }  // namespace
 
 extern "C" {
@@ -252,6 +305,20 @@ int pin_reg_solve(const double* acc, double lm_lambda, const double* pose_in, do
     if (!acc || !delta_pose || !status || (pose_out && !pose_in)) return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_reg_solve, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), acc, lm_lambda,
                        pose_in, delta_pose, pose_out, status);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}
+
+int pin_reg_step(const float* points, const float* sdf, const float* grad, const int32_t* nn_count,
+                 const float* sdf_std, const float* sdf_label, int64_t n, const PinRegParams* prm, double* workspace,
+                 double* acc, double lm_lambda, const double* pose_in, double* delta_pose, double* pose_out,
+                 double* status, void* stream) {
+    if (!prm || !acc || !workspace || !delta_pose || !status || (pose_out && !pose_in) || n < 0) return PIN_ERR_ARG;
+    if (n > 0 && (!points || !sdf || !grad || !nn_count)) return PIN_ERR_ARG;
+    const int nblk = (int)std::min<int64_t>(std::max<int64_t>((n + kRegBlock - 1) / kRegBlock, 1), kRegMaxBlocks);
+    unsigned* counter = (unsigned*)(workspace + kRegMaxBlocks * PIN_REG_NACC);
+    hipLaunchKernelGGL(k_reg_step, dim3(nblk), dim3(kRegBlock), 0, reinterpret_cast<hipStream_t>(stream), points, sdf,
+                       grad, nn_count, sdf_std, sdf_label, n, *prm, workspace, counter, acc, lm_lambda, pose_in,
+                       delta_pose, pose_out, status);
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

@@ -150,6 +150,7 @@ def _reg_buffers(dev):
         W = _lib.REG_WORKSPACE_DOUBLES
         n = W + _lib.REG_NACC + _lib.REG_NSTATUS + 16 * 3
         buf = torch.empty(n, dtype=torch.float64, device=dev)
+        buf[W - 8:W].zero_()   # pin_reg_step's counter word (left zero by every call)
         host = torch.empty(_lib.REG_NACC + _lib.REG_NSTATUS, dtype=torch.float64, pin_memory=buf.is_cuda)
         host2 = torch.empty((2, _lib.REG_NACC + _lib.REG_NSTATUS + 16), dtype=torch.float64, pin_memory=buf.is_cuda)
         o = W + _lib.REG_NACC + _lib.REG_NSTATUS
