@@ -518,6 +518,19 @@ int pin_train_gather(const float* coord_pool, const float* label_pool, const int
                      void* stream);
 
 /*
+ * pin_pool_pack -- the sample pool as one 32-B record per sample (8 f32 words): {x, y, z, label,
+ * bits(ts lo), bits(ts hi), weight, 0} from coord [n,3], label [n], ts [n] int64 (may be NULL: 0),
+ * weight [n] (may be NULL: 1).  packed 16-B aligned, [n, 8] f32.
+ * pin_train_gather_packed -- pin_train_gather over such a pool: one line per batch row instead of
+ * four (ts_out / weight_out may be NULL: not written; weight_out = |weight|).
+ */
+int pin_pool_pack(const float* coord, const float* label, const int64_t* ts, const float* weight, int64_t n,
+                  float* packed, void* stream);
+int pin_train_gather_packed(const float* packed_pool, int64_t pool_rows, const int64_t* index, const PinTrainCfg* cfg,
+                            float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                            void* stream);
+
+/*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping
  * iteration (mapper.py:461-468, :683-711; neural_points.py:528-674 with training_mode): fills
  * st->ids/weights/x/sdf and applies the certainty / ts_update side effects with atomics.

@@ -166,6 +166,9 @@ _SIGS = {
     "pin_train_rows": [c_void_p, _P(PinTrainCfg), c_void_p, c_void_p],
     "pin_train_gather": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_pool_pack": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, c_void_p],
+    "pin_train_gather_packed": [c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,

@@ -111,15 +111,14 @@ k_reg_partials(const float* __restrict__ pts, const float* __restrict__ sdf, con
 // out[k] = sum of the block partials in a fixed order: thread t serves accumulator t / 8
 // (31 x 8 = 248 threads), strided partial sums over the blocks, then a shuffle tree over
 // the 8 lanes of each accumulator
-// COHERENT: the partials were written by other blocks of the SAME launch (read at device scope)
-template <bool COHERENT>
+// fixed-order sum of the block partials: thread (k, l) sums blocks l, l + 8, ... of accumulator k,
+// then a shuffle tree over the 8 lanes
 __device__ __forceinline__ double reg_final_sum(const double* __restrict__ partials, int nblk, int k, int l) {
     double v = 0.0;
-    if (k < PIN_REG_NACC)
-        for (int b = l; b < nblk; b += 8) {
-            const double* a = partials + (int64_t)b * PIN_REG_NACC + k;
-            v += COHERENT ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *a;
-        }
+    if (k < PIN_REG_NACC) {
+#pragma unroll 8
+        for (int b = l; b < nblk; b += 8) v += partials[(int64_t)b * PIN_REG_NACC + k];
+    }
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);
     v += __shfl_xor(v, 4);
@@ -129,7 +128,7 @@ __device__ __forceinline__ double reg_final_sum(const double* __restrict__ parti
 __global__ void __launch_bounds__(256) k_reg_final(const double* __restrict__ partials, int nblk,
                                                    double* __restrict__ out) {
     const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
-    const double v = reg_final_sum<false>(partials, nblk, k, l);
+    const double v = reg_final_sum(partials, nblk, k, l);
     if (k < PIN_REG_NACC && l == 0) out[k] = v;
 }
 
@@ -264,14 +263,25 @@ k_reg_step(const float* __restrict__ pts, const float* __restrict__ sdf, const f
     reg_block_partials(pts, sdf, grad, nn, std_, label, nullptr, n, prm, partials, nullptr);
     __shared__ int last;
     __shared__ double s_acc[PIN_REG_NACC];
-    __threadfence();   // this block's partials before its ticket
+    // hand-off of the block partials (MI355X_MICROARCH.md, inter-workgroup visibility, valid form):
+    // storing waves wait for their stores, one lane releases at agent scope (the L2 write-back),
+    // waits for it, then takes the ticket; the last block's lane 0 acquires (its CU's L1
+    // invalidated) before the block's plain loads.  One fence per block, not per thread.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicInc(counter, gridDim.x - 1) == gridDim.x - 1;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicInc(counter, gridDim.x - 1) == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
     __syncthreads();
     if (!last) return;
-    __threadfence();
     const int k = threadIdx.x >> 3, l = threadIdx.x & 7;
-    const double v = reg_final_sum<true>(partials, gridDim.x, k, l);
+    const double v = reg_final_sum(partials, gridDim.x, k, l);
     if (k < PIN_REG_NACC && l == 0) {
         acc[k] = v;
         s_acc[k] = v;

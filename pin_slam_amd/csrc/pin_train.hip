@@ -312,6 +312,55 @@ k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool,
     }
 }
 
+// The sample pool as one 32-B record per sample, {x, y, z, label} {ts lo, ts hi, weight, 0}, so a
+// batch row costs ONE line gathered from a pool far larger than L2 instead of four (coordinates,
+// label, ts, weight live in separate tensors in the reference's layout).
+__global__ void __launch_bounds__(kBlock)
+k_pool_pack(const float* __restrict__ coord, const float* __restrict__ label, const int64_t* __restrict__ ts,
+            const float* __restrict__ weight, int64_t n, float4* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int64_t t = ts ? ts[i] : 0;
+    out[2 * i] = make_float4(coord[3 * i], coord[3 * i + 1], coord[3 * i + 2], label[i]);
+    out[2 * i + 1] = make_float4(__int_as_float((int)(t & 0xffffffff)), __int_as_float((int)(t >> 32)),
+                                 weight ? weight[i] : 1.f, 0.f);
+}
+
+// k_train_gather over the packed pool: the row's two 16-B halves of one 32-B record
+__global__ void __launch_bounds__(kBlock)
+k_train_gather_packed(const float4* __restrict__ pool, int64_t pool_rows, const int64_t* __restrict__ index,
+                      PinTrainCfg c, float* __restrict__ rows, float* __restrict__ label, int64_t* __restrict__ ts,
+                      float* __restrict__ weight, int* __restrict__ error) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= c.n_main) return;
+    int64_t i = index[r];
+    if (i < 0 || i >= pool_rows) {   // never gather outside the pool: clamp and report
+        if (error) atomicOr(error, 1);
+        i = 0;
+    }
+    const float4 a = pool[2 * i], b = pool[2 * i + 1];
+    rows[3 * r] = a.x;
+    rows[3 * r + 1] = a.y;
+    rows[3 * r + 2] = a.z;
+    label[r] = a.w;
+    if (ts) ts[r] = (int64_t)(uint32_t)__float_as_int(b.x) | ((int64_t)__float_as_int(b.y) << 32);
+    if (weight) weight[r] = fabsf(b.z);
+    if (c.n_stencil > 0 && r % c.decimation == 0 && r / c.decimation < c.n_stencil) {
+        const int64_t k = r / c.decimation;
+#pragma unroll
+        for (int blk = 0; blk < 6; ++blk) {
+            float x = a.x, y = a.y, z = a.z;
+            if ((blk >> 1) == 0) x = (blk & 1) ? x - c.eps : x + c.eps;
+            else if ((blk >> 1) == 1) y = (blk & 1) ? y - c.eps : y + c.eps;
+            else z = (blk & 1) ? z - c.eps : z + c.eps;
+            float* o = rows + 3 * (c.n_main + blk * c.n_stencil + k);
+            o[0] = x;
+            o[1] = y;
+            o[2] = z;
+        }
+    }
+}
+
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + expf(-v)); }
 
 // loss / gradient factor of a batch row: grad_scale, or grad_scale_tail for the last n_tail rows
@@ -1128,6 +1177,30 @@ int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, 
     if (rows == 0) return PIN_OK;
     if (!coord || !rows_out) return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_train_rows, grid_for(rows), dim3(kBlock), 0, as_stream(stream), coord, *cfg, rows_out);
+    return launch_status();
+}
+
+int pin_pool_pack(const float* coord, const float* label, const int64_t* ts, const float* weight, int64_t n,
+                  float* packed, void* stream) {
+    if (n < 0 || (n > 0 && (!coord || !label || !packed)) || ((uintptr_t)packed & 15)) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_pool_pack, grid_for(n), dim3(kBlock), 0, as_stream(stream), coord, label, ts, weight, n,
+                       (float4*)packed);
+    return launch_status();
+}
+
+int pin_train_gather_packed(const float* packed_pool, int64_t pool_rows, const int64_t* index, const PinTrainCfg* cfg,
+                            float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                            void* stream) {
+    if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
+    if (cfg->n_stencil > 0 && (cfg->n_stencil - 1) * (int64_t)cfg->decimation >= cfg->n_main) return PIN_ERR_ARG;
+    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
+    if (rows == 0) return PIN_OK;
+    if (!packed_pool || ((uintptr_t)packed_pool & 15) || !index || !rows_out || !label_out || pool_rows < 1)
+        return PIN_ERR_ARG;
+    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream),
+                       (const float4*)packed_pool, pool_rows, index, *cfg, rows_out, label_out, ts_out, weight_out,
+                       (int*)error);
     return launch_status();
 }
 

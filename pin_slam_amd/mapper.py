@@ -36,6 +36,8 @@ from .sharding import all_reduce
 # weighted_first with a training decoder: decode each row in the backward on the matrix cores
 # (PIN_TRAIN_ROW_DECODE=0: the f32 VALU decoder backward, for A/B runs)
 _ROW_DECODE = os.environ.get("PIN_TRAIN_ROW_DECODE", "1") != "0"
+# the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
+_PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 
 
 def _viewed_elsewhere(t: torch.Tensor) -> bool:
@@ -200,6 +202,7 @@ class Mapper:
         time_repeat = torch.full((coord.shape[0],), int(frame_id), dtype=torch.long, device=self.device)
         self.cur_sample_count = sdf_label.shape[0]
         self.pool_sample_count = self.sdf_label_pool.shape[0]
+        sig_before = self._pool_signature() if self.global_coord_pool is not None else None
         if getattr(c, "from_sample_points", True):                                       # :163-171
             if getattr(c, "from_all_samples", False):
                 update_points = coord
@@ -230,6 +233,13 @@ class Mapper:
             self.ba_done_flag = False
         else:
             self.global_coord_pool = self._pool_append("global_coord", self.global_coord_pool, global_coord)
+        # the packed records follow the pools: the new samples packed and appended (a stale or
+        # missing packed pool is left for _packed_pool to rebuild in one pass)
+        track = _PACK_POOL and self.__dict__.get("_pool_packed") is not None and sig_before is not None \
+            and self.__dict__.get("_pool_packed_sig") == sig_before and self._pools_fusable()
+        if track:
+            self._pool_packed = self._pool_append("packed", self._pool_packed,
+                                                  self._pack(global_coord, sdf_label, time_repeat, weight))
         if (frame_id + 1) % int(c.pool_filter_freq) == 0:                                # :226-262
             rel = self.global_coord_pool - frame_origin.to(self.global_coord_pool)
             filter_mask = torch.sum(rel ** 2, dim=-1) < c.window_radius ** 2
@@ -245,6 +255,8 @@ class Mapper:
             self.sdf_label_pool = self._pool_compact("sdf_label", self.sdf_label_pool, keep)
             self.weight_pool = self._pool_compact("weight", self.weight_pool, keep)
             self.time_pool = self._pool_compact("time", self.time_pool, keep)
+            if track:
+                self._pool_packed = self._pool_compact("packed", self._pool_packed, keep)
             if sem_label is not None:
                 self.sem_label_pool = self._pool_compact("sem", self.sem_label_pool, keep)
             if color_label is not None:
@@ -255,6 +267,8 @@ class Mapper:
         else:
             self.cur_sample_count = coord.shape[0]
             self.pool_sample_count = self.coord_pool.shape[0]
+        if track:
+            self._pool_packed_sig = self._pool_signature()
         if int(getattr(c, "bs_new_sample", 0)) > 0:                                      # :269-304
             cur = self.global_coord_pool[-self.cur_sample_count:]
             cur_label = self.sdf_label_pool[-self.cur_sample_count:]
@@ -338,6 +352,46 @@ class Mapper:
         self.time_pool = ts
         self.weight_pool = torch.ones_like(sdf_label) if weight is None else weight
         self.pool_sample_count = int(sdf_label.shape[0])
+
+    def _pool_signature(self):
+        pools = (self.global_coord_pool, self.sdf_label_pool, self.time_pool, self.weight_pool)
+        return tuple((id(t), t.data_ptr(), t._version, t.shape[0]) if t is not None else None for t in pools)
+
+    @staticmethod
+    def _pack(coord, label, ts, weight, out=None):
+        """pin_pool_pack of [n] samples -> [n, 8] f32 records (out: written in place)."""
+        n = label.shape[0]
+        out = torch.empty((n, 8), dtype=torch.float32, device=label.device) if out is None else out
+        w = None if weight is None else weight.detach().to(torch.float32).contiguous()
+        _lib.call("pin_pool_pack", _lib.ptr(coord.contiguous()), _lib.ptr(label.contiguous()),
+                  _lib.ptr(None if ts is None else ts.to(torch.int64).contiguous()), _lib.ptr(w), n, _lib.ptr(out),
+                  _lib.stream())
+        return out
+
+    def _packed_pool(self):
+        """The pools (global coordinates, labels, ts, weights) as one 32-B record per sample, for the
+        batch gather.  process_frame keeps it current incrementally (new samples packed on append,
+        the window filter's compaction applied to it too); any other change to the pools (set_pool,
+        the bundle-adjustment re-transform, a caller's assignment) is detected by the pools'
+        identity / version / length and the records are rebuilt in one pass."""
+        sig = self._pool_signature()
+        pk = self.__dict__.get("_pool_packed")
+        if pk is not None and self.__dict__.get("_pool_packed_sig") == sig:
+            return pk
+        if not self._pools_fusable():
+            return None
+        n = self.sdf_label_pool.shape[0]
+        if self.global_coord_pool.shape[0] != n or (self.time_pool is not None and self.time_pool.shape[0] != n):
+            return None
+        weight = self.weight_pool if (self.weight_pool is not None and self.weight_pool.shape[0] == n) else None
+        bufs = self.__dict__.setdefault("_pool_bufs", {})
+        buf = bufs.get("packed", (None, -1))[0]
+        if buf is None or buf.shape[0] < n:
+            buf = torch.empty((max(n, self._pool_rows_hint(0)), 8), dtype=torch.float32, device=self.device)
+        pk = self._pack(self.global_coord_pool, self.sdf_label_pool, self.time_pool, weight, out=buf[:n])
+        bufs["packed"] = (buf, n)
+        self._pool_packed, self._pool_packed_sig = pk, sig
+        return pk
 
     def _randint(self, high, n):
         """torch.randint(0, high, (n,)) on the mapper's device: every draw of get_batch goes through
@@ -441,18 +495,19 @@ class Mapper:
         # a get_batch replaced on the instance (tests, callers) is honoured
         fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
         part, slab_rows, slab_new, scales = self._slab_partition(world, fused)
+        packed = self._packed_pool() if fused and _PACK_POOL else None
         for _ in range(iter_count):
             if fused:
                 if part is None:
                     index = self._batch_index()
                     self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
-                                    world, index=index, weight=self.weight_pool)
+                                    world, index=index, weight=self.weight_pool, packed=packed)
                 else:
                     index = self._batch_index(slab_rows, slab_new)
                     scale_h, scale_n = scales(int(index.shape[0]) - self._n_new_rows, self._n_new_rows)
                     self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
                                     world, index=index, reduce=False, scale=scale_h, n_tail=self._n_new_rows,
-                                    scale_tail=scale_n, weight=self.weight_pool)
+                                    scale_tail=scale_n, weight=self.weight_pool, packed=packed)
             else:
                 coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
                 if self.ba_done_flag:
@@ -536,7 +591,7 @@ class Mapper:
                 and (t is None or (t.dtype == torch.int64 and t.is_contiguous())))
 
     def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None, reduce=True,
-                   scale=None, n_tail=0, scale_tail=0.0, weight=None):
+                   scale=None, n_tail=0, scale_tail=0.0, weight=None, packed=None):
         """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
         SUM all-reduced over the group when world > 1 and reduce.  Returns the device loss tensor.
         index ([N] int64): coord / sdf_label / ts are then the sample pools and the batch is their
@@ -544,7 +599,8 @@ class Mapper:
         scale: loss / gradient factor (default 1/world); the last n_tail batch rows (and the
         stencil groups based on them) take scale_tail instead (slab sharding's new-sample rows).
         weight: the batch rows' sample weights (the weight pool with index), used as |weight| by the
-        BCE term when loss_weight_on (utils/mapper.py:514-516)."""
+        BCE term when loss_weight_on (utils/mapper.py:514-516).
+        packed: the same pools as one 32-B record per sample (_packed_pool), gathered instead."""
         c = self.config
         nm = self.neural_points
         weighted = bool(getattr(c, "loss_weight_on", False)) and weight is not None
@@ -593,11 +649,16 @@ class Mapper:
         else:
             label = b.label
             ts64 = b.ts if ts is not None else None
-            wpool = weight.detach().to(torch.float32).contiguous() if weighted else None
             wrow = b.wrow if weighted else None
-            _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
-                      int(q.shape[0]), _lib.ptr(index), ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label),
-                      _lib.ptr(ts64), _lib.ptr(wrow), _lib.ptr(b.gather_error), s)
+            if packed is not None:
+                _lib.call("pin_train_gather_packed", _lib.ptr(packed), int(packed.shape[0]), _lib.ptr(index),
+                          ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), _lib.ptr(wrow),
+                          _lib.ptr(b.gather_error), s)
+            else:
+                wpool = weight.detach().to(torch.float32).contiguous() if weighted else None
+                _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
+                          int(q.shape[0]), _lib.ptr(index), ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label),
+                          _lib.ptr(ts64), _lib.ptr(wrow), _lib.ptr(b.gather_error), s)
         cfg.flags = _lib.PIN_TRAIN_ROWS
         q = rows_xyz
         sorted_rows = None
