@@ -22,11 +22,6 @@ namespace {
 constexpr int kRegBlock = 256;
 constexpr int kRegMaxBlocks = 256;
 
-__device__ __forceinline__ double wave_sum(double v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
-    return v;
-}
-
 // one block's partial accumulators -> partials[blockIdx.x * PIN_REG_NACC ..]
 __device__ __forceinline__ void reg_block_partials(const float* __restrict__ pts, const float* __restrict__ sdf,
                                                    const float* __restrict__ grad, const int32_t* __restrict__ nn,
@@ -85,19 +80,24 @@ __device__ __forceinline__ void reg_block_partials(const float* __restrict__ pts
 #pragma unroll
         for (int a = 0; a < 6; ++a) acc[25 + a] += wd * rd * J[a];
     }
-    __shared__ double red[kRegBlock / 64][PIN_REG_NACC];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // block reduction, transposed through LDS: every thread's 31 accumulators land in column tid,
+    // then 8 threads per accumulator sum 32 columns each (fixed order) and a 3-step xor tree joins
+    // them.  (Per-accumulator shuffle trees were 372 ds_bpermute with ~190 waits per wave.)
+    __shared__ double red[PIN_REG_NACC][kRegBlock];
+    const int tid = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < PIN_REG_NACC; ++k) {
-        const double v = wave_sum(acc[k]);
-        if (lane == 0) red[wave][k] = v;
-    }
+    for (int k = 0; k < PIN_REG_NACC; ++k) red[k][tid] = acc[k];
     __syncthreads();
-    if (threadIdx.x < PIN_REG_NACC) {
-        double v = 0.0;
-        for (int w = 0; w < kRegBlock / 64; ++w) v += red[w][threadIdx.x];
-        partials[(int64_t)blockIdx.x * PIN_REG_NACC + threadIdx.x] = v;
+    const int k = tid >> 3, part = tid & 7;
+    double v = 0.0;
+    if (k < PIN_REG_NACC) {
+#pragma unroll 8
+        for (int c = 0; c < kRegBlock / 8; ++c) v += red[k][part * (kRegBlock / 8) + c];
     }
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    if (k < PIN_REG_NACC && part == 0) partials[(int64_t)blockIdx.x * PIN_REG_NACC + k] = v;
 }
 
 __global__ void __launch_bounds__(kRegBlock)
