@@ -29,8 +29,15 @@ def surface_points(n_side, res=0.3):
 def surface_map(n_side, res=0.3, seed=42, device="cuda", buffer_size=int(5e7), nn_k=8, weighted_first=True,
                 feature_std=0.05, num_nei_cells=2, search_alpha=0.2, **cfg_kw):
     """Returns (NeuralPoints with the whole map local, Decoder, host points [M,3])."""
+    return points_map(surface_points(n_side, res), res, seed, device, buffer_size, nn_k, weighted_first,
+                      feature_std, num_nei_cells, search_alpha, **cfg_kw)
+
+
+def points_map(pts, res=0.3, seed=42, device="cuda", buffer_size=int(5e7), nn_k=8, weighted_first=True,
+               feature_std=0.05, num_nei_cells=2, search_alpha=0.2, **cfg_kw):
+    """surface_map over the given host points [M,3] (random features and certainties)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
-    pts = surface_points(n_side, res)
+    pts = torch.as_tensor(pts, dtype=torch.float32)
     cfg = Config(device=device, voxel_size_m=res, buffer_size=buffer_size, query_nn_k=nn_k,
                  weighted_first=weighted_first, local_map_radius=1e9, num_nei_cells=num_nei_cells,
                  search_alpha=search_alpha, **cfg_kw)

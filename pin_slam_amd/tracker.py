@@ -381,6 +381,9 @@ class Tracker:
                 self.last_status = "eigenvalue check failed"
         if cov_mat is not None:
             cov_mat = cov_mat.detach().cpu().numpy()
+        # diagnostics of the last call (not part of the reference's return): the optimised pose
+        # before a failed check replaces it with the initial guess, and the final residual
+        self.last_pose, self.last_residual_cm = T, sdf_residual_cm
         if not valid_flag:
             T = init_pose
             cov_mat = None
