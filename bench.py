@@ -341,7 +341,10 @@ def tracker_leg(nm, dec, pts, args, dev, world, rank):
                                                                                             dtype=torch.float64))),
             "final_residual_cm": tr.last_residual_cm,
             "residual_bound_cm": nm.config.surface_sample_range_m * 0.5 * 100.0,
-            "note": "Tracker.tracking from the identity guess, median of 5 windows; iterations counted as run"}
+            "note": "Tracker.tracking from the identity guess, median of 5 windows; iterations counted as run. "
+                    "The synthetic surface is smooth and gently sloped, so an xy shift is weakly observable and the "
+                    "300-iteration fit leaves a coarse SDF: the loop's validity checks can fail here; the "
+                    "configs[0] street sequence (slam_frame) is the pose-accuracy check"}
     return {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
             "queries_per_sec": TRACKER_SRC * steps / el, "ms_per_iter": el / steps * 1e3, "steps": steps,
             "valid_points": int(out[4].shape[0]), "scaling": "replicas", "map_fit_loss": fit_loss,

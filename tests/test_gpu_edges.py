@@ -7,6 +7,7 @@ import torch
 
 import pin_slam_amd as P
 from oracle import pin_oracle as O
+from pin_slam_amd.synthetic import points_map
 from tests import helpers as H
 
 pytestmark = pytest.mark.gpu
@@ -130,3 +131,50 @@ def test_registration_with_too_few_points(small_map, dev):
     T, cov, eig, _, valid, resid, _ = tr.registration_step(src, None, torch.zeros(5, device=dev), None, 0, 0.5, 2.0,
                                                            0.5, 0.2, 1e-4)
     assert torch.equal(T, torch.eye(4, dtype=torch.float64, device=dev)) and valid.shape[0] == 0
+
+
+def _lattice_map(dev, nn_k, seed):
+    """One point per cell centre of a 24 x 24 lattice, 2 layers deep at x < 12 cells and 6 layers
+    deep beyond; half of the points moved by up to 2e-6 m per axis (a few f32 ulps), so that the
+    queries below see exactly equal and nearly equal candidate distances."""
+    res = 0.3
+    rng = np.random.default_rng(seed)
+    i, j, k = np.meshgrid(np.arange(24), np.arange(24), np.arange(6), indexing="ij")
+    keep = (k < 2) | (i >= 12)
+    pts = (np.stack([i[keep], j[keep], k[keep]], 1) + 0.5) * res
+    moved = rng.random(pts.shape[0]) < 0.5
+    pts[moved] += rng.uniform(-2e-6, 2e-6, (int(moved.sum()), 3))
+    nm, dec, _ = points_map(pts.astype(np.float32), res=res, seed=seed, device=dev,
+                                        buffer_size=1 << 22, nn_k=nn_k)
+    return nm, dec, res
+
+
+@pytest.mark.parametrize("nn_k", [8, 6])
+def test_equal_and_near_equal_distances_match_oracle(dev, nn_k):
+    """Candidates at exactly equal distances (a query on a lattice node is equidistant from 8
+    cell centres) and at distances a few ulps apart.  The reference keeps the k nearest with a
+    stable sort, ties in cell order (model/neural_points.py:561-565); the grid kernel's packed-key
+    selection truncates d2 to 18 mantissa bits and must fall back to the exact order where that
+    matters.  Two layers (<= 32 occupied cells per query: packed keys) and six (33 > 32:
+    the segmented scan).  A different neighbour set would move the SDF by ~1e-2."""
+    nm, dec, res = _lattice_map(dev, nn_k, 3 + nn_k)
+    assert nm.backend() == "grid"
+    rng = np.random.default_rng(11)
+    a, b = np.meshgrid(np.arange(2, 23), np.arange(2, 23), indexing="ij")
+    nodes = np.stack([a.ravel(), b.ravel()], 1).astype(np.float64)
+    qs = []
+    for z in (1.0, 0.5, 3.0):                     # lattice nodes, cell centres in z, deep layers
+        qs.append(np.concatenate([nodes, np.full((nodes.shape[0], 1), z)], 1) * res)
+        qs.append(np.concatenate([nodes + [0.5, 0.0], np.full((nodes.shape[0], 1), z)], 1) * res)
+    q = np.concatenate(qs, 0)
+    q = np.concatenate([q, q + rng.uniform(-3e-7, 3e-7, q.shape)], 0).astype(np.float32)
+    qt = torch.from_numpy(q).to(dev)
+    sdf, grad, nn, _, _ = P.query_sdf(nm, dec, qt, query_locally=False, want_grad=True)
+    st, mlp = H.oracle_state(nm), H.oracle_mlp(dec)
+    osdf, ograd, _, oq = O.sdf_and_grad(st, mlp, q, nn_k, O.neighbor_offsets(2, 0.2), nm.max_valid_dist2,
+                                        True, False)
+    np.testing.assert_array_equal(_np(nn), oq.nn_counts)
+    assert int(oq.nn_counts.max()) > 32 and float((oq.nn_counts > nn_k).mean()) > 0.5
+    np.testing.assert_allclose(_np(sdf), osdf, atol=1e-5)
+    gerr = np.abs(_np(grad) - ograd).max(-1) / np.maximum(np.abs(ograd).max(-1), 1e-3)
+    assert float(gerr.max()) < 1e-3
