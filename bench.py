@@ -22,8 +22,9 @@ RCCL when N > 1).
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
 mean duration of the SDF+grad kernel alone (HIP events on the launch stream around
-pin_query_sdf_grid_sorted with the sort precomputed); the ordering pass is reported beside it.  cpu_baseline: the numpy oracle
-(oracle/pin_oracle.py, single thread) on one full batch, rank 0 at N=1 only.
+pin_query_sdf_grid_sorted with the sort precomputed); the ordering pass is reported beside it.  cpu_baseline: the
+PyTorch-CPU restatement (oracle/pin_torch_cpu.py, every core the process may use, median of 5) on one full batch,
+rank 0 at N=1 only.
 """
 import argparse
 import json
