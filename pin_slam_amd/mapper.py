@@ -152,14 +152,19 @@ class Mapper:
 
     # ---------------------------------------------------------------- data pool
     def dynamic_filter(self, points_torch, type_2_on: bool = False):
-        """utils/mapper.py:79-108 (strategy 1): measurements in confidently free space are
-        dynamic.  One fused query (local map, SDF + certainty) instead of query_feature + sdf."""
-        if type_2_on:
-            raise NotImplementedError("dynamic_filter type_2 (gradient-norm test) is not on the fused path")
-        sdf, _, _, cert, _ = query_sdf(self.neural_points, self.geo_mlp, points_torch, query_locally=True,
-                                       want_grad=False, want_certainty=True)
+        """utils/mapper.py:79-108.  Strategy 1: measurements in confidently free space are dynamic.
+        Strategy 2 (type_2_on): also dynamic where the SDF's analytic gradient is flat
+        (|grad| <= 0.3) at a certain point (certainty >= 0.5) -- the reference's get_gradient of
+        sdf_pred w.r.t. the points, here the fused kernel's closed-form gradient.  One fused query
+        (local map, SDF + certainty [+ gradient]) instead of query_feature + sdf + autograd."""
+        sdf, grad, _, cert, _ = query_sdf(self.neural_points, self.geo_mlp, points_torch, query_locally=True,
+                                          want_grad=bool(type_2_on), want_certainty=True)
         c = self.config
-        return (cert < c.dynamic_certainty_thre) | (sdf < c.dynamic_sdf_ratio_thre * c.voxel_size_m)
+        static_mask = (cert < c.dynamic_certainty_thre) | (sdf < c.dynamic_sdf_ratio_thre * c.voxel_size_m)
+        if type_2_on:
+            min_grad_norm, certainty_thre = 0.3, 0.5            # utils/mapper.py:101-102
+            static_mask = static_mask & ((grad.norm(dim=-1) > min_grad_norm) | (cert < certainty_thre))
+        return static_mask
 
     def _used_poses(self):
         """utils/mapper.py:205-211."""

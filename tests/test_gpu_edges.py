@@ -178,3 +178,39 @@ def test_equal_and_near_equal_distances_match_oracle(dev, nn_k):
     np.testing.assert_allclose(_np(sdf), osdf, atol=1e-5)
     gerr = np.abs(_np(grad) - ograd).max(-1) / np.maximum(np.abs(ograd).max(-1), 1e-3)
     assert float(gerr.max()) < 1e-3
+
+
+def test_dynamic_filter_both_strategies_match_oracle(dev):
+    """Mapper.dynamic_filter (utils/mapper.py:79-108): strategy 1 (certain free space: certainty
+    and SDF thresholds) and strategy 2 (type_2_on: also a flat analytic gradient at a certain
+    point, |grad| <= 0.3 and certainty >= 0.5) against the oracle's SDF, gradient and queried
+    certainty.  The thresholds are set (config) or scaled into (decoder output weights, which the
+    gradient is linear in) the middle of this map's values so both outcomes occur; decisions
+    within the parity tolerance of a threshold are not compared."""
+    nm, dec, pts = H.surface_map(80, device=dev, buffer_size=1 << 20)
+    q = H.surface_queries(pts, 4096, seed=5, device=dev)
+    qn = _np(q)
+    off = O.neighbor_offsets(2, 0.2)
+
+    def oracle():
+        return O.sdf_and_grad(H.oracle_state(nm), H.oracle_mlp(dec), qn, 8, off, nm.max_valid_dist2, True, True)
+    _, ograd, _, _ = oracle()
+    with torch.no_grad():   # median gradient norm -> 0.3
+        dec.lout.weight.mul_(0.3 / float(np.median(np.linalg.norm(ograd, axis=-1))))
+    osdf, ograd, _, oq = oracle()
+    c = nm.config
+    c.dynamic_certainty_thre = float(np.median(oq.certainty))
+    c.dynamic_sdf_ratio_thre = float(np.median(osdf)) / c.voxel_size_m
+    thr_s = np.float32(c.dynamic_sdf_ratio_thre * c.voxel_size_m)
+    cert, gn = oq.certainty, np.linalg.norm(ograd.astype(np.float64), axis=-1)
+    s1 = (cert < c.dynamic_certainty_thre) | (osdf < thr_s)
+    s2 = s1 & ((gn > 0.3) | (cert < 0.5))
+    near = ((np.abs(osdf - thr_s) <= 1e-5) | (np.abs(gn - 0.3) <= 1e-4) |
+            (np.abs(cert - c.dynamic_certainty_thre) <= 1e-5) | (np.abs(cert - 0.5) <= 1e-5))
+    assert near.mean() < 0.01
+    mapper = P.Mapper(c, None, nm, dec)
+    for type_2, ref in ((False, s1), (True, s2)):
+        got = _np(mapper.dynamic_filter(q, type_2))
+        assert got.dtype == np.bool_ and got.shape == (qn.shape[0],)
+        np.testing.assert_array_equal(got[~near], ref[~near])
+        assert 0.05 < float(ref.mean()) < 0.95
