@@ -530,6 +530,16 @@ int pin_train_gather_packed(const float* packed_pool, int64_t pool_rows, const i
                             float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
                             void* stream);
 
+/* pin_train_gather_packed_split -- pin_train_gather_packed with get_batch's two draws kept apart
+ * (utils/mapper.py:335-340): batch rows r < n_index gather pool row index[r], the remaining
+ * n_main - n_index rows gather new_idx[index_new[r - n_index]] (new_idx: the new samples' pool rows,
+ * new_count of them) -- the torch.cat and the new_idx indexing done by the gather itself.
+ * index_new entries outside [0, new_count) are clamped to 0 and reported in *error. */
+int pin_train_gather_packed_split(const float* packed_pool, int64_t pool_rows, const int64_t* index, int64_t n_index,
+                                  const int64_t* new_idx, int64_t new_count, const int64_t* index_new,
+                                  const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out,
+                                  float* weight_out, int32_t* error, void* stream);
+
 /*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping
  * iteration (mapper.py:461-468, :683-711; neural_points.py:528-674 with training_mode): fills
@@ -565,6 +575,13 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
 /* pin_adam_step -- dense Adam over n floats in place (torch.optim.Adam, weight_decay 0). */
 int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const PinAdamStep* a,
                   void* stream);
+
+/* pin_adam_step_segments -- pin_adam_step over the n feature floats and pin_adam_segments over the
+ * decoder's segments in ONE launch, with the same scalars a (a training mapper iteration: the
+ * feature and decoder parameter groups of the reference's one optimizer, utils/tools.py:89-116). */
+int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
+                           float* seg_exp_avg_sq, const PinAdamStep* a, void* stream);
 
 /* pin_adam_segments -- the same Adam update over nseg (<= 8) separate parameter tensors params[k]
  * of sizes[k] floats whose gradients and moments lie end to end in contiguous grad / exp_avg /

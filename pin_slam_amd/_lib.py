@@ -169,6 +169,8 @@ _SIGS = {
     "pin_pool_pack": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, c_void_p],
     "pin_train_gather_packed": [c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p],
+    "pin_train_gather_packed_split": [c_void_p, i64, c_void_p, i64, c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,
@@ -176,6 +178,8 @@ _SIGS = {
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_adam_rows": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_adam_segments": [_P(c_void_p), _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
+    "pin_adam_step_segments": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(c_void_p), _P(i64), i32, c_void_p,
+                               c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
     "pin_map_workspace_bytes": [i64],
     "pin_voxel_down_sample": [c_void_p, i64, f32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_map_insert": [c_void_p, c_void_p, i64, f32, c_void_p, i64, c_void_p, c_void_p, i64, c_void_p, i64, f32, f32,

@@ -329,11 +329,23 @@ k_pool_pack(const float* __restrict__ coord, const float* __restrict__ label, co
 // k_train_gather over the packed pool: the row's two 16-B halves of one 32-B record
 __global__ void __launch_bounds__(kBlock)
 k_train_gather_packed(const float4* __restrict__ pool, int64_t pool_rows, const int64_t* __restrict__ index,
-                      PinTrainCfg c, float* __restrict__ rows, float* __restrict__ label, int64_t* __restrict__ ts,
-                      float* __restrict__ weight, int* __restrict__ error) {
+                      int64_t n_index, const int64_t* __restrict__ new_idx, int64_t new_count,
+                      const int64_t* __restrict__ index_new, PinTrainCfg c, float* __restrict__ rows,
+                      float* __restrict__ label, int64_t* __restrict__ ts, float* __restrict__ weight,
+                      int* __restrict__ error) {
     const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= c.n_main) return;
-    int64_t i = index[r];
+    int64_t i;
+    if (r < n_index) {
+        i = index[r];
+    } else {   // get_batch's new-sample rows: new_idx[index_new[.]] (utils/mapper.py:335-340)
+        int64_t j = index_new[r - n_index];
+        if (j < 0 || j >= new_count) {
+            if (error) atomicOr(error, 1);
+            j = 0;
+        }
+        i = new_idx[j];
+    }
     if (i < 0 || i >= pool_rows) {   // never gather outside the pool: clamp and report
         if (error) atomicOr(error, 1);
         i = 0;
@@ -1002,11 +1014,29 @@ __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ 
 // units 4b..4b+3 (64 products of T, and of T' with the analytic eikonal), 4 waves over interleaved
 // block ranges, then mlp_grad += dW1 = w2 o (T + s T')[:, 0:11], db1 = w2 o T[:, 11],
 // dW2 = rowwise W1 . (T + s T')[:, 0:11] + b1 o T[:, 11]; block 0 also adds db2 = sum so.
+// Block kH / 4 (launched when loss_out is wanted) reduces the loss partials instead, so that a
+// training-decoder backward ends with one launch, not k_loss_final + this.
 __global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk, int extra,
-                                                           PinMlp m, float* __restrict__ out) {
+                                                           PinMlp m, float* __restrict__ out,
+                                                           const double* __restrict__ lpart, int64_t nl,
+                                                           double* __restrict__ loss_out) {
     __shared__ float red[kWaves][2][64];
     __shared__ float s_b2[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (blockIdx.x == kH / 4) {   // the loss: fixed-order sum of the per-wave partials
+        __shared__ double lred[kWaves];
+        double v = 0.0;
+        for (int64_t k = threadIdx.x; k < nl; k += kBlock) v += lpart[k];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) lred[wave] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double tot = 0.0;
+            for (int w = 0; w < kWaves; ++w) tot += lred[w];
+            loss_out[0] = tot;
+        }
+        return;
+    }
     const int c = 4 * blockIdx.x + (lane >> 4), i = lane & 15;
     const int e = c * 16 + i;
     float t = 0.f, te = 0.f, b2 = 0.f;
@@ -1065,10 +1095,10 @@ __device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v,
     return p;
 }
 
-__global__ void __launch_bounds__(kBlock)
-k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
-       PinAdamStep a) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// dense Adam over 4 consecutive floats per thread (k_adam, k_adam_step_segments)
+__device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ prm, float* __restrict__ grad,
+                                                float* __restrict__ m_, float* __restrict__ v_, int64_t n,
+                                                const PinAdamStep& a) {
     const int64_t i0 = 4 * t;
     if (i0 >= n) return;
     if (i0 + 4 <= n) {
@@ -1092,6 +1122,12 @@ k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_
         v_[i] = v;
         if (a.zero_grad) grad[i] = 0.f;
     }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
+       PinAdamStep a) {
+    adam_dense_body((int64_t)blockIdx.x * kBlock + threadIdx.x, prm, grad, m_, v_, n, a);
 }
 
 // Adam on listed rows of a [rows, 8] parameter (the owned rows of a spatially sharded mapper):
@@ -1122,9 +1158,10 @@ struct AdamSegs {
     int n;
 };
 
-__global__ void __launch_bounds__(kBlock)
-k_adam_segments(AdamSegs sg, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, PinAdamStep a) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// one element of the segments (k_adam_segments, k_adam_step_segments)
+__device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg, float* __restrict__ grad,
+                                                  float* __restrict__ m_, float* __restrict__ v_,
+                                                  const PinAdamStep& a) {
     if (t >= sg.off[sg.n]) return;
     int s = 0;
 #pragma unroll
@@ -1138,15 +1175,28 @@ k_adam_segments(AdamSegs sg, float* __restrict__ grad, float* __restrict__ m_, f
     if (a.zero_grad) grad[t] = 0.f;
 }
 
+__global__ void __launch_bounds__(kBlock)
+k_adam_segments(AdamSegs sg, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, PinAdamStep a) {
+    adam_segment_body((int64_t)blockIdx.x * kBlock + threadIdx.x, sg, grad, m_, v_, a);
+}
+
+// The feature Adam and the decoder's segments in one launch (a training mapper iteration): the
+// first nb_dense blocks run k_adam's body, the rest k_adam_segments' (the same scalars).
+__global__ void __launch_bounds__(kBlock)
+k_adam_step_segments(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_,
+                     float* __restrict__ v_, int64_t n, int64_t nb_dense, AdamSegs sg, float* __restrict__ sgrad,
+                     float* __restrict__ sm, float* __restrict__ sv, PinAdamStep a) {
+    if ((int64_t)blockIdx.x < nb_dense) adam_dense_body((int64_t)blockIdx.x * kBlock + threadIdx.x, prm, grad, m_, v_, n, a);
+    else adam_segment_body(((int64_t)blockIdx.x - nb_dense) * kBlock + threadIdx.x, sg, sgrad, sm, sv, a);
+}
+
 }  // namespace
 
 extern "C" {
 
-int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, float* grad, float* exp_avg,
-                      float* exp_avg_sq, const PinAdamStep* a, void* stream) {
-    if (!a || !params || !sizes || nseg < 1 || nseg > kMaxSeg || !grad || !exp_avg || !exp_avg_sq) return PIN_ERR_ARG;
-    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
-    AdamSegs sg{};
+static int adam_segs(float* const* params, const int64_t* sizes, int nseg, AdamSegs& sg) {
+    if (!params || !sizes || nseg < 1 || nseg > kMaxSeg) return PIN_ERR_ARG;
+    sg = AdamSegs{};
     sg.n = nseg;
     sg.off[0] = 0;
     for (int k = 0; k < nseg; ++k) {
@@ -1154,6 +1204,34 @@ int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, floa
         sg.p[k] = params[k];
         sg.off[k + 1] = sg.off[k] + sizes[k];
     }
+    return PIN_OK;
+}
+
+int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
+                           float* seg_exp_avg_sq, const PinAdamStep* a, void* stream) {
+    if (!a || n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) || !seg_grad || !seg_exp_avg ||
+        !seg_exp_avg_sq)
+        return PIN_ERR_ARG;
+    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
+    AdamSegs sg;
+    const int rc = adam_segs(params, sizes, nseg, sg);
+    if (rc != PIN_OK) return rc;
+    const int64_t nb_dense = (n + 4 * kBlock - 1) / (4 * kBlock);
+    const int64_t nb_seg = (sg.off[nseg] + kBlock - 1) / kBlock;
+    if (nb_dense + nb_seg == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_adam_step_segments, dim3((unsigned)(nb_dense + nb_seg)), dim3(kBlock), 0, as_stream(stream),
+                       param, grad, exp_avg, exp_avg_sq, n, nb_dense, sg, seg_grad, seg_exp_avg, seg_exp_avg_sq, *a);
+    return launch_status();
+}
+
+int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, float* grad, float* exp_avg,
+                      float* exp_avg_sq, const PinAdamStep* a, void* stream) {
+    if (!a || !grad || !exp_avg || !exp_avg_sq) return PIN_ERR_ARG;
+    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
+    AdamSegs sg;
+    const int rc = adam_segs(params, sizes, nseg, sg);
+    if (rc != PIN_OK) return rc;
     if (sg.off[nseg] == 0) return PIN_OK;
     hipLaunchKernelGGL(k_adam_segments, grid_for(sg.off[nseg]), dim3(kBlock), 0, as_stream(stream), sg, grad, exp_avg,
                        exp_avg_sq, *a);
@@ -1189,18 +1267,39 @@ int pin_pool_pack(const float* coord, const float* label, const int64_t* ts, con
     return launch_status();
 }
 
+static int gather_packed_args(const float* packed_pool, int64_t pool_rows, const PinTrainCfg* cfg,
+                              const float* rows_out, const float* label_out) {
+    if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
+    if (cfg->n_stencil > 0 && (cfg->n_stencil - 1) * (int64_t)cfg->decimation >= cfg->n_main) return PIN_ERR_ARG;
+    if (cfg->n_main == 0) return PIN_OK;
+    if (!packed_pool || ((uintptr_t)packed_pool & 15) || !rows_out || !label_out || pool_rows < 1) return PIN_ERR_ARG;
+    return PIN_OK;
+}
+
 int pin_train_gather_packed(const float* packed_pool, int64_t pool_rows, const int64_t* index, const PinTrainCfg* cfg,
                             float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
                             void* stream) {
-    if (!cfg || cfg->n_main < 0 || cfg->n_stencil < 0 || cfg->decimation < 1) return PIN_ERR_ARG;
-    if (cfg->n_stencil > 0 && (cfg->n_stencil - 1) * (int64_t)cfg->decimation >= cfg->n_main) return PIN_ERR_ARG;
-    const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
-    if (rows == 0) return PIN_OK;
-    if (!packed_pool || ((uintptr_t)packed_pool & 15) || !index || !rows_out || !label_out || pool_rows < 1)
-        return PIN_ERR_ARG;
+    const int rc = gather_packed_args(packed_pool, pool_rows, cfg, rows_out, label_out);
+    if (rc != PIN_OK || cfg->n_main == 0) return rc;
+    if (!index) return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream),
-                       (const float4*)packed_pool, pool_rows, index, *cfg, rows_out, label_out, ts_out, weight_out,
-                       (int*)error);
+                       (const float4*)packed_pool, pool_rows, index, cfg->n_main, nullptr, (int64_t)0, nullptr, *cfg,
+                       rows_out, label_out, ts_out, weight_out, (int*)error);
+    return launch_status();
+}
+
+int pin_train_gather_packed_split(const float* packed_pool, int64_t pool_rows, const int64_t* index, int64_t n_index,
+                                  const int64_t* new_idx, int64_t new_count, const int64_t* index_new,
+                                  const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out,
+                                  float* weight_out, int32_t* error, void* stream) {
+    if (!cfg || n_index < 0 || n_index > cfg->n_main) return PIN_ERR_ARG;
+    if (n_index < cfg->n_main && (!new_idx || !index_new || new_count < 1)) return PIN_ERR_ARG;
+    if (n_index > 0 && !index) return PIN_ERR_ARG;
+    const int rc = gather_packed_args(packed_pool, pool_rows, cfg, rows_out, label_out);
+    if (rc != PIN_OK || cfg->n_main == 0) return rc;
+    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream),
+                       (const float4*)packed_pool, pool_rows, index, n_index, new_idx, new_count, index_new, *cfg,
+                       rows_out, label_out, ts_out, weight_out, (int*)error);
     return launch_status();
 }
 
@@ -1314,8 +1413,11 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     }
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
-    if (loss_out) hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
-    if (mlp_grad) hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4), dim3(kBlock), 0, s, mpart, nblk, extra, *mlp, mlp_grad);
+    if (mlp_grad)   // decoder gradients (+ the loss in one more block)
+        hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4 + (loss_out ? 1 : 0)), dim3(kBlock), 0, s, mpart, nblk, extra,
+                           *mlp, mlp_grad, lpart, nblk * kWaves, loss_out);
+    else if (loss_out)
+        hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
     return launch_status();
 }
 

@@ -413,6 +413,14 @@ class Mapper:
         """The pool rows of one batch: get_batch's sampling (utils/mapper.py:323-350), same draws.
         rows / new_idx: the pool rows (and new samples) to draw from instead of the whole pool
         (a spatially sharded rank's slab).  self._n_new_rows: rows at the end that are new samples."""
+        index_history, new_sel, index_new = self._batch_parts(rows, new_idx)
+        if new_sel is None:
+            return index_history
+        return torch.cat((index_history, new_sel[index_new]), dim=0)
+
+    def _batch_parts(self, rows=None, new_idx=None):
+        """_batch_index's two draws kept apart: (history rows, new_idx or None, draw into new_idx or
+        None); the batch is history rows followed by new_idx[draw] (the gather concatenates)."""
         bs = int(self.config.bs)
         bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
         count = self.pool_sample_count if rows is None else rows.shape[0]
@@ -427,9 +435,8 @@ class Mapper:
                 index_history = pick(self._randint(count, bs_history))
                 index_new_batch = self._randint(new_idx_count, bs_new)
                 self._n_new_rows = bs_new
-                return torch.cat((index_history, new_idx[index_new_batch]), dim=0)
-            return pick(self._randint(count, bs))
-        return pick(self._randint(count, bs))
+                return index_history, new_idx, index_new_batch
+        return pick(self._randint(count, bs)), None, None
 
     def get_batch(self, global_coord=False):
         """utils/mapper.py:323-361."""
@@ -504,9 +511,10 @@ class Mapper:
         for _ in range(iter_count):
             if fused:
                 if part is None:
-                    index = self._batch_index()
+                    index, new_sel, index_new = self._batch_parts()
                     self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
-                                    world, index=index, weight=self.weight_pool, packed=packed)
+                                    world, index=index, weight=self.weight_pool, packed=packed,
+                                    index_new=None if new_sel is None else (new_sel, index_new))
                 else:
                     index = self._batch_index(slab_rows, slab_new)
                     scale_h, scale_n = scales(int(index.shape[0]) - self._n_new_rows, self._n_new_rows)
@@ -596,7 +604,7 @@ class Mapper:
                 and (t is None or (t.dtype == torch.int64 and t.is_contiguous())))
 
     def train_step(self, coord, sdf_label, ts, grad_features, mlp_grad=None, world=1, index=None, reduce=True,
-                   scale=None, n_tail=0, scale_tail=0.0, weight=None, packed=None):
+                   scale=None, n_tail=0, scale_tail=0.0, weight=None, packed=None, index_new=None):
         """Forward + backward of one iteration: grad_features [L+1,8] (+ mlp_grad [833]) += dL/d*,
         SUM all-reduced over the group when world > 1 and reduce.  Returns the device loss tensor.
         index ([N] int64): coord / sdf_label / ts are then the sample pools and the batch is their
@@ -605,7 +613,9 @@ class Mapper:
         stencil groups based on them) take scale_tail instead (slab sharding's new-sample rows).
         weight: the batch rows' sample weights (the weight pool with index), used as |weight| by the
         BCE term when loss_weight_on (utils/mapper.py:514-516).
-        packed: the same pools as one 32-B record per sample (_packed_pool), gathered instead."""
+        packed: the same pools as one 32-B record per sample (_packed_pool), gathered instead.
+        index_new: (new_idx, draw) -- the batch continues with rows new_idx[draw] after index
+        (get_batch's new samples, _batch_parts), concatenated by the packed gather itself."""
         c = self.config
         nm = self.neural_points
         weighted = bool(getattr(c, "loss_weight_on", False)) and weight is not None
@@ -622,7 +632,13 @@ class Mapper:
             q = coord
             _lib.require_device(q)
             index = index.to(device=q.device, dtype=torch.int64).contiguous()
-            n = index.shape[0]
+            if index_new is not None:
+                new_sel, draw = (t.to(device=q.device, dtype=torch.int64).contiguous() for t in index_new)
+                if packed is None:    # the unpacked gather takes one index
+                    index, index_new = torch.cat((index, new_sel[draw]), dim=0), None
+                else:
+                    index_new = (new_sel, draw)
+            n = index.shape[0] + (0 if index_new is None else index_new[1].shape[0])
         if grad_features is not None and (grad_features.shape[1] != 8 or not grad_features.is_contiguous()):
             raise ValueError("grad_features must be a contiguous [L+1, 8] float32 tensor")
         dec = int(c.gradient_decimation)
@@ -655,7 +671,13 @@ class Mapper:
             label = b.label
             ts64 = b.ts if ts is not None else None
             wrow = b.wrow if weighted else None
-            if packed is not None:
+            if packed is not None and index_new is not None:
+                new_sel, draw = index_new
+                _lib.call("pin_train_gather_packed_split", _lib.ptr(packed), int(packed.shape[0]), _lib.ptr(index),
+                          int(index.shape[0]), _lib.ptr(new_sel), int(new_sel.shape[0]), _lib.ptr(draw),
+                          ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), _lib.ptr(wrow),
+                          _lib.ptr(b.gather_error), s)
+            elif packed is not None:
                 _lib.call("pin_train_gather_packed", _lib.ptr(packed), int(packed.shape[0]), _lib.ptr(index),
                           ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), _lib.ptr(wrow),
                           _lib.ptr(b.gather_error), s)
@@ -714,7 +736,13 @@ class Mapper:
         self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
-        if partition is None:
+        segs = self._adam_segments(mlp_params, m_grad) if m_grad is not None else None
+        if partition is None and segs is not None:
+            # the features and the decoder's four tensors in one launch (same scalars)
+            _lib.call("pin_adam_step_segments", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
+                      fdata.numel(), segs[0], segs[1], len(mlp_params), _lib.ptr(m_grad), _lib.ptr(m_m),
+                      _lib.ptr(m_v), ctypes.byref(st), s)
+        elif partition is None:
             _lib.call("pin_adam_step", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
                       fdata.numel(), ctypes.byref(st), s)
         else:
@@ -724,21 +752,27 @@ class Mapper:
         feats = self.neural_points.local_geo_features
         self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
         if m_grad is not None:
-            # the decoder's parameters in one launch: their gradients / moments lie end to end
-            for p in mlp_params:
-                if not (p.data.is_contiguous() and p.data.dtype == torch.float32):
-                    raise RuntimeError("decoder parameters must be contiguous float32")
-            n = len(mlp_params)
-            ptrs = (ctypes.c_void_p * n)(*[p.data.data_ptr() for p in mlp_params])
-            sizes = (ctypes.c_int64 * n)(*[p.numel() for p in mlp_params])
-            if sum(sizes) != m_grad.numel():
-                raise RuntimeError("decoder parameters do not match the gradient layout")
-            _lib.call("pin_adam_segments", ptrs, sizes, n, _lib.ptr(m_grad), _lib.ptr(m_m), _lib.ptr(m_v),
-                      ctypes.byref(st), s)
+            if partition is not None:   # the decoder's parameters in one launch of their own
+                _lib.call("pin_adam_segments", segs[0], segs[1], len(mlp_params), _lib.ptr(m_grad), _lib.ptr(m_m),
+                          _lib.ptr(m_v), ctypes.byref(st), s)
             # the step wrote through raw pointers: bump the versions so views built on the
             # parameters (the matrix-core operand image of mlp_view) are rebuilt before the next use
             for p in mlp_params:
                 torch.autograd.graph.increment_version(p)
+
+    @staticmethod
+    def _adam_segments(mlp_params, m_grad):
+        """(pointer array, size array) of the decoder tensors, whose gradients / moments lie end to
+        end in m_grad / m_m / m_v (pin_adam_segments' layout)."""
+        for p in mlp_params:
+            if not (p.data.is_contiguous() and p.data.dtype == torch.float32):
+                raise RuntimeError("decoder parameters must be contiguous float32")
+        n = len(mlp_params)
+        ptrs = (ctypes.c_void_p * n)(*[p.data.data_ptr() for p in mlp_params])
+        sizes = (ctypes.c_int64 * n)(*[p.numel() for p in mlp_params])
+        if sum(sizes) != m_grad.numel():
+            raise RuntimeError("decoder parameters do not match the gradient layout")
+        return ptrs, sizes
 
 
     # ---------------------------------------------------------------- autograd helpers

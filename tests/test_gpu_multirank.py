@@ -61,7 +61,11 @@ def _worker(rank, world, port, case, shard, q):
         step = mapper.train_step
 
         def recorded(*a, **kw):
-            calls.append(dict(index=kw["index"].cpu().numpy(), scale=kw.get("scale"), n_tail=int(kw.get("n_tail", 0)),
+            index = kw["index"]
+            if kw.get("index_new") is not None:      # a batch split into history rows + new_idx[draw]
+                new_sel, draw = kw["index_new"]
+                index = torch.cat((index, new_sel[draw]), dim=0)
+            calls.append(dict(index=index.cpu().numpy(), scale=kw.get("scale"), n_tail=int(kw.get("n_tail", 0)),
                               scale_tail=float(kw.get("scale_tail", 0.0)), world=int(a[5])))
             return step(*a, **kw)
         mapper.train_step = recorded
