@@ -225,6 +225,79 @@ def test_adam_matches_torch(dev):
         np.testing.assert_allclose(_np(mine), _np(ref), rtol=1e-6, atol=1e-7)
 
 
+def test_fused_adam_equals_separate_launches(dev):
+    """pin_adam_step_segments (features + the decoder's segments in one launch, the mapper's
+    training iteration) against pin_adam_step + pin_adam_segments on copies: bitwise equal."""
+    import ctypes
+    from pin_slam_amd.mapper import adam_scalars
+    g = torch.Generator(device="cpu").manual_seed(1)
+    n = 8 * 1237
+    sizes = [704, 64, 64, 1]
+    fa = [torch.randn(n, generator=g).to(dev) for _ in range(4)]          # param, grad, m, v
+    fa[3] = fa[3].abs()
+    seg = [torch.randn(k, generator=g).to(dev) for k in sizes]
+    sg, sm, sv = (torch.randn(sum(sizes), generator=g).to(dev) for _ in range(3))
+    sv = sv.abs()
+    fb, segb = [t.clone() for t in fa], [t.clone() for t in seg]
+    sgb, smb, svb = sg.clone(), sm.clone(), sv.clone()
+    st = adam_scalars(0.01, 3, 1e-15)
+    ptrs = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in seg])
+    szs = (ctypes.c_int64 * 4)(*sizes)
+    _lib.call("pin_adam_step_segments", *[_lib.ptr(t) for t in fa], n, ptrs, szs, 4, _lib.ptr(sg), _lib.ptr(sm),
+              _lib.ptr(sv), ctypes.byref(st), _lib.stream())
+    _lib.call("pin_adam_step", *[_lib.ptr(t) for t in fb], n, ctypes.byref(st), _lib.stream())
+    ptrs_b = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in segb])
+    _lib.call("pin_adam_segments", ptrs_b, szs, 4, _lib.ptr(sgb), _lib.ptr(smb), _lib.ptr(svb), ctypes.byref(st),
+              _lib.stream())
+    torch.cuda.synchronize()
+    for a, b in zip(fa + seg + [sg, sm, sv], fb + segb + [sgb, smb, svb]):
+        assert torch.equal(a, b)
+    assert float(fa[1].abs().max()) == 0.0 and float(sg.abs().max()) == 0.0   # gradients zeroed
+
+
+def test_split_gather_equals_concatenated_index(dev):
+    """pin_train_gather_packed_split (get_batch's history draw + new_idx[draw], utils/mapper.py:
+    335-340) against pin_train_gather_packed over the torch.cat of the same rows: bitwise equal
+    rows (batch + stencil), labels, ts, weights; a draw outside new_idx is clamped and reported."""
+    import ctypes
+    g = torch.Generator(device="cpu").manual_seed(2)
+    N, n_hist, n_new, n_sel = 5000, 700, 324, 300
+    coord = torch.randn(N, 3, generator=g).to(dev)
+    label = torch.randn(N, generator=g).to(dev)
+    ts = torch.randint(0, 1 << 40, (N,), generator=g).to(dev)
+    weight = torch.randn(N, generator=g).to(dev)
+    packed = P.Mapper._pack(coord, label, ts, weight)
+    index = torch.randint(0, N, (n_hist,), generator=g).to(dev)
+    new_sel = torch.randint(0, N, (n_sel,), generator=g).to(dev)
+    draw = torch.randint(0, n_sel, (n_new,), generator=g).to(dev)
+    n = n_hist + n_new
+    cfg = _lib.PinTrainCfg(n_main=n, n_stencil=(n + 9) // 10, decimation=10, nn_k=8, weighted_first=1, eps=0.06,
+                           sigma=0.1, weight_e=0.1, grad_scale=1.0, flags=0, n_tail=0, grad_scale_tail=0.0)
+    rows = n + 6 * cfg.n_stencil
+
+    def outs():
+        return (torch.empty(rows * 3, device=dev), torch.empty(n, device=dev),
+                torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, device=dev),
+                torch.zeros(1, dtype=torch.int32, device=dev))
+    a, b = outs(), outs()
+    full = torch.cat((index, new_sel[draw]))
+    _lib.call("pin_train_gather_packed", _lib.ptr(packed), N, _lib.ptr(full), ctypes.byref(cfg),
+              *[_lib.ptr(t) for t in a], _lib.stream())
+    _lib.call("pin_train_gather_packed_split", _lib.ptr(packed), N, _lib.ptr(index), n_hist, _lib.ptr(new_sel), n_sel,
+              _lib.ptr(draw), ctypes.byref(cfg), *[_lib.ptr(t) for t in b], _lib.stream())
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert int(b[4].item()) == 0
+    bad = draw.clone()
+    bad[5] = n_sel
+    c = outs()
+    _lib.call("pin_train_gather_packed_split", _lib.ptr(packed), N, _lib.ptr(index), n_hist, _lib.ptr(new_sel), n_sel,
+              _lib.ptr(bad), ctypes.byref(cfg), *[_lib.ptr(t) for t in c], _lib.stream())
+    torch.cuda.synchronize()
+    assert int(c[4].item()) == 1
+
+
 def test_fat_cache_sees_training_writes(dev):
     """Local inference queries read cached copies of the local features and certainties (fat
     compact records).  mapping() writes those through raw pointers (Adam, certainty / ts side
