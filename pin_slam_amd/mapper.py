@@ -566,36 +566,20 @@ class Mapper:
             return None, None, None, None
         group = getattr(self, "group", None)
         nm = self.neural_points
-        dev = nm.local_neural_points.device
         if not fused:
             raise NotImplementedError("shard='space' samples device pools through the fused batch path")
-        from .sharding import SlabPartition, query_reach
+        from .sharding import SlabPartition, query_reach, slab_batch_plan
         part = SlabPartition(nm.local_neural_points, query_reach(nm, self.config), group,
                              layout=getattr(self, "slab_layout", "auto"))
-        mask = part.sample_mask(self.global_coord_pool[: self.pool_sample_count])
-        slab_rows = torch.nonzero(mask).flatten()
-        slab_new = self.new_idx[mask[self.new_idx]] if self.new_idx is not None else None
-        n_r = 0 if slab_new is None else int(slab_new.numel())
-        cnt = torch.tensor([float(slab_rows.numel()), float(n_r), 1.0 if slab_rows.numel() == 0 else 0.0],
-                           dtype=torch.float64, device=dev)
-        all_reduce(cnt, group=group)
-        if float(cnt[2]) > 0:
+        plan = slab_batch_plan(part, self.global_coord_pool[: self.pool_sample_count], self.new_idx,
+                               int(self.config.bs), int(getattr(self.config, "bs_new_sample", 0)),
+                               self._new_sample_mode())
+        if plan is None:
             warnings.warn("shard='space': a slab holds no pool samples; this mapping() call uses the dense "
                           "gradient all-reduce")
             return None, None, None, None
-        N, n = float(cnt[0]), float(cnt[1])
-        N_r = float(slab_rows.numel())
-        bs = int(self.config.bs)
-        bs_new = min(int(n), int(getattr(self.config, "bs_new_sample", 0))) if (self._new_sample_mode() and n > 0) \
-            else 0
-        bs_hist = bs - bs_new
-
-        def scales(bs_hist_r, bs_new_r):
-            sh = (bs_hist / bs_hist_r) * (N_r / N) if bs_hist_r > 0 else 0.0
-            sn = (bs_new / bs_new_r) * (n_r / n) if bs_new_r > 0 else 0.0
-            return sh, sn
         self._partition = part
-        return part, slab_rows, slab_new, scales
+        return (part,) + plan
 
     def _pools_fusable(self):
         c, l, t = self.global_coord_pool, self.sdf_label_pool, self.time_pool

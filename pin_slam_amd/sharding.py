@@ -275,6 +275,38 @@ class SlabPartition:
                     flat.index_copy_(0, rows_of[s], out[s][: rows_of[s].numel()])
 
 
+def slab_batch_plan(part, pool_coords, new_idx, bs, bs_new_sample, new_mode):
+    """The batch plan of one shard="space" mapping() call on this rank (Mapper._slab_partition):
+    (the slab's pool rows, the slab's new samples, scales), or None on EVERY rank when any slab
+    holds no pool samples (the counts are all-reduced first, so all ranks take the same branch and
+    the call falls back to the dense gradient all-reduce together).
+
+    scales(bs_hist_r, bs_new_r) -> (history-row scale, new-row scale): the rank draws its batch from
+    its slab only, so its rows are weighted to keep the union of the ranks' batches an unbiased
+    estimate of the reference's single batch (utils/mapper.py:323-350: bs_hist rows uniform over
+    the N pool samples, bs_new rows uniform over the n new ones):
+        scale_h = (bs_hist / bs_hist_r) (N_r / N),   scale_n = (bs_new / bs_new_r) (n_r / n)."""
+    mask = part.sample_mask(pool_coords)
+    slab_rows = torch.nonzero(mask).flatten()
+    slab_new = new_idx[mask[new_idx]] if new_idx is not None else None
+    n_r = 0 if slab_new is None else int(slab_new.numel())
+    cnt = torch.tensor([float(slab_rows.numel()), float(n_r), 1.0 if slab_rows.numel() == 0 else 0.0],
+                       dtype=torch.float64, device=pool_coords.device)
+    all_reduce(cnt, group=part.group)
+    if float(cnt[2]) > 0:
+        return None
+    N, n = float(cnt[0]), float(cnt[1])
+    N_r = float(slab_rows.numel())
+    bs_new = min(int(n), int(bs_new_sample)) if (new_mode and n > 0) else 0
+    bs_hist = int(bs) - bs_new
+
+    def scales(bs_hist_r, bs_new_r):
+        sh = (bs_hist / bs_hist_r) * (N_r / N) if bs_hist_r > 0 else 0.0
+        sn = (bs_new / bs_new_r) * (n_r / n) if bs_new_r > 0 else 0.0
+        return sh, sn
+    return slab_rows, slab_new, scales
+
+
 def query_reach(nm, config) -> float:
     """Farthest point a mapping row can touch along a horizontal axis: the neighbour search radius
     (sqrt(max_valid_dist2)) + the numerical-gradient step, with a margin for float rounding."""

@@ -170,7 +170,8 @@ def _shard_worker(rank, world, port, q, grid, layout):
 
 @pytest.mark.parametrize("world,grid,layout,shape", [(2, (120, 40), "auto", (2, 1)),
                                                     (4, (60, 60), "auto", (2, 2)),
-                                                    (4, (60, 60), "1d", (4, 1))])
+                                                    (4, (60, 60), "1d", (4, 1)),
+                                                    (8, (100, 80), "auto", (4, 2))])
 def test_slab_sharded_mapping_equals_dense_data_parallel(world, grid, layout, shape):
     """shard='space' (pin_slam_amd.sharding): halo gradients to owners, Adam on owned rows (and
     the shared row), halo features refreshed, side effects reconciled, owned rows all-gathered --
@@ -212,6 +213,60 @@ def test_slab_sharded_mapping_equals_dense_data_parallel(world, grid, layout, sh
         np.testing.assert_allclose(res[r][1], st.local_features, rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(res[r][2], cert0 + cert_delta, rtol=1e-5, atol=1e-5)
         np.testing.assert_array_equal(res[r][3], ts)
+
+
+def _plan_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pin_slam_amd.sharding import SlabPartition, slab_batch_plan
+        st, _, _, cfg = _shard_setup(100, 80)
+        reach = float(np.sqrt(cfg["maxd2"])) * 1.001 + cfg["eps"] + 1e-3
+        part = SlabPartition(torch.from_numpy(st.local_points), reach)
+        rng = np.random.default_rng(5)
+        pool = torch.from_numpy(st.points[rng.integers(0, st.points.shape[0], 20000)])
+        new_idx = torch.arange(15000, 20000)
+        out = {"shape": part.shape}
+        plan = slab_batch_plan(part, pool, new_idx, bs=4096, bs_new_sample=1024, new_mode=True)
+        rows, new, scales = plan
+        # this rank's draw: as many history / new rows as its share (any positive counts would do)
+        bh = max(1, int(round(3072 * rows.numel() / 20000)))
+        bn = max(1, int(round(1024 * new.numel() / 5000)))
+        sh, sn = scales(bh, bn)
+        out["full"] = (int(rows.numel()), int(new.numel()), bh * sh, bn * sn,
+                       bool(part.sample_mask(pool[rows]).all()))
+        # pool samples only left of the map's middle: the right-hand cells hold none
+        left = pool[pool[:, 0] < float(st.points[:, 0].mean())]
+        out["empty"] = slab_batch_plan(part, left, None, bs=4096, bs_new_sample=0, new_mode=False)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_slab_batch_plan_world8_and_dense_fallback():
+    """slab_batch_plan (Mapper._slab_partition) on 8 ranks with the 4 x 2 cells of bench.py's 8-GPU
+    mapper leg: the slabs' pool rows partition the pool, the scaled history / new rows of the
+    ranks add up to one reference batch (3,072 + 1,024 rows); and when one cell holds no pool
+    samples EVERY rank returns None (the call falls back to the dense all-reduce together)."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [r[1] for r in sorted(q.get(timeout=240) for _ in range(world))]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(r["shape"] == (4, 2) for r in res)
+    assert sum(r["full"][0] for r in res) == 20000 and sum(r["full"][1] for r in res) == 5000
+    assert all(r["full"][0] > 0 and r["full"][4] for r in res)
+    assert sum(r["full"][2] for r in res) == pytest.approx(3072, rel=1e-12)
+    assert sum(r["full"][3] for r in res) == pytest.approx(1024, rel=1e-12)
+    assert all(r["empty"] is None for r in res)
 
 
 def _world_worker(rank, world, port, q):
