@@ -55,6 +55,9 @@ typedef struct PinPoints {
     int64_t rows;
     int32_t after_pgo;           /* rotate neighbour vectors (model/neural_points.py:606-607) */
     int32_t reserved;
+    const float* positions4;     /* [rows, 4] x, y, z, pad: the same positions as 16-B rows, or NULL.  Set:
+                                    pin_train_forward reads each neighbour's position with one 16-B
+                                    load beside its feature loads (all by id) instead of three 4-B ones */
 } PinPoints;
 
 /* Occupancy-grid box: origin cell (ox,oy,oz) and extent in 4x4x4-cell bricks. */
@@ -354,7 +357,7 @@ int pin_grid_fill(const float* positions, int64_t num_points, float resolution, 
  * totals and a done counter) that must be ZERO before the first call on a workspace and that
  * every call leaves zero again (calls sharing one workspace must be ordered on one stream), then
  * 8 bytes per query. */
-#define PIN_ORDER_STATE_BYTES 16640
+#define PIN_ORDER_STATE_BYTES 65600   /* up to 16384 tiles: 4 B per tile + the counter line */
 static inline int64_t pin_query_order_workspace_bytes(int64_t n) {
     return PIN_ORDER_STATE_BYTES + 8 * n;
 }
@@ -444,8 +447,8 @@ typedef struct PinTrainCfg {
     int32_t flags;               /* PIN_TRAIN_ROWS: `coord` of pin_train_forward holds every row (batch and
                                     stencil, pin_train_rows / pin_train_gather) instead of the batch;
                                     PIN_TRAIN_DX (weighted_first, mlp->packed set, no decoder gradient):
-                                    the forward decodes on the matrix cores and saves s dsdf/dx[0:8] in
-                                    x[:, 0:8] instead of the input, and the backward applies it without
+                                    the forward decodes on the matrix cores and saves s dsdf/dx[0:8] as
+                                    x [rows, 8] instead of the input, and the backward applies it without
                                     re-evaluating the decoder;
                                     PIN_TRAIN_EIK: analytic-gradient eikonal (numerical_grad off,
                                     mapper.py:481-482, get_gradient create_graph=True, tools.py:174-184):
@@ -467,7 +470,8 @@ typedef struct PinTrainCfg {
 typedef struct PinTrainState {
     int32_t* ids;                /* [rows, nn_k] local feature rows, -1 invalid */
     float* weights;              /* [rows, nn_k] IDW weights */
-    float* x;                    /* weighted_first: [rows, 11] decoder input; else [rows, nn_k, 3] vectors */
+    float* x;                    /* weighted_first: [rows, 11] decoder input (PIN_TRAIN_DX: [rows, 8] s dsdf/dx
+                                    over the features); else [rows, nn_k, 3] vectors */
     float* sdf;                  /* [rows] predicted sdf */
     float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL */
     int64_t* ts_update;          /* [L] amax with the main rows' ts (neural_points.py:644), may be NULL */

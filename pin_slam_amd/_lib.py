@@ -40,7 +40,7 @@ class PinHash(ctypes.Structure):
 class PinPoints(ctypes.Structure):
     _fields_ = [("records", c_void_p), ("num_points", i64), ("features", c_void_p), ("positions", c_void_p),
                 ("orientations", c_void_p), ("certainties", c_void_p), ("rows", i64), ("after_pgo", i32),
-                ("reserved", i32)]
+                ("reserved", i32), ("positions4", c_void_p)]
 
 
 class PinGridDims(ctypes.Structure):

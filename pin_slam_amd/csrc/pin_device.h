@@ -877,6 +877,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     }
     wave_lds_sync();
     // B operands of the four query tiles (lane group 3 reads lo-row halves; its A slots are 0)
+    uint32_t mbits[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};   // ReLU masks: [query tile][hidden half]
 #if PIN_MF_NT_OUTER
     // query tile outer: one tile's B operands, masks and GEMM2 accumulator live at a time (the A
     // tiles are re-read from LDS per tile); g of tile nt is written over its own, consumed B rows
@@ -901,6 +902,11 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
                 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bl, d, 0, 0, 0);
                 mk[2 * h] = mask_f16x2(d[0], d[1]);
                 mk[2 * h + 1] = mask_f16x2(d[2], d[3]);
+                if (mask) {   // as in the default order below
+                    const uint32_t b4 = (d[0] > 0.f ? 1u : 0u) | (d[1] > 0.f ? 2u : 0u) | (d[2] > 0.f ? 4u : 0u) |
+                                        (d[3] > 0.f ? 8u : 0u);
+                    mbits[nt][ch] |= b4 << (16 * h + 4 * grp);
+                }
             }
             const f16x8 a2h = ((const f16x8*)(pk + kPkA2))[(2 * ch) * 64 + lane];
             const f16x8 a2l = ((const f16x8*)(pk + kPkA2))[(2 * ch + 1) * 64 + lane];
@@ -924,7 +930,6 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     f32x4 acc[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    uint32_t mbits[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};   // [query tile][hidden half]
 #pragma unroll
     for (int ch = 0; ch < 2; ++ch) {
         uint32_t mk[4][4];
@@ -959,6 +964,14 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
             acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l, b, acc[nt], 0, 0, 0);
         }
     }
+    // ---- g back to the query's lane: lane (col, grp) holds rows 4grp..4grp+3 of query 16nt+col
+    wave_lds_sync();   // every lane has read its B operands
+    if (grp < 3) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
+    }
+    wave_lds_sync();
+#endif
     if (mask) {
         // OR over the four lane groups (grp) holding a query's hidden rows; lane q = col + 16 grp
         // then holds query 16 nt + col's whole mask for every nt -- its own query at nt = grp
@@ -975,14 +988,6 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
         }
         *mask = ((uint64_t)hi << 32) | lo;
     }
-    // ---- g back to the query's lane: lane (col, grp) holds rows 4grp..4grp+3 of query 16nt+col
-    wave_lds_sync();   // every lane has read its B operands
-    if (grp < 3) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
-    }
-    wave_lds_sync();
-#endif
     const f32x4* r = (const f32x4*)(xs + lane * kXsStride);
     const f32x4 g0 = r[0], g1 = r[1], g2 = r[2];
     const f32x4* us = (const f32x4*)(pk + kPkScale);

@@ -81,9 +81,13 @@ __device__ __forceinline__ void reg_block_partials(const float* __restrict__ pts
         for (int a = 0; a < 6; ++a) acc[25 + a] += wd * rd * J[a];
     }
     // block reduction, transposed through LDS: every thread's 31 accumulators land in column tid,
-    // then 8 threads per accumulator sum 32 columns each (fixed order) and a 3-step xor tree joins
-    // them.  (Per-accumulator shuffle trees were 372 ds_bpermute with ~190 waits per wave.)
-    __shared__ double red[PIN_REG_NACC][kRegBlock];
+    // then 8 threads per accumulator sum 32 columns each (fixed order: part p takes columns
+    // p, p + 8, ...) and a 3-step xor tree joins them.  (Per-accumulator shuffle trees were 372
+    // ds_bpermute with ~190 waits per wave.)  Rows are padded to kRegBlock + 8 doubles: a wave's
+    // 64 lanes (8 accumulators x 8 parts) then read dwords 16k + 2p (+16c) mod 64, every bank
+    // pair twice -- the least a 64-lane 8-B read can do (unpadded, with contiguous column runs per
+    // part, all 64 lanes hit one bank).
+    __shared__ double red[PIN_REG_NACC][kRegBlock + 8];
     const int tid = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < PIN_REG_NACC; ++k) red[k][tid] = acc[k];
@@ -92,7 +96,7 @@ __device__ __forceinline__ void reg_block_partials(const float* __restrict__ pts
     double v = 0.0;
     if (k < PIN_REG_NACC) {
 #pragma unroll 8
-        for (int c = 0; c < kRegBlock / 8; ++c) v += red[k][part * (kRegBlock / 8) + c];
+        for (int c = 0; c < kRegBlock / 8; ++c) v += red[k][part + 8 * c];
     }
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);

@@ -49,12 +49,11 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 #ifndef PIN_TRAIN_IDP
 #define PIN_TRAIN_IDP 1   // training forward: top-k payload = feature-row id (GridSource IDP)
 #endif
-#ifndef PIN_CERT_T8
-#define PIN_CERT_T8 1   // certainty side effect: flush transposed, 8 lanes per row (see k_train_forward_grid)
-#endif
 
 // MF (PIN_TRAIN_DX): whole waves call this (the matrix-core decoder); live false = a lane past
-// the last row that runs slot 0 and writes nothing.
+// the last row that runs slot 0 and writes nothing.  The neighbours' ids and weights are returned
+// in cid / cw (-1 / 0 invalid); the block's flush_rows stores them (coalesced) and applies the
+// training side effects.
 template <bool WF, class Src, bool MF = false>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
@@ -102,9 +101,16 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             id = valid ? tk.g[j] : -1;
             const int64_t ii = id > 0 ? id : 0;
             src.features(0, ii, f0, f1);
-            v0 = qx - p.positions[3 * ii];
-            v1 = qy - p.positions[3 * ii + 1];
-            v2 = qz - p.positions[3 * ii + 2];
+            if (p.positions4) {   // one 16-B load beside the feature loads (all three by id)
+                const float4 pp = ((const float4*)p.positions4)[ii];
+                v0 = qx - pp.x;
+                v1 = qy - pp.y;
+                v2 = qz - pp.z;
+            } else {
+                v0 = qx - p.positions[3 * ii];
+                v1 = qy - p.positions[3 * ii + 1];
+                v2 = qz - p.positions[3 * ii + 2];
+            }
         } else {
             const float4 rc = src.record(tk.g[j]);
             const int raw = __float_as_int(rc.w);
@@ -122,21 +128,8 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         if (p.after_pgo && valid) quat_rotate_passive(((const float4*)p.orientations)[id], v0, v1, v2);
         const float w = valid && nn > 0 ? u[j] / S : 0.f;
         const float xj[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
-        if (j < nn_k && live) {
-            st.ids[t * nn_k + j] = id;
-            st.weights[t * nn_k + j] = w;
-        }
         cid[j] = valid && live ? id : -1;
         cw[j] = w;
-#if !PIN_CERT_T8
-        if (valid) {
-            // training side effects (neural_points.py:640, :644); ts: read first, the max is
-            // usually a no-op
-            if (st.certainties) atomicAdd(st.certainties + id, w);
-            if (qts >= 0 && st.ts_update && st.ts_update[id] < qts)
-                atomicMax((unsigned long long*)(st.ts_update + id), (unsigned long long)qts);
-        }
-#endif
         if (WF) {
 #pragma unroll
             for (int d = 0; d < kD; ++d) x[d] = x[d] + (valid ? xj[d] : 0.f) * w;
@@ -154,12 +147,13 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         }
     }
     if (WF) {
-        if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX)
+        if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX: [rows, 8])
             float gx[kF];
             sdf = mlp_sdf_mfma16<true, 0, kF>(m, x, gx);
             if (live) {
-#pragma unroll
-                for (int d = 0; d < kF; ++d) st.x[t * kD + d] = gx[d];
+                float4* xo = (float4*)(st.x + t * kF);
+                xo[0] = make_float4(gx[0], gx[1], gx[2], gx[3]);
+                xo[1] = make_float4(gx[4], gx[5], gx[6], gx[7]);
             }
         } else {
             float gx[kD];
@@ -171,15 +165,19 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     if (live) st.sdf[r] = sdf;
 }
 
-// The training side effects (neural_points.py:640 certainty scatter_add, :644 ts amax) are one
+// End of a training forward block (all threads): the rows' neighbour ids / weights (cid, cw) are
+// staged in LDS, stored to st.ids / st.weights as the block's contiguous [rows, nn_k] run (256-B
+// coalesced stores instead of one 4-B store per lane and neighbour at a 4 nn_k-B stride, which
+// cost ~115 us of the 1.68M-row forward), then the training side effects are applied
+// (neural_points.py:640 certainty scatter_add, :644 ts amax).  The side effects are one
 // memory-side atomic per (row, neighbour); with one lane per row every wave-instruction would hit
-// 64 unrelated 64-B segments (the slow shape, MI355X_MICROARCH.md Global float atomics).  Both are
-// flushed transposed instead -- through LDS, 8 lanes per row, 8 rows per instruction: a row's
-// neighbours (adjacent cells) share segments, and the ts reads (the max is usually a no-op) are
-// issued together instead of one dependent read per neighbour inside the streaming loop.
-__device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int64_t* __restrict__ ts_update,
-                                                   const int (&cid)[kK], const float (&cw)[kK], int64_t qts) {
-#if PIN_CERT_T8
+// 64 unrelated 64-B segments (the slow shape, MI355X_MICROARCH.md Global float atomics), so they
+// are issued transposed, 8 lanes per row, 8 rows per instruction: a row's neighbours (adjacent
+// cells) share segments, and the ts reads (the max is usually a no-op) are issued together
+// instead of one dependent read per neighbour inside the streaming loop.
+__device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainState& st, int64_t t0, int64_t rows,
+                                           const int (&cid)[kK], const float (&cw)[kK], int64_t qts,
+                                           bool store_ids) {
     __shared__ int s_id[kBlock * kK];
     __shared__ float s_w[kBlock * kK];
     __shared__ int64_t s_ts[kBlock];
@@ -191,8 +189,27 @@ __device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int
     }
     s_ts[tid] = qts;
     __syncthreads();
+    if (store_ids && t0 < rows) {
+        const int nn_k = c.nn_k;
+        const int nr = (int)(rows - t0 < kBlock ? rows - t0 : kBlock);
+        int* __restrict__ ido = st.ids + t0 * nn_k;
+        float* __restrict__ wo = st.weights + t0 * nn_k;
+        if (nn_k == kK) {
+            for (int e = tid; e < nr * kK; e += kBlock) {
+                ido[e] = s_id[e];
+                wo[e] = s_w[e];
+            }
+        } else {
+            for (int e = tid; e < nr * nn_k; e += kBlock) {
+                const int r = e / nn_k, j = e - r * nn_k;
+                ido[e] = s_id[r * kK + j];
+                wo[e] = s_w[r * kK + j];
+            }
+        }
+    }
     const int base = (tid & ~63) * kK, lane = tid & 63;
-    if (cert) {
+    if (st.certainties) {
+        float* __restrict__ cert = st.certainties;
 #pragma unroll
         for (int u = 0; u < kK; ++u) {
             const int e = base + u * 64 + lane;
@@ -200,7 +217,8 @@ __device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int
             if (id >= 0) atomicAdd(cert + id, s_w[e]);
         }
     }
-    if (ts_update) {
+    if (st.ts_update) {
+        int64_t* __restrict__ ts_update = st.ts_update;
         int64_t cur[kK];
 #pragma unroll
         for (int u = 0; u < kK; ++u) {
@@ -215,7 +233,6 @@ __device__ __forceinline__ void flush_side_effects(float* __restrict__ cert, int
             if (cur[u] < q) atomicMax((unsigned long long*)(ts_update + s_id[e]), (unsigned long long)q);
         }
     }
-#endif
 }
 
 template <bool WF, bool MF>
@@ -236,7 +253,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
         const HashSource src(h, p);
         train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts, t < rows);
     }
-    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
+    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw, qts, true);
 }
 
 template <bool WF, bool MF>
@@ -258,9 +275,7 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
         train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts,
                                                                      t < rows);
     }
-#ifndef PIN_CERT_SKIP
-    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
-#endif
+    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw, qts, true);
 }
 
 __global__ void __launch_bounds__(kBlock)
@@ -616,7 +631,7 @@ __device__ __forceinline__ void train_forward_eik_kernel_body(const Src& src, co
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains, cid, cw, qts);
-    if (st.certainties || st.ts_update) flush_side_effects(st.certainties, st.ts_update, cid, cw, qts);
+    flush_rows(c, st, xcd_block() * kBlock, c.n_main, cid, cw, qts, false);
 }
 
 template <bool WF>
@@ -871,9 +886,16 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = dsdf * gx[d];
         mlp_grad_mfma<false>(mws, mk, so, x, nullptr, accT, accE);
         so_sum += so;
-    } else if (WF && MF) {
+    } else if (WF && MF) {   // PIN_TRAIN_DX: x rows of 8 (s dsdf/dx over the features)
+        float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0;
+        if (live) {
+            const float4* xr = (const float4*)(st.x + r * kF);
+            g0 = xr[0];
+            g1 = xr[1];
+        }
+        const float gv[kF] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
 #pragma unroll
-        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? dsdf * st.x[r * kD + d] : 0.f;
+        for (int d = 0; d < kF; ++d) gst[threadIdx.x * kF + d] = live ? dsdf * gv[d] : 0.f;
     } else if (WF) {
         float x[kD];
 #pragma unroll

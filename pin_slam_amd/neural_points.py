@@ -787,7 +787,15 @@ class NeuralPoints(nn.Module):
             return hit[1]
         hv = hash_view(self)
         f = src[0].data if isinstance(src[0], nn.Parameter) else src[0]
-        pv = points_view(rec, f, src[1], src[2], src[3], self.after_pgo)
+        # the local map's positions also as 16-B rows: the training forward (mapping, local rows)
+        # reads every neighbour's position by id beside its feature rows
+        # (cached on the positions alone: the view itself is rebuilt whenever the features move)
+        p4 = None
+        if query_locally and src[1] is not None and src[1].shape[0] > 0:
+            pos = src[1]
+            p4 = self._cached("positions4_local", (pos,), (),
+                              lambda: torch.nn.functional.pad(pos.detach().to(torch.float32), (0, 1)).contiguous())
+        pv = points_view(rec, f, src[1], src[2], src[3], self.after_pgo, positions4=p4)
         # the key is taken after hash_view, which may build the cell table
         key = key[:-1] + (id(self._cells),)
         self._view_cache[(mode, bool(query_locally))] = (key, (hv, pv))

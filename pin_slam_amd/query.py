@@ -7,7 +7,6 @@ import os
 
 import numpy as np
 import torch
-from torch.autograd.function import once_differentiable
 
 from . import _lib
 
@@ -40,7 +39,9 @@ def hash_view(nm) -> _View:
     return _View(s, (table, cells))
 
 
-def points_view(records, features, positions, orientations, certainties, after_pgo) -> _View:
+def points_view(records, features, positions, orientations, certainties, after_pgo, positions4=None) -> _View:
+    """positions4: the positions as [rows, 4] f32 (optional; the training forward's neighbour
+    position loads)."""
     features = _f32(features)
     positions = _f32(positions)
     orientations = _f32(orientations) if after_pgo else None
@@ -51,8 +52,9 @@ def points_view(records, features, positions, orientations, certainties, after_p
                        positions=positions.data_ptr() if positions is not None else None,
                        orientations=orientations.data_ptr() if orientations is not None else None,
                        certainties=certainties.data_ptr() if certainties is not None else None,
-                       rows=features.shape[0], after_pgo=int(bool(after_pgo)), reserved=0)
-    v = _View(s, (records, features, positions, orientations, certainties))
+                       rows=features.shape[0], after_pgo=int(bool(after_pgo)), reserved=0,
+                       positions4=positions4.data_ptr() if positions4 is not None else None)
+    v = _View(s, (records, features, positions, orientations, certainties, positions4))
     v.features = features
     return v
 
@@ -108,9 +110,56 @@ def _mlp_view(decoder) -> _View:
     return _View(s, (W1, b1, W2, b2))
 
 
+def _quat_rotate_passive(quat, v):
+    """utils/tools.py:316-323 apply_quaternion_rotation (passive): v + w t + u x t, t = 2 u x v,
+    u = -quat[1:]."""
+    w = quat[..., 0:1]
+    u = -quat[..., 1:]
+    t = 2 * torch.linalg.cross(u, v)
+    return v + w * t + torch.linalg.cross(u, t)
+
+
+def _query_feature_restated(q, feats, ids, gids, records, positions, orientations, after_pgo, wf):
+    """model/neural_points.py:577-662 over the neighbour sets the kernel found (ids: feature rows,
+    gids: the candidates' records, -1 invalid), as differentiable torch ops in q and feats: the
+    distance and IDW weights from the record (global) position, the decoder input's neighbour
+    vector from the local position (flagged records, the global2local quirk) rotated after PGO.
+    Used only to differentiate the backward itself (create_graph=True)."""
+    qf = q.to(torch.float32)
+    valid = gids >= 0
+    g = gids.clamp(min=0).long()
+    il = ids.clamp(min=0).long()
+    rec = records.index_select(0, g.reshape(-1)).reshape(g.shape + (4,))
+    bits = records.view(torch.int32)[:, 3].index_select(0, g.reshape(-1)).reshape(g.shape)
+    pg = qf[:, None, :] - rec[..., :3]
+    d2 = (pg[..., 0] * pg[..., 0] + pg[..., 1] * pg[..., 1]) + pg[..., 2] * pg[..., 2]
+    u = torch.where(valid, 1.0 / (d2 + 1e-15), torch.zeros_like(d2))
+    S = u.sum(1, keepdim=True)
+    w = torch.where(valid, u / torch.where(S > 0, S, torch.ones_like(S)), torch.zeros_like(u))
+    unf = valid & ((bits & _lib.RECORD_UNFAITHFUL) != 0)
+    ploc = rec[..., :3]
+    if bool(unf.any()):
+        ploc = torch.where(unf[..., None], positions.index_select(0, il.reshape(-1)).reshape(il.shape + (3,)), ploc)
+    v = qf[:, None, :] - ploc
+    if after_pgo:
+        v = _quat_rotate_passive(orientations.index_select(0, il.reshape(-1)).reshape(il.shape + (4,)), v)
+    zero = torch.zeros((), dtype=torch.float32, device=q.device)
+    v = torch.where(valid[..., None], v, zero)
+    f = torch.where(valid[..., None], feats.index_select(0, il.reshape(-1)).reshape(il.shape + (feats.shape[1],)), zero)
+    x = torch.cat((f, v), -1)
+    out = (x * w[..., None]).sum(1) if wf else x
+    return out, w
+
+
 class QueryFeatureFn(torch.autograd.Function):
     """neural_points.py:528-674 forward on the GPU; backward = dL/dq and a float-atomic
-    scatter of dL/dfeatures (the reference's autograd through index_put / gather)."""
+    scatter of dL/dfeatures (the reference's autograd through index_put / gather).
+
+    Second order (a caller differentiating the gradient, e.g. get_gradient with create_graph=True,
+    utils/tools.py:174-184): the backward is then itself differentiable -- it is taken by autograd
+    over _query_feature_restated on the kernel's own neighbour sets, so the double backward has the
+    reference's autograd semantics (the fused mapping() evaluates that case in closed form instead,
+    PIN_TRAIN_EIK); the first-order backward stays the native kernel."""
 
     @staticmethod
     def forward(ctx, q, feats, hv, pv, nn_k, weighted_first, gv=None):
@@ -132,7 +181,8 @@ class QueryFeatureFn(torch.autograd.Function):
             _lib.call("pin_query_feature_fwd", hv.ref(), pv.ref(), _lib.ptr(qd), n, nn_k, int(weighted_first),
                       _lib.ptr(feat), _lib.ptr(weights), _lib.ptr(nn_counts), _lib.ptr(cert), _lib.ptr(ids),
                       _lib.ptr(gids), _lib.stream())
-        ctx.save_for_backward(qd, ids, gids, weights)
+        # q and feats themselves are kept for the differentiable (second-order) backward
+        ctx.save_for_backward(q, feats, qd, ids, gids, weights)
         ctx.pv = pv
         ctx.nn_k = nn_k
         ctx.wf = weighted_first
@@ -141,12 +191,31 @@ class QueryFeatureFn(torch.autograd.Function):
         return feat, weights, nn_counts, cert, ids
 
     @staticmethod
-    @once_differentiable
     def backward(ctx, g_feat, g_w, _g_nn, _g_cert, _g_ids):
-        qd, ids, gids, weights = ctx.saved_tensors
+        q, feats, qd, ids, gids, weights = ctx.saved_tensors
         need_q, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_q or need_f):
             return None, None, None, None, None, None, None
+        if torch.is_grad_enabled():   # create_graph=True: the backward must itself be differentiable
+            pv = ctx.pv
+            records, _, positions, orientations = pv.keep[0], pv.keep[1], pv.keep[2], pv.keep[3]
+            with torch.enable_grad():
+                out, w = _query_feature_restated(q, feats, ids, gids, records, positions, orientations,
+                                                 bool(pv.struct.after_pgo), ctx.wf)
+                outs, gos = [], []
+                for o, go in ((out, g_feat), (w, g_w)):
+                    if go is not None:
+                        outs.append(o)
+                        gos.append(go)
+                inputs = [t for t, need in ((q, need_q), (feats, need_f)) if need]
+                grads = list(torch.autograd.grad(outs, inputs, gos, create_graph=True, allow_unused=True))
+            gq = grads.pop(0) if need_q else None
+            gf = grads.pop(0) if need_f else None
+            if need_q and gq is None:
+                gq = torch.zeros_like(q)
+            if need_f and gf is None:
+                gf = torch.zeros_like(feats)
+            return gq, gf, None, None, None, None, None
         n = qd.shape[0]
         grad_q = torch.empty_like(qd) if need_q else None
         grad_f = torch.zeros_like(ctx.pv.features) if need_f else None
@@ -160,7 +229,7 @@ class QueryFeatureFn(torch.autograd.Function):
         return grad_q, grad_f, None, None, None, None, None
 
 
-ORDER_STATE_BYTES = 16640   # PIN_ORDER_STATE_BYTES
+ORDER_STATE_BYTES = 65600   # PIN_ORDER_STATE_BYTES
 _order_ws = {}
 
 

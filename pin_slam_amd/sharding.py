@@ -66,7 +66,8 @@ class SlabPartition:
     cells along y (a x b = W, a k-d split); rank r owns cell (r // b, r % b).  layout "auto"
     picks the factor pair with the shortest total cut length ((a-1) span_y + (b-1) span_x,
     proportional to the halo volume), so 8 ranks on a square map become 4 x 2 cells instead of 8
-    thin strips, and a corridor stays 1-D; "1d" cuts only along the longer horizontal axis.
+    thin strips, and a corridor stays 1-D; "1d" cuts only along the longer horizontal axis; an
+    (a, b) pair forces that grid.
 
     shared_rows: local rows whose gradient may come from any slab.  The reference's global2local
     table maps every non-local point to local row 1 (neural_points.py:290-300, the fill quirk):
@@ -85,12 +86,17 @@ class SlabPartition:
         dev = pos.device
         if L == 0:
             raise ValueError("SlabPartition: empty local map")
-        if layout not in ("auto", "1d"):
-            raise ValueError("layout must be 'auto' or '1d'")
+        if isinstance(layout, (tuple, list)):
+            if len(layout) != 2 or int(layout[0]) * int(layout[1]) != W or min(int(v) for v in layout) < 1:
+                raise ValueError(f"layout {tuple(layout)}: a x b cells must equal the world size {W}")
+        elif layout not in ("auto", "1d"):
+            raise ValueError("layout must be 'auto', '1d' or an (a, b) pair with a * b = world size")
         lo = pos.min(0).values.double().cpu()
         hi = pos.max(0).values.double().cpu()
         span = [max(float(hi[d] - lo[d]), 1e-9) for d in (0, 1)]
-        if layout == "1d":
+        if isinstance(layout, (tuple, list)):
+            self.shape = (int(layout[0]), int(layout[1]))
+        elif layout == "1d":
             self.shape = (W, 1) if span[0] >= span[1] else (1, W)
         else:
             # shortest total cut length; ties to more columns (the 1-D case along x first)

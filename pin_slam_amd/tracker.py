@@ -141,11 +141,14 @@ _REG_BUF: dict = {}
 
 
 def _reg_buffers(dev):
-    """Per-device buffers reused every step: the reduction workspace, the accumulators + status
-    record (one D2H copy), delta_T and two pose slots (the loop ping-pongs between them), and the
-    pinned host mirror of accumulators + status.  The host read in _register synchronises the
-    stream, so reuse is safe."""
-    key = str(dev)
+    """Buffers reused every step, one set per (device, stream): the reduction workspace (with
+    pin_reg_step's last-block ticket), the accumulators + status record (one D2H copy), delta_T
+    and two pose slots (the loop ping-pongs between them), and the pinned host mirrors.  Within a
+    stream, launches are ordered and the host read in _register / _RegLoop.result synchronises, so
+    reuse is safe; registrations on another stream (e.g. a loop-closure registration on a side
+    stream) get their own set, so they never share the ticket counter or the partials."""
+    s = _lib.stream(dev) if torch.device(dev).type == "cuda" else None
+    key = (str(dev), s.value if s is not None else None)
     if key not in _REG_BUF:
         W = _lib.REG_WORKSPACE_DOUBLES
         n = W + _lib.REG_NACC + _lib.REG_NSTATUS + 16 * 3

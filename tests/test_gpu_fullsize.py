@@ -98,7 +98,8 @@ def test_mapper_batch_scatter_and_sdf(dev):
     order = b.rows4[:rows, 3].contiguous().view(torch.int32).long() if mapper._order is not None else \
         torch.arange(rows, device=dev)
     dsdf = _row_dsdf(b.sdf[:rows], label, n, nd, cfg, float(np.float32(mapper.sdf_scale)))
-    contrib = dsdf[order][:, None, None] * b.weights[:rows, :, None] * b.x[:rows, None, :_lib.FEATURE_DIM]
+    dx = b.x.view(-1)[:rows * _lib.FEATURE_DIM].view(rows, 1, _lib.FEATURE_DIM)   # PIN_TRAIN_DX: [rows, 8]
+    contrib = dsdf[order][:, None, None] * b.weights[:rows, :, None] * dx
     ids = b.ids[:rows].long()
     ok = ids >= 0
     want = torch.zeros_like(fg, dtype=torch.float64)

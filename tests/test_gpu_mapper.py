@@ -521,3 +521,66 @@ def test_analytic_eikonal_mapping_call(golden, dev, backend, case):
     tol = 1e-3 * _norm(want - before) + 3 * float(z["spread_norm_global_features_after"])
     print(f"   after {int(z['iters'])} iterations: |ours - ref| {_norm(got - want):.3e}, moved {_norm(want - before):.3e}")
     assert _norm(got - want) <= tol, (_norm(got - want), tol)
+
+
+@pytest.mark.parametrize("case", ["mapping_eik_wf", "mapping_eik_livox"])
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_query_feature_double_backward_matches_reference(golden, dev, backend, case):
+    """The reference's own first mapping iteration with numerical_grad off, written with its
+    autograd calls on the DROP-IN query_feature (utils/mapper.py:448-573): get_gradient(coord, sdf)
+    with create_graph=True (utils/tools.py:174-184), BCE + weight_e * mean((|g| - 1)^2), backward --
+    a double backward through QueryFeatureFn.  The feature and decoder gradients must match the
+    reference's first-step gradients (it0_*) with the analytic-eikonal test's tolerances (1e-4 of
+    their norm + 3 x the reference's own 1- vs 8-thread spread)."""
+    import torch.nn as nn
+    z = golden(case)
+    nm, dec, mapper, _ = _mapping_call_setup(z, dev, backend)
+    cfg = nm.config
+    assert not bool(cfg.numerical_grad)
+    index = mapper._batch_index()                       # the first iteration's draws
+    coord = mapper.global_coord_pool[index].clone().requires_grad_(True)
+    label = mapper.sdf_label_pool[index]
+    ts = mapper.time_pool[index]
+    weight = torch.abs(mapper.weight_pool[index]).detach()
+    feats = nm.local_geo_features
+    feats.grad = None
+    for p in dec.parameters():
+        p.grad = None
+    geo, _, wk, _, _ = nm.query_feature(coord, ts)
+    sdf = dec.sdf(geo)
+    if not cfg.weighted_first:
+        sdf = torch.sum(sdf * wk, dim=1).squeeze(1)
+    g = torch.autograd.grad(sdf, coord, torch.ones_like(sdf), create_graph=True, retain_graph=True,
+                            only_inputs=True)[0]
+    sigma = mapper.sdf_scale
+    bce = (nn.BCEWithLogitsLoss(weight=weight) if cfg.loss_weight_on else nn.BCEWithLogitsLoss())(
+        sdf / sigma, torch.sigmoid(label / sigma))
+    loss = bce + cfg.weight_e * ((g.norm(2, dim=-1) - 1.0) ** 2).mean()
+    loss.backward()
+    got, want = _np(feats.grad), z["it0_feat_grad"]
+    tol = 1e-4 * _norm(want) + 3 * float(z["spread_norm_it0_feat_grad"])
+    print(f"{case}: drop-in double backward, feature gradient |ours - ref| {_norm(got - want):.3e} (tol {tol:.3e})")
+    assert _norm(got - want) <= tol, (_norm(got - want), tol)
+    for key, p in zip(MLP_KEYS, dec.parameters()):
+        ref = z[f"it0_grad_{key}"]
+        tol = 1e-4 * _norm(ref) + 3 * float(z[f"spread_norm_it0_grad_{key}"])
+        assert _norm(_np(p.grad) - ref) <= tol, (key, _norm(_np(p.grad) - ref), tol)
+
+
+def test_query_feature_backward_first_order_unchanged(golden, dev):
+    """Without create_graph the backward stays the native kernel; with it, the differentiable
+    restatement gives the same first-order gradients (it is only needed for the second order)."""
+    z = golden("mapping_eik_wf")
+    nm, dec, mapper, _ = _mapping_call_setup(z, dev, "grid")
+    index = mapper._batch_index()
+    outs = []
+    for create in (False, True):
+        coord = mapper.global_coord_pool[index].clone().requires_grad_(True)
+        nm.local_geo_features.grad = None
+        geo, _, wk, _, _ = nm.query_feature(coord, None, training_mode=False)
+        sdf = dec.sdf(geo)
+        gq, = torch.autograd.grad(sdf.sum(), coord, create_graph=create, retain_graph=True)
+        gf, = torch.autograd.grad(sdf.sum(), nm.local_geo_features, create_graph=create)
+        outs.append((gq.detach(), gf.detach()))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-7)

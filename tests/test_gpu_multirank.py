@@ -44,7 +44,7 @@ def _state(nm, dec):
                 dec=[p.detach().cpu().numpy().copy() for p in dec.parameters()])
 
 
-def _worker(rank, world, port, case, shard, q):
+def _worker(rank, world, port, case, shard, q, layout="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -55,6 +55,7 @@ def _worker(rank, world, port, case, shard, q):
         nm, dec, mapper, _ = _mapping_call_setup(z, "cuda", "grid")
         mapper.group = dist.group.WORLD
         mapper.shard = shard
+        mapper.slab_layout = layout
         draws = ReplayDraws(7000 + 31 * rank)
         mapper._randint = lambda high, k: torch.from_numpy(draws.randint(high, k)).to("cuda")
         calls = []
@@ -87,7 +88,7 @@ def _worker(rank, world, port, case, shard, q):
         dist.destroy_process_group()
 
 
-def _single_process(case, calls, dev):
+def _single_process(case, calls, dev, world=WORLD):
     """The union of the ranks' batches in one process: per iteration every rank's train_step into
     one accumulator (reduce=False, the rank's scales), then one Adam step over all rows."""
     from tests.test_gpu_mapper import _mapping_call_setup
@@ -104,7 +105,7 @@ def _single_process(case, calls, dev):
         m_m, m_v = torch.zeros_like(m_grad), torch.zeros_like(m_grad)
     mapper._adam_t = 0
     for it in range(ITERS):
-        for r in range(WORLD):
+        for r in range(world):
             c = calls[r][it]
             scale = c["scale"] if c["scale"] is not None else 1.0 / c["world"]
             mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, f_grad, m_grad, 1,
@@ -115,21 +116,21 @@ def _single_process(case, calls, dev):
     return _state(nm, dec), feats0, mapper
 
 
-def _run(case, shard):
+def _run(case, shard, world=WORLD, layout="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, case, shard, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, shard, q, layout)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        res = dict(q.get(timeout=240) for _ in range(WORLD))
+        res = dict(q.get(timeout=240) for _ in range(world))
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for r in range(WORLD):
+    for r in range(world):
         assert isinstance(res[r], dict), f"rank {r}: {res[r]}"
     assert all(p.exitcode == 0 for p in procs)
     return res
@@ -139,33 +140,42 @@ def _norm(a):
     return float(np.linalg.norm(np.asarray(a, dtype=np.float64).ravel()))
 
 
-@pytest.mark.parametrize("case,shard", [("mapping_wf", "dense"), ("mapping_wf", "space"),
-                                        ("mapping_wf_frozen", "space"), ("mapping_nwf_weighted", "space")])
-def test_multirank_mapping_equals_union_of_batches(case, shard):
+@pytest.mark.parametrize("case,shard,world,layout", [("mapping_wf", "dense", 2, "auto"), ("mapping_wf", "space", 2, "auto"),
+                                                     ("mapping_wf_frozen", "space", 2, "auto"),
+                                                     ("mapping_nwf_weighted", "space", 2, "auto"),
+                                                     ("mapping_wf", "space", 4, (2, 2)),
+                                                     ("mapping_wf_frozen", "space", 4, (2, 2))])
+def test_multirank_mapping_equals_union_of_batches(case, shard, world, layout):
+    """world 4 runs the 2-D cell path (2 x 2 cells, the bench's 8-GPU layout is 4 x 2): halo rows
+    exchanged with up to three neighbours, the shared quirk row summed over four ranks."""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
-    res = _run(case, shard)
-    r0, r1 = res[0], res[1]
-    calls = [r0["calls"], r1["calls"]]
+    res = _run(case, shard, world, layout)
+    r0 = res[0]
+    calls = [res[r]["calls"] for r in range(world)]
     assert all(len(c) == ITERS for c in calls)
     if shard == "space":
-        assert r0["part"] is not None and not any("dense" in w for w in r0["warnings"]), r0["warnings"]
-        assert r0["part"]["shared"] == [1]
-        assert r0["part"]["owned"] + r1["part"]["owned"] == r0["feats"].shape[0] - 1
+        for r in range(world):
+            assert res[r]["part"] is not None and not any("dense" in w for w in res[r]["warnings"]), res[r]["warnings"]
+            assert res[r]["part"]["shared"] == [1]
+            if world == 4:
+                assert tuple(res[r]["part"]["shape"]) == (2, 2)
+        assert sum(res[r]["part"]["owned"] for r in range(world)) == r0["feats"].shape[0] - 1
     else:
         assert r0["part"] is None
     # replicas agree bit for bit
-    for key in ("feats", "cert", "ts"):
-        np.testing.assert_array_equal(r0[key], r1[key], err_msg=key)
-    for a, b in zip(r0["dec"], r1["dec"]):
-        np.testing.assert_array_equal(a, b)
-    ref, feats0, mapper = _single_process(case, calls, "cuda")
+    for r in range(1, world):
+        for key in ("feats", "cert", "ts"):
+            np.testing.assert_array_equal(r0[key], res[r][key], err_msg=key)
+        for a, b in zip(r0["dec"], res[r]["dec"]):
+            np.testing.assert_array_equal(a, b)
+    ref, feats0, mapper = _single_process(case, calls, "cuda", world)
     if shard == "space":
         # the slab scales keep the union an unbiased estimate of one batch: sum_r scale_h,r bs_hist,r / bs_hist = 1
         c = mapper.config
         n_new = int(mapper.new_idx.numel())
         bs_hist = int(c.bs) - min(n_new, int(c.bs_new_sample))
-        tot = sum(calls[r][0]["scale"] * (calls[r][0]["index"].size - calls[r][0]["n_tail"]) for r in range(WORLD))
+        tot = sum(calls[r][0]["scale"] * (calls[r][0]["index"].size - calls[r][0]["n_tail"]) for r in range(world))
         assert tot / bs_hist == pytest.approx(1.0, rel=1e-9)
     moved = _norm(ref["feats"] - feats0)
     d = r0["feats"] - ref["feats"]
