@@ -818,8 +818,12 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     static_assert(!EIK || !(WF && MF), "analytic eikonal, weighted_first: gx from the forward");
     constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
     constexpr bool kRowDecode = MF && WF && MLP_GRAD; // weighted_first, training decoder: one decode per row
-    constexpr int kJ = WF ? 1 : kK;                   // staged gradient rows per query row
-    __shared__ float gst[kBlock * kJ * kF];
+    // weighted_first: one staged gradient row per query row, scattered by the block at the end;
+    // per-neighbour: each neighbour's rows are staged and scattered by their own wave inside the
+    // neighbour loop (s_nwf: 64 rows x 8 floats + 64 ids per wave, no block barrier), so the block
+    // does not hold all k x 8 floats per row (64 KB at k = 8: one wave per SIMD)
+    __shared__ float gst[WF ? kBlock * kF : 1];
+    __shared__ float s_nwf[WF ? 1 : kWaves][WF ? 1 : 64 * kF + 64];
     __shared__ float s_mg[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMgWave : 1];
     __shared__ float s_so[kWaves];
     __shared__ float s_mlp[MF ? 1 : kWSize];
@@ -971,8 +975,24 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             } else if (__any(ok)) {
                 decoder_backward(mlpw, x, coef * mlpw.sdf_scale, gf);
             }
+            if constexpr (!WF) {
+                // this neighbour's 64 gradient rows, scattered by the wave: 8 lanes x 32 contiguous
+                // bytes per (row, neighbour), 8 rows per instruction (the shape of the block scatter)
+                float* wg = s_nwf[wave];
+                int* wid = (int*)(wg + 64 * kF);
+                const int lane = threadIdx.x & 63;
+                wave_lds_sync();   // the previous neighbour's scatter has read the slots
 #pragma unroll
-            for (int d = 0; d < kF; ++d) gst[(threadIdx.x * kK + j) * kF + d] = gf[d];
+                for (int d = 0; d < kF; ++d) wg[lane * kF + d] = gf[d];
+                wid[lane] = ok && grad_features ? id : -1;
+                wave_lds_sync();
+#pragma unroll
+                for (int u = 0; u < kF; ++u) {
+                    const int e = u * 64 + lane;
+                    const int rid = wid[e >> 3];
+                    if (rid >= 0) atomicAdd(grad_features + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
+                }
+            }
         }
     }
     {
@@ -985,13 +1005,13 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     }
     if constexpr (MLP_GRAD) mlp_grad_flush<EIK>(s_mg, s_so, accT, accE, so_sum, mlp_part + (int64_t)blockIdx.x * kMlpPart);
     __syncthreads();
-    if (!grad_features) return;
+    if (!WF || !grad_features) return;   // per-neighbour: scattered in the neighbour loop
     // scatter: element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour)
     // pairs x 32 contiguous bytes, one memory-side request each -- the cheapest atomic shape
     // measured (LDS pre-aggregation per block, and 64-B rows carrying the certainty, were slower).
     // The block's ids (and WF weights) are staged in LDS first with coalesced loads, so the
     // scatter loop issues its atomics back to back instead of waiting on a load per element.
-    __shared__ int s_ids[kBlock * kK];
+    __shared__ int s_ids[WF ? kBlock * kK : 1];
     __shared__ float s_wt[WF ? kBlock * kK : 1];
     __shared__ float s_al[WF && EIK ? kBlock * kK : 1];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
@@ -1009,10 +1029,10 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         const int rj = e >> 3;
         const int id = s_ids[rj];
         if (id < 0) continue;
-        const int lr = rj / nn_k, j = rj - lr * nn_k;
+        const int lr = rj / nn_k;
         float g;
         if (WF && EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
-        else g = WF ? s_wt[rj] * gst[lr * kF + d] : gst[(lr * kK + j) * kF + d];
+        else g = s_wt[rj] * gst[lr * kF + d];
         atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }

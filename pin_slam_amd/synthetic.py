@@ -289,3 +289,58 @@ class FrameLoop:
         mark("mapping")
         self.processed_frame += 1
         return valid
+
+
+# KITTI-style settings (config/lidar_slam/run_kitti.yaml) for the configs[2] registration workload
+KITTI_CFG = dict(voxel_size_m=0.4, query_nn_k=6, search_alpha=0.5, weighted_first=False, surface_sample_range_m=0.25,
+                 surface_sample_n=4, free_front_n=2, sigma_sigmoid_m=0.08, loss_weight_on=True, dist_weight_scale=0.8,
+                 bs_new_sample=2000, pool_capacity=int(2e7), freeze_after_frame=30, reg_iter_n=100, reg_GM_grad=0.1,
+                 reg_GM_dist_m=0.2, max_range=80.0, min_range=3.0, vox_down_m=0.08, min_z=-3.5,
+                 source_vox_down_m=0.8, track_on=True)
+
+
+def street_map(frames=12, device="cuda", seed=21, cfg_overrides=None):
+    """A neural-point map of the synthetic street built by PIN-SLAM's mapping steps with the
+    ground-truth poses (pin_slam.py:161-257 with tracking replaced by the known pose, i.e. the
+    reference's mapping-only mode): per frame voxel down-sample + crop, process_frame (sampling,
+    map update, pool), mapping(iters; 40 x on frame 0) with the decoder training.  KITTI settings
+    (KITTI_CFG) unless overridden.  Returns (nm, dec, cfg, scene, poses, rng); the map is centred
+    on the last pose's local map."""
+    from .mapper import Mapper
+    from .neural_points import voxel_down_sample
+    kw = dict(KITTI_CFG)
+    kw.update(cfg_overrides or {})
+    cfg = Config(device=device, **kw)
+    rng = np.random.default_rng(seed)
+    scene = street_scene(rng)
+    poses = slam_poses(frames + 1)
+    nm = NeuralPoints(cfg)
+    torch.manual_seed(42)
+    dec = Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(device)
+    mapper = Mapper(cfg, None, nm, dec)
+    travel = [0.0]
+    for k in range(frames):
+        if k > 0:
+            travel.append(travel[-1] + float(np.linalg.norm(poses[k][:3, 3] - poses[k - 1][:3, 3])))
+        pts = torch.from_numpy(lidar_scan(poses[k], scene, rng).astype(np.float32) / np.float32(Q_SCALE)).to(device)
+        cloud = pts[voxel_down_sample(pts, cfg.vox_down_m)]
+        dist = torch.norm(cloud, dim=1)
+        cloud = cloud[(dist > cfg.min_range) & (dist < cfg.max_range) & (cloud[:, 2] > cfg.min_z) &
+                      (cloud[:, 2] < cfg.max_z)]
+        pose = torch.tensor(poses[k], dtype=torch.float32, device=device)
+        nm.travel_dist = torch.tensor(np.array(travel), dtype=torch.float32, device=device)
+        mapper.process_frame(cloud, None, pose, k, False)
+        if k == cfg.freeze_after_frame:
+            for p in dec.parameters():
+                p.requires_grad_(False)
+        mapper.mapping(cfg.iters * cfg.init_iter_ratio if k == 0 else cfg.iters)
+    return nm, dec, cfg, scene, poses, rng
+
+
+def perturb_pose(T, dx=0.2, yaw_deg=0.5):
+    """T (4x4 f64) moved by dx metres along its x axis and rotated by yaw_deg about z."""
+    a = np.deg2rad(yaw_deg)
+    D = np.eye(4)
+    D[:3, :3] = [[np.cos(a), -np.sin(a), 0.0], [np.sin(a), np.cos(a), 0.0], [0.0, 0.0, 1.0]]
+    D[0, 3] = dx
+    return T @ D

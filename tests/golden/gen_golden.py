@@ -816,16 +816,17 @@ class _ReplayTorch:
         return torch.from_numpy(self.replay.randn(n)).reshape(size)
 
 
-def slam_config():
+def slam_config(freeze_after_frame=15):
     """config/lidar_slam/run_demo.yaml (the reference's sanity-test config, README.md:148-160) on
     the CPU: deskew off (the synthetic scans carry no point times and roma is absent) and the
-    decoder frozen after frame 6 so both mapper paths (trainable / frozen decoder) run."""
+    decoder frozen after frame 15 so both mapper paths (trainable / frozen decoder) run, each
+    across window filters of the pool (pool_filter_freq 10: frames 9, 19, 29)."""
     c = Config()
     c.load(os.path.join(REF, "config/lidar_slam/run_demo.yaml"))
     c.device = "cpu"
     c.silence = True
     c.deskew = False
-    c.freeze_after_frame = 6
+    c.freeze_after_frame = freeze_after_frame
     return c
 
 
@@ -840,7 +841,7 @@ def config_scalars(c):
     return out
 
 
-def gen_slam_sequence(name="slam_seq", frames=12, seed=21, replay_seed=2024):
+def gen_slam_sequence(name="slam_seq", frames=30, seed=21, replay_seed=2024):
     """The sequence with 8 torch threads, saved; then again with 1 thread, whose differences (only
     the reduction order changes) are kept as the reference's own spread (keys spread_*)."""
     import math
@@ -979,8 +980,11 @@ def _slam_sequence_run(name, frames, seed, replay_seed, threads):
                        merged_raises=np.bool_(False))
     finally:
         rds.torch, rmapper.torch = saved
-    for k in range(frames):
-        rec[f"f{k}_scan"] = scans[k]
+    # the scans are not stored: the test regenerates them (pin_slam_amd.synthetic, same seed and
+    # call order) and checks them against these digests
+    import hashlib
+    rec["scan_sha256"] = np.asarray([hashlib.sha256(np.ascontiguousarray(s_).tobytes()).hexdigest() for s_ in scans])
+    rec["scan_seed"] = np.int64(seed)
     rec["truth_poses"] = np.stack(poses)
     rec.update(surface_probes=surf, f0_surface_probes=surf0)
     rec["config_json"] = np.asarray(json.dumps(config_scalars(cfg)))

@@ -124,3 +124,114 @@ def _row_dsdf(sdf, label, n, nd, cfg, sigma):
     sten = torch.stack([dg[0], -dg[0], dg[1], -dg[1], dg[2], -dg[2]])
     out[n:] = sten.reshape(-1)
     return out
+
+
+# ------------------------------------------------------------------ configs[2]: 200K-point registration
+@pytest.fixture(scope="module")
+def street(dev):
+    from pin_slam_amd.synthetic import Q_SCALE, lidar_scan, perturb_pose, street_map
+    from pin_slam_amd.tracker import transform_points
+    nm, dec, cfg, scene, poses, rng = street_map(12, device=dev)
+    T_true = poses[12]
+    scan = torch.from_numpy(lidar_scan(T_true, scene, rng, cols=3200).astype(np.float32) / np.float32(Q_SCALE)).to(dev)
+    guess = torch.tensor(perturb_pose(T_true), dtype=torch.float64, device=dev)
+    return nm, dec, cfg, T_true, scan, guess, transform_points(scan, guess)
+
+
+def test_registration_200k_tile_order_and_point_split(dev, street):
+    """configs[2] (bench.py tracker leg): one registration step of a ~200K-point KITTI-style scan.
+    The tile-sorted query (outputs and normal equations in tile order) gives the same accumulators
+    as the unsorted input-order query (f64 sums in another order: rel 1e-9), the same valid points;
+    and the accumulators of the two halves of the cloud, summed as the point-sharded Tracker's
+    all-reduce does, equal the whole cloud's (the sharded step's increment therefore equals the
+    single-process one)."""
+    import pin_slam_amd as P
+    from pin_slam_amd import query as Q
+    nm, dec, cfg, _, scan, _, src = street
+    n = src.shape[0]
+    assert n > 190_000
+    tr = P.Tracker(cfg, nm, dec)
+    args = (None, None, cfg.reg_min_grad_norm, cfg.reg_max_grad_norm, cfg.reg_GM_dist_m, cfg.reg_GM_grad,
+            cfg.reg_lm_lambda, False)
+
+    def reg(pts):
+        valid = torch.empty(pts.shape[0], dtype=torch.uint8, device=dev)
+        r = tr._register(pts.contiguous(), *args, valid_out=valid)
+        return r["acc"], r["status"], valid.clone()
+    acc_t, st_t, v_t = reg(src)
+    assert st_t[0] > n // 4, "the registration needs valid points"
+    old = Q._TILE_QUERIES
+    try:
+        Q._TILE_QUERIES = False
+        acc_i, st_i, v_i = reg(src)
+    finally:
+        Q._TILE_QUERIES = old
+    assert torch.equal(v_t, v_i) and st_t[0] == st_i[0]
+    np.testing.assert_allclose(acc_t, acc_i, rtol=1e-9, atol=1e-9 * np.abs(acc_t).max())
+    h = n // 2
+    acc_a, _, _ = reg(src[:h])
+    acc_b, _, _ = reg(src[h:])
+    np.testing.assert_allclose(acc_a + acc_b, acc_t, rtol=1e-9, atol=1e-9 * np.abs(acc_t).max())
+
+
+def test_tracking_200k_converges_to_true_pose(dev, street):
+    """The configs[2] tracking loop from the 0.2 m / 0.5 deg perturbed pose is valid and lands
+    within 5 cm / 0.1 deg of the scan's true pose."""
+    import pin_slam_amd as P
+    nm, dec, cfg, T_true, scan, guess, _ = street
+    tr = P.Tracker(cfg, nm, dec)
+    T, _, _, ok = tr.tracking(scan, guess)
+    Te = T.cpu().numpy()
+    assert ok, tr.last_status
+    dR = Te[:3, :3].T @ T_true[:3, :3]
+    rot = float(np.degrees(np.arccos(np.clip((np.trace(dR) - 1) / 2, -1.0, 1.0))))
+    assert float(np.linalg.norm(Te[:3, 3] - T_true[:3, 3])) <= 0.05 and rot <= 0.1, (Te, T_true)
+
+
+# ------------------------------------------------------------------ configs[4]: 512^3 mesher grid
+def test_mesher_512_slabs_equal_one_pass_and_subset_vs_oracle(dev):
+    """configs[4] (bench.py mesher leg): the 512^3 grid at 0.1 m over the 1M-point map, SDF-only
+    with zero_empty (Mesher.query_points, utils/mesher.py:41-136).  The z-slab split the bench
+    gives each rank (here 4 slabs) reproduces one pass bitwise; a strided subset matches the
+    oracle (counts exact, SDF 1e-5, empty cells 0)."""
+    from pin_slam_amd.query import query_sdf
+    nm, dec, pts = H.surface_map(N_SIDE, device=dev, buffer_size=int(5e7))
+    R, res, batch = 512, 0.1, 1 << 20
+    lo = pts.mean(0) - 0.5 * R * res
+
+    def grid(z0, z1):
+        i = torch.arange(R, device=dev, dtype=torch.float32)
+        zs = torch.arange(z0, z1, device=dev, dtype=torch.float32)
+        gx, gy, gz = torch.meshgrid(i, i, zs, indexing="ij")
+        return torch.stack([gx.reshape(-1), gy.reshape(-1), gz.reshape(-1)], 1) * res + lo.to(dev)
+
+    def run(coord):
+        sdf = torch.empty(coord.shape[0], device=dev)
+        nn = torch.empty(coord.shape[0], dtype=torch.int32, device=dev)
+        for b0 in range(0, coord.shape[0], batch):
+            s, _, c, _, _ = query_sdf(nm, dec, coord[b0:b0 + batch], query_locally=False, want_grad=False,
+                                      zero_empty=True, want_certainty=False)
+            sdf[b0:b0 + batch] = s
+            nn[b0:b0 + batch] = c
+        return sdf, nn
+    coord = grid(0, R)
+    sdf, nn = run(coord)
+    assert bool(torch.isfinite(sdf).all()) and int(nn.max()) <= int(nm.neighbor_K)
+    assert 0.0 < float((nn > 0).float().mean()) < 1.0
+    full_sdf, full_nn = sdf.view(R, R, R), nn.view(R, R, R)
+    for k in range(4):
+        z0, z1 = k * R // 4, (k + 1) * R // 4
+        s, c = run(grid(z0, z1))
+        assert torch.equal(s.view(R, R, z1 - z0), full_sdf[:, :, z0:z1])
+        assert torch.equal(c.view(R, R, z1 - z0), full_nn[:, :, z0:z1])
+    del full_sdf, full_nn
+    # strided subset, denser where the surface is (the cells with neighbours)
+    occ = torch.nonzero(nn > 0).flatten()
+    sub = torch.cat((torch.arange(0, coord.shape[0], 100_003, device=dev), occ[::max(1, occ.numel() // 3000)]))
+    st, mlp = H.oracle_state(nm), H.oracle_mlp(dec)
+    osdf, _, _, oq = O.sdf_and_grad(st, mlp, _np(coord[sub]), 8, O.neighbor_offsets(2, 0.2), nm.max_valid_dist2,
+                                    True, False)
+    np.testing.assert_array_equal(_np(nn[sub]), oq.nn_counts)
+    empty = oq.nn_counts == 0
+    assert (_np(sdf[sub])[empty] == 0).all()
+    np.testing.assert_allclose(_np(sdf[sub])[~empty], osdf[~empty], rtol=0, atol=SDF_ATOL)

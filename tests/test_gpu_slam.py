@@ -1,5 +1,6 @@
 """BASELINE configs[0], the plumbing run: the reference's pin_slam.py frame loop (:96-257) over a
-12-frame synthetic 64-beam street sequence (64K points per scan), replayed through
+30-frame synthetic 64-beam street sequence (64K points per scan; three window filters of the
+sample pool, frames 9, 19, 29, and the decoder frozen after frame 15), replayed through
 pin_slam_amd's classes and compared with the reference's own run of the same loop
 (tests/golden/slam_seq.npz, written by tests/golden/gen_golden.py gen_slam_sequence with the
 reference's Tracker / Mapper / NeuralPoints / DataSampler and its dataset bookkeeping methods).
@@ -17,7 +18,7 @@ tests/test_gpu_mapper.py::test_whole_mapping_call_fixture.)
 Tolerances, checked per frame:
   * preprocessed cloud / source point counts, tracking validity, draw-stream position: exact;
   * pose within max(5 cm, 3 x spread) and max(0.1 deg, 3 x spread) of the reference's estimate,
-    and within 5 cm of the ground truth;
+    and within max(5 cm, the reference's own error + that tolerance) of the ground truth;
   * neural-point / local-map counts within max(1 %, 3 x spread), pool size within 0.1 %, new
     samples within max(15 %, 3 x spread) (they follow the certainty threshold);
   * the map's SDF on the surface (scan points placed by the TRUE poses) after frame 0 and at the
@@ -34,7 +35,7 @@ import pytest
 import torch
 
 import pin_slam_amd as P
-from pin_slam_amd.synthetic import FrameLoop
+from pin_slam_amd.synthetic import FrameLoop, lidar_scan, slam_poses, street_scene
 from tests.replay import ReplayDraws
 
 pytestmark = pytest.mark.gpu
@@ -97,9 +98,18 @@ def test_slam_sequence_matches_reference(golden, dev):
     def draws(n):
         return (torch.from_numpy(replay.randn(n * S)), torch.from_numpy(replay.rand(n * Ff)),
                 torch.from_numpy(replay.rand(n * Fb)))
+    # the scans, regenerated as the generator made them (same seed and call order), checked
+    # against the fixture's digests
+    import hashlib
+    rng = np.random.default_rng(int(z["scan_seed"]))
+    scene = street_scene(rng)
+    scans = [lidar_scan(T, scene, rng) for T in slam_poses(frames)]
+    for k, sc in enumerate(scans):
+        assert hashlib.sha256(np.ascontiguousarray(sc).tobytes()).hexdigest() == str(z["scan_sha256"][k]), \
+            f"frame {k}: regenerated scan differs from the reference run's"
     report = []
     for k in range(frames):
-        pts = torch.from_numpy(z[f"f{k}_scan"].astype(np.float32) / np.float32(z["q_scale"])).to(dev)
+        pts = torch.from_numpy(scans[k].astype(np.float32) / np.float32(z["q_scale"])).to(dev)
         seen = {}
 
         def check(part, k=k):
@@ -122,7 +132,9 @@ def test_slam_sequence_matches_reference(golden, dev):
         tol_t = max(0.05, 3 * float(z["spread_pose_dt"][k]))
         tol_r = max(0.1, 3 * float(z["spread_pose_dr"][k]))
         assert dt <= tol_t and dr <= tol_r, f"frame {k}: pose differs from the reference by {dt:.4f} m / {dr:.4f} deg"
-        assert dt_true <= 0.05, f"frame {k}: pose {dt_true:.4f} m from the ground truth"
+        # the reference itself drifts from the truth over the 30 frames (6-7 cm by frame 29)
+        ref_true, _ = _pose_err(z["hist_pose"][k], z["truth_poses"][k])
+        assert dt_true <= max(0.05, ref_true + tol_t), f"frame {k}: pose {dt_true:.4f} m from the ground truth"
         for name, g, w, rel in zip(("map_count", "local_count", "pool", "new"), counts, want, (0.01, 0.01, 0.001, 0.15)):
             rel = max(rel, 3 * float(z[f"spread_rel_{name}"][k]))
             assert _within(g, w, rel), f"frame {k}: {name} {g} vs reference {w}"

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/profm; rm -rf $OUT; mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-tracker --no-mesher --no-map-update \
-    --no-process-frame --no-nwf-leg --no-slam ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || exit $?
+    --no-process-frame --no-nwf-leg --no-slam --no-mapper-nwf ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || exit $?
 python3 - <<'PY'
 import csv
 rows = list(csv.DictReader(open("gpurun_out/profm/run_kernel_trace.csv")))

@@ -32,7 +32,7 @@ def run(args):
             legs = [] if os.environ.get("VAR_MAPPER") else ["--no-mapper"]
             legs += [] if os.environ.get("VAR_NWF") else ["--no-nwf-leg"]
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *legs, "--no-cpu-baseline",
-                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", "--no-slam", *args],
+                                "--no-tracker", "--no-mesher", "--no-map-update", "--no-process-frame", "--no-slam", "--no-mapper-nwf", *args],
                                env=env, capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 print(lib, "FAILED", r.stderr[-2000:])
