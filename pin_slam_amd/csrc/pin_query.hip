@@ -462,13 +462,22 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
 //                 lands at base[tile] + off.  The last block to finish zeroes the totals again.
 // Workspace state (PIN_ORDER_STATE_BYTES): tile totals + a done counter, zero before the first
 // call and zero again after each call; then n int2 (tile, off).
+// Tile capacity: 4,096 tiles (16x16-cell columns on the 1000x1000 surface: ~one wave per tile)
+// for batches below 1M rows; 16,384 for larger ones (the mapper's 1.68M rows over the 2000x2000
+// map: 16x16-cell columns instead of 32x32, ~107 rows per tile -- mapper +6 % measured; at 262K
+// queries the query kernel gains 2 us but the sort's larger histograms cost 4.5 us).
 #ifndef PIN_MAX_TILES
 #define PIN_MAX_TILES 4096
 #endif
-constexpr int kMaxTiles = PIN_MAX_TILES;   // 16x16-cell columns on the 1000x1000 surface: ~one wave per tile
+#ifndef PIN_MAX_TILES_LARGE
+#define PIN_MAX_TILES_LARGE 16384
+#endif
+constexpr int kMaxTiles = PIN_MAX_TILES;
+constexpr int kMaxTilesLarge = PIN_MAX_TILES_LARGE;
+constexpr int64_t kLargeBatch = 1 << 20;
 constexpr int kPartThreads = 1024;
-constexpr int kTpt = kMaxTiles / kPartThreads;   // tiles per thread in the atomic and scan phases
-static_assert(kMaxTiles % kPartThreads == 0, "tile capacity must be a multiple of the block");
+static_assert(kMaxTiles % kPartThreads == 0 && kMaxTilesLarge % kPartThreads == 0,
+              "tile capacity must be a multiple of the block");
 
 struct TileMap {
     int64_t ox, oy, oz;
@@ -485,10 +494,11 @@ __device__ __forceinline__ int tile_of(float x, float y, float z, const TileMap&
 }
 
 // Both kernels issue every load of a thread before using any (one memory round trip per phase).
-template <int PER>
+template <int PER, int MAXT>
 __global__ void __launch_bounds__(kPartThreads)
 k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ tot, int2* __restrict__ tk) {
-    __shared__ int h[kMaxTiles];
+    constexpr int kTpt = MAXT / kPartThreads;   // tiles per thread in the atomic and scan phases
+    __shared__ int h[MAXT];
     const int k = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < kTpt; ++j) h[k + j * kPartThreads] = 0;
@@ -526,11 +536,12 @@ k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__
     }
 }
 
-template <int PER>
+template <int PER, int MAXT>
 __global__ void __launch_bounds__(kPartThreads)
 k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict__ tot, unsigned* __restrict__ done,
              const int2* __restrict__ tk, float4* __restrict__ q4, int* __restrict__ order) {
-    __shared__ int base[kMaxTiles];
+    constexpr int kTpt = MAXT / kPartThreads;
+    __shared__ int base[MAXT];
     __shared__ int wsum[kPartThreads / 64];
     __shared__ int last;
     const int k = threadIdx.x;
@@ -577,7 +588,7 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
         const int64_t i = lo + (int64_t)u * kPartThreads;
-        const int64_t pos = (int64_t)base[e[u].x & (kMaxTiles - 1)] + e[u].y;
+        const int64_t pos = (int64_t)base[e[u].x & (MAXT - 1)] + e[u].y;
         if (i >= n || pos < 0 || pos >= n) continue;   // pos: only a workspace whose state was not zeroed
         if (q4) q4[pos] = make_float4(x[u], y[u], z[u], __int_as_float((int)i));
         if (order) order[pos] = (int)i;
@@ -591,8 +602,8 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
     }
 }
 
-// host: tile map of a grid box
-TileMap tile_map(const PinGrid& g) {
+// host: tile map of a grid box with at most maxt tiles
+TileMap tile_map(const PinGrid& g, int maxt) {
     TileMap t;
     t.ox = g.dims.ox;
     t.oy = g.dims.oy;
@@ -603,7 +614,7 @@ TileMap tile_map(const PinGrid& g) {
     for (;; ++sh) {
         const int64_t nx = (ex + (1ll << sh) - 1) >> sh, ny = (ey + (1ll << sh) - 1) >> sh,
                       nz = (ez + (1ll << sh) - 1) >> sh;
-        if (nx * ny * nz <= kMaxTiles) {
+        if (nx * ny * nz <= maxt) {
             t.ntx = (int)nx;
             t.nty = (int)ny;
             t.ntz = (int)nz;
@@ -621,11 +632,15 @@ TileMap tile_map(const PinGrid& g) {
 // 4M): few blocks keep the same-address atomics on the tile totals few.
 int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* order, void* workspace,
                  hipStream_t s) {
-    const TileMap t = tile_map(g);
+    const bool large = n >= kLargeBatch;
+    const TileMap t = tile_map(g, large ? kMaxTilesLarge : kMaxTiles);
     char* ws = (char*)workspace;
     int* tot = (int*)ws;
-    unsigned* done = (unsigned*)(ws + 4 * kMaxTiles);
-    static_assert(4 * kMaxTiles + 64 <= PIN_ORDER_STATE_BYTES, "order workspace state too small");
+    // the done counter sits past the largest capacity's totals (either capacity leaves its
+    // totals zero, so calls of both sizes may share a workspace)
+    unsigned* done = (unsigned*)(ws + 4 * (kMaxTilesLarge > kMaxTiles ? kMaxTilesLarge : kMaxTiles));
+    static_assert(4 * kMaxTilesLarge + 64 <= PIN_ORDER_STATE_BYTES && 4 * kMaxTiles + 64 <= PIN_ORDER_STATE_BYTES,
+                  "order workspace state too small");
     int2* tk = (int2*)(ws + PIN_ORDER_STATE_BYTES);
     // the placement does not depend on the ranking's blocks: it runs 2 queries per thread (more
     // blocks in flight for its scattered 16-B stores)
@@ -637,15 +652,17 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
 #endif
     constexpr int kPlacePer = PIN_PLACE_PER;
     const int nplace = (int)((n + kPlacePer * kPartThreads - 1) / (kPlacePer * kPartThreads));
-    auto launch = [&](auto per_tag) {
+    auto launch = [&](auto per_tag, auto maxt_tag) {
         constexpr int PER = decltype(per_tag)::value;
+        constexpr int MAXT = decltype(maxt_tag)::value;
         const int nblk = (int)((n + PER * kPartThreads - 1) / (PER * kPartThreads));
-        hipLaunchKernelGGL(k_tile_rank<PER>, dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot, tk);
-        hipLaunchKernelGGL(k_tile_place<kPlacePer>, dim3(nplace), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot, done,
-                           tk, q4, order);
+        hipLaunchKernelGGL((k_tile_rank<PER, MAXT>), dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot, tk);
+        hipLaunchKernelGGL((k_tile_place<kPlacePer, MAXT>), dim3(nplace), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot,
+                           done, tk, q4, order);
     };
-    if (n <= (1 << 19)) launch(std::integral_constant<int, PIN_RANK_PER>());
-    else launch(std::integral_constant<int, 16>());
+    if (n <= (1 << 19)) launch(std::integral_constant<int, PIN_RANK_PER>(), std::integral_constant<int, kMaxTiles>());
+    else if (!large) launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTiles>());
+    else launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTilesLarge>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 

@@ -165,56 +165,86 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     if (live) st.sdf[r] = sdf;
 }
 
-// End of a training forward block (all threads): the rows' neighbour ids / weights (cid, cw) are
-// staged in LDS, stored to st.ids / st.weights as the block's contiguous [rows, nn_k] run (256-B
-// coalesced stores instead of one 4-B store per lane and neighbour at a 4 nn_k-B stride, which
-// cost ~115 us of the 1.68M-row forward), then the training side effects are applied
-// (neural_points.py:640 certainty scatter_add, :644 ts amax).  The side effects are one
-// memory-side atomic per (row, neighbour); with one lane per row every wave-instruction would hit
-// 64 unrelated 64-B segments (the slow shape, MI355X_MICROARCH.md Global float atomics), so they
-// are issued transposed, 8 lanes per row, 8 rows per instruction: a row's neighbours (adjacent
-// cells) share segments, and the ts reads (the max is usually a no-op) are issued together
-// instead of one dependent read per neighbour inside the streaming loop.
+// End of a training forward (all lanes of every wave, each wave on its own 64 rows -- no block
+// barrier: a wave flushes as soon as its own scan and decode are done).  Everything is staged in
+// the wave's slice of the scan list (free once the scan and the decoder are done):
+//  * the rows' neighbour ids / weights (cid, cw) are stored to st.ids / st.weights as the wave's
+//    contiguous [64, nn_k] run (256-B coalesced stores instead of one 4-B store per lane and
+//    neighbour at a 4 nn_k-B stride, which cost ~115 us of the 1.68M-row forward);
+//  * the certainty side effect (neural_points.py:640 scatter_add) is pre-summed per point in a
+//    512-slot table keyed by the id's low bits (LDS CAS on the tag, LDS float add; a slot taken
+//    by another id sends the add straight to memory), then the table goes out slot by slot: each
+//    memory-side atomic instruction covers 64 consecutive slots, i.e. ids that differ in their
+//    low bits only, instead of 64 (row, neighbour) pairs scattered over 8 rows' neighbourhoods
+//    (on the 4M-point map the scattered form cost ~115 us; the same atomics at contiguous
+//    addresses ~17 us);
+//  * the ts amax (:644): the reads of ts_update (the max is usually a no-op) issued together, 8
+//    lanes per row, then the atomicMax of the rows that raise it.
+// t0: the processing slot of the block's first row.
+constexpr int kCertSlots = 512;
+static_assert(kListSeg * 64 >= 2 * 64 * kK + 2 * kCertSlots, "flush staging must fit the wave's scan list");
+
 __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainState& st, int64_t t0, int64_t rows,
                                            const int (&cid)[kK], const float (&cw)[kK], int64_t qts,
                                            bool store_ids) {
-    __shared__ int s_id[kBlock * kK];
-    __shared__ float s_w[kBlock * kK];
-    __shared__ int64_t s_ts[kBlock];
-    const int tid = threadIdx.x;
+    __shared__ int64_t s_ts_all[kBlock / 64][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* const s_id = wave_list();
+    float* const s_w = (float*)(s_id + 64 * kK);
+    int* const tag = s_id + 2 * 64 * kK;
+    float* const val = (float*)(tag + kCertSlots);
+    int64_t* const s_ts = s_ts_all[wave];
+    wave_lds_sync();   // the slice was the scan list / decoder scratch: every lane is past its reads
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
-        s_id[tid * kK + j] = cid[j];
-        s_w[tid * kK + j] = cw[j];
+        s_id[lane * kK + j] = cid[j];
+        s_w[lane * kK + j] = cw[j];
     }
-    s_ts[tid] = qts;
-    __syncthreads();
-    if (store_ids && t0 < rows) {
+    s_ts[lane] = qts;
+    if (st.certainties) {
+#pragma unroll
+        for (int k = lane; k < kCertSlots; k += 64) {
+            tag[k] = -1;
+            val[k] = 0.f;
+        }
+    }
+    wave_lds_sync();
+    const int64_t tw = t0 + 64 * wave;   // the wave's first slot
+    if (store_ids && tw < rows) {
         const int nn_k = c.nn_k;
-        const int nr = (int)(rows - t0 < kBlock ? rows - t0 : kBlock);
-        int* __restrict__ ido = st.ids + t0 * nn_k;
-        float* __restrict__ wo = st.weights + t0 * nn_k;
+        const int nr = (int)(rows - tw < 64 ? rows - tw : 64);
+        int* __restrict__ ido = st.ids + tw * nn_k;
+        float* __restrict__ wo = st.weights + tw * nn_k;
         if (nn_k == kK) {
-            for (int e = tid; e < nr * kK; e += kBlock) {
+            for (int e = lane; e < nr * kK; e += 64) {
                 ido[e] = s_id[e];
                 wo[e] = s_w[e];
             }
         } else {
-            for (int e = tid; e < nr * nn_k; e += kBlock) {
+            for (int e = lane; e < nr * nn_k; e += 64) {
                 const int r = e / nn_k, j = e - r * nn_k;
                 ido[e] = s_id[r * kK + j];
                 wo[e] = s_w[r * kK + j];
             }
         }
     }
-    const int base = (tid & ~63) * kK, lane = tid & 63;
     if (st.certainties) {
         float* __restrict__ cert = st.certainties;
 #pragma unroll
-        for (int u = 0; u < kK; ++u) {
-            const int e = base + u * 64 + lane;
-            const int id = s_id[e];
-            if (id >= 0) atomicAdd(cert + id, s_w[e]);
+        for (int j = 0; j < kK; ++j) {
+            const int id = cid[j];
+            if (id >= 0) {
+                const int k = id & (kCertSlots - 1);
+                const int old = atomicCAS(tag + k, -1, id);
+                if (old == -1 || old == id) atomicAdd(val + k, cw[j]);
+                else atomicAdd(cert + id, cw[j]);
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int k = lane; k < kCertSlots; k += 64) {
+            const int id = tag[k];
+            if (id >= 0) atomicAdd(cert + id, val[k]);
         }
     }
     if (st.ts_update) {
@@ -222,13 +252,13 @@ __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainS
         int64_t cur[kK];
 #pragma unroll
         for (int u = 0; u < kK; ++u) {
-            const int e = base + u * 64 + lane;
+            const int e = u * 64 + lane;
             const int id = s_id[e];
             cur[u] = (id >= 0 && s_ts[e / kK] >= 0) ? ts_update[id] : INT64_MAX;
         }
 #pragma unroll
         for (int u = 0; u < kK; ++u) {
-            const int e = base + u * 64 + lane;
+            const int e = u * 64 + lane;
             const int64_t q = s_ts[e / kK];
             if (cur[u] < q) atomicMax((unsigned long long*)(ts_update + s_id[e]), (unsigned long long)q);
         }
