@@ -473,8 +473,10 @@ typedef struct PinTrainState {
     float* x;                    /* weighted_first: [rows, 11] decoder input (PIN_TRAIN_DX: [rows, 8] s dsdf/dx
                                     over the features); else [rows, nn_k, 3] vectors */
     float* sdf;                  /* [rows] predicted sdf */
-    float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL */
-    int64_t* ts_update;          /* [L] amax with the main rows' ts (neural_points.py:644), may be NULL */
+    float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL;
+                                    applied by pin_train_backward from ids / weights */
+    int64_t* ts_update;          /* [L] amax with the batch rows' ts (row_ts, neural_points.py:644), may be
+                                    NULL; applied by pin_train_backward */
     const int32_t* order;        /* [rows] processing order (pin_query_order over pin_train_rows), may be
                                     NULL; ids/weights/x are stored per processing slot, sdf per row */
     const float* sorted_rows;    /* [rows,4] the rows in processing order as {x, y, z, bits(row)}
@@ -487,6 +489,8 @@ typedef struct PinTrainState {
     float* eik_vec;              /* PIN_TRAIN_EIK: weighted_first: [rows, 11] A^T u = sum_j (u . dw_j/dq) x_j
                                     + (sum_j w_j) [0, u] (decoder-parameter term, written only when
                                     the decoder trains); per-neighbour: [rows, 3] u */
+    const int64_t* row_ts;       /* [n_main] the batch rows' ts (the `ts` of pin_train_forward), read by
+                                    pin_train_backward for the ts_update side effect; NULL: none */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */

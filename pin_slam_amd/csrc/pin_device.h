@@ -191,10 +191,12 @@ __device__ __forceinline__ uint32_t sel4v(uint32_t w0, uint32_t w1, uint32_t w2,
 #define PIN_LIST_SEG 32
 #endif
 constexpr int kListSeg = PIN_LIST_SEG;   // offsets per list segment
-__device__ __forceinline__ int* wave_list() {
+// the block's lists, contiguous: after a block barrier a kernel may reuse all of it (block_list)
+__device__ __forceinline__ int* block_list() {
     __shared__ int s_list[kBlock / 64][kListSeg * 64];
-    return s_list[threadIdx.x >> 6];
+    return &s_list[0][0];
 }
+__device__ __forceinline__ int* wave_list() { return block_list() + (threadIdx.x >> 6) * (kListSeg * 64); }
 
 // IDP: the top-k payload is the record's feature-row id (flags stripped) instead of its
 // compact index -- for the training forward, which reads features and positions by id and never
@@ -217,6 +219,24 @@ struct GridSource {
 
     template <int CH>
     __device__ __forceinline__ int scan(float qx, float qy, float qz, TopK& tk) const {
+#if defined(PIN_CHECK_SCAN) && PIN_CHECK_SCAN
+        // self-check build (tools/check_scan.py): the brick-window scan -- its wave-major LDS
+        // list shared with the decoder scratch -- against the per-cell scan, which uses no LDS;
+        // the same cells in the same order must give the same count, payloads and distances
+        // bitwise.  A mismatch poisons the query (nearest distance NaN -> NaN outputs).
+        if (gr.window <= 2) {
+            TopK t2;
+            t2.init();
+            const int n2 = scan_cells<CH>(qx, qy, qz, t2);
+            const int n1 = scan_window<CH>(qx, qy, qz, tk);
+            bool same = n1 == n2;
+#pragma unroll
+            for (int j = 0; j < kK; ++j)
+                same = same && tk.g[j] == t2.g[j] && __float_as_int(tk.d[j]) == __float_as_int(t2.d[j]);
+            if (!same) tk.d[0] = __int_as_float(0x7fc00000);
+            return n1;
+        }
+#endif
         if (gr.window <= 2) return scan_window<CH>(qx, qy, qz, tk);
         return scan_cells<CH>(qx, qy, qz, tk);
     }

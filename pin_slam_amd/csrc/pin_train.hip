@@ -58,7 +58,7 @@ template <bool WF, class Src, bool MF = false>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
-                                                   float (&cw)[kK], int64_t& qts_out, bool live = true) {
+                                                   float (&cw)[kK], bool live = true) {
     // t: processing slot (per-slot state), r: the row it processes (row order: sdf, ts)
     if (!live) t = 0;
     int64_t r;
@@ -86,8 +86,6 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
 #pragma unroll
     for (int d = 0; d < kD; ++d) x[d] = 0.f;
     float sdf = 0.f;
-    const int64_t qts = (live && ts && r < c.n_main) ? ts[r] : -1;
-    qts_out = qts;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
@@ -166,101 +164,41 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
 }
 
 // End of a training forward (all lanes of every wave, each wave on its own 64 rows -- no block
-// barrier: a wave flushes as soon as its own scan and decode are done).  Everything is staged in
-// the wave's slice of the scan list (free once the scan and the decoder are done):
-//  * the rows' neighbour ids / weights (cid, cw) are stored to st.ids / st.weights as the wave's
-//    contiguous [64, nn_k] run (256-B coalesced stores instead of one 4-B store per lane and
-//    neighbour at a 4 nn_k-B stride, which cost ~115 us of the 1.68M-row forward);
-//  * the certainty side effect (neural_points.py:640 scatter_add) is pre-summed per point in a
-//    512-slot table keyed by the id's low bits (LDS CAS on the tag, LDS float add; a slot taken
-//    by another id sends the add straight to memory), then the table goes out slot by slot: each
-//    memory-side atomic instruction covers 64 consecutive slots, i.e. ids that differ in their
-//    low bits only, instead of 64 (row, neighbour) pairs scattered over 8 rows' neighbourhoods
-//    (on the 4M-point map the scattered form cost ~115 us; the same atomics at contiguous
-//    addresses ~17 us);
-//  * the ts amax (:644): the reads of ts_update (the max is usually a no-op) issued together, 8
-//    lanes per row, then the atomicMax of the rows that raise it.
+// barrier): the rows' neighbour ids / weights (cid, cw) are staged in the wave's slice of the scan
+// list (free once the scan and the decoder are done) and stored to st.ids / st.weights as the
+// wave's contiguous [64, nn_k] run (256-B coalesced stores instead of one 4-B store per lane and
+// neighbour at a 4 nn_k-B stride, which cost ~115 us of the 1.68M-row forward).  The training
+// side effects are applied by the backward (train_side_effects) from these arrays.
 // t0: the processing slot of the block's first row.
-constexpr int kCertSlots = 512;
-static_assert(kListSeg * 64 >= 2 * 64 * kK + 2 * kCertSlots, "flush staging must fit the wave's scan list");
-
 __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainState& st, int64_t t0, int64_t rows,
-                                           const int (&cid)[kK], const float (&cw)[kK], int64_t qts,
-                                           bool store_ids) {
-    __shared__ int64_t s_ts_all[kBlock / 64][64];
+                                           const int (&cid)[kK], const float (&cw)[kK]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int* const s_id = wave_list();
     float* const s_w = (float*)(s_id + 64 * kK);
-    int* const tag = s_id + 2 * 64 * kK;
-    float* const val = (float*)(tag + kCertSlots);
-    int64_t* const s_ts = s_ts_all[wave];
+    static_assert(kListSeg * 64 >= 2 * 64 * kK, "flush staging must fit the wave's scan list");
     wave_lds_sync();   // the slice was the scan list / decoder scratch: every lane is past its reads
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         s_id[lane * kK + j] = cid[j];
         s_w[lane * kK + j] = cw[j];
     }
-    s_ts[lane] = qts;
-    if (st.certainties) {
-#pragma unroll
-        for (int k = lane; k < kCertSlots; k += 64) {
-            tag[k] = -1;
-            val[k] = 0.f;
-        }
-    }
     wave_lds_sync();
     const int64_t tw = t0 + 64 * wave;   // the wave's first slot
-    if (store_ids && tw < rows) {
-        const int nn_k = c.nn_k;
-        const int nr = (int)(rows - tw < 64 ? rows - tw : 64);
-        int* __restrict__ ido = st.ids + tw * nn_k;
-        float* __restrict__ wo = st.weights + tw * nn_k;
-        if (nn_k == kK) {
-            for (int e = lane; e < nr * kK; e += 64) {
-                ido[e] = s_id[e];
-                wo[e] = s_w[e];
-            }
-        } else {
-            for (int e = lane; e < nr * nn_k; e += 64) {
-                const int r = e / nn_k, j = e - r * nn_k;
-                ido[e] = s_id[r * kK + j];
-                wo[e] = s_w[r * kK + j];
-            }
+    if (tw >= rows) return;
+    const int nn_k = c.nn_k;
+    const int nr = (int)(rows - tw < 64 ? rows - tw : 64);
+    int* __restrict__ ido = st.ids + tw * nn_k;
+    float* __restrict__ wo = st.weights + tw * nn_k;
+    if (nn_k == kK) {
+        for (int e = lane; e < nr * kK; e += 64) {
+            ido[e] = s_id[e];
+            wo[e] = s_w[e];
         }
-    }
-    if (st.certainties) {
-        float* __restrict__ cert = st.certainties;
-#pragma unroll
-        for (int j = 0; j < kK; ++j) {
-            const int id = cid[j];
-            if (id >= 0) {
-                const int k = id & (kCertSlots - 1);
-                const int old = atomicCAS(tag + k, -1, id);
-                if (old == -1 || old == id) atomicAdd(val + k, cw[j]);
-                else atomicAdd(cert + id, cw[j]);
-            }
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int k = lane; k < kCertSlots; k += 64) {
-            const int id = tag[k];
-            if (id >= 0) atomicAdd(cert + id, val[k]);
-        }
-    }
-    if (st.ts_update) {
-        int64_t* __restrict__ ts_update = st.ts_update;
-        int64_t cur[kK];
-#pragma unroll
-        for (int u = 0; u < kK; ++u) {
-            const int e = u * 64 + lane;
-            const int id = s_id[e];
-            cur[u] = (id >= 0 && s_ts[e / kK] >= 0) ? ts_update[id] : INT64_MAX;
-        }
-#pragma unroll
-        for (int u = 0; u < kK; ++u) {
-            const int e = u * 64 + lane;
-            const int64_t q = s_ts[e / kK];
-            if (cur[u] < q) atomicMax((unsigned long long*)(ts_update + s_id[e]), (unsigned long long)q);
+    } else {
+        for (int e = lane; e < nr * nn_k; e += 64) {
+            const int r = e / nn_k, j = e - r * nn_k;
+            ido[e] = s_id[r * kK + j];
+            wo[e] = s_w[r * kK + j];
         }
     }
 }
@@ -276,14 +214,13 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
-    int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const HashSource src(h, p);
-        train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts, t < rows);
+        train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, t < rows);
     }
-    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw, qts, true);
+    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw);
 }
 
 template <bool WF, bool MF>
@@ -297,15 +234,14 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
-    int64_t qts = -1;
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const GridSource<false, PIN_TRAIN_IDP> src(g, p);
-        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, qts,
+        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw,
                                                                      t < rows);
     }
-    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw, qts, true);
+    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw);
 }
 
 __global__ void __launch_bounds__(kBlock)
@@ -485,8 +421,7 @@ template <bool WF, class Src>
 __device__ __forceinline__ void train_forward_eik_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                        const float* __restrict__ coord,
                                                        const int64_t* __restrict__ ts, const PinTrainCfg& c,
-                                                       int64_t t, const PinTrainState& st, bool mlp_trains,
-                                                       int (&cid)[kK], float (&cw)[kK], int64_t& qts_out) {
+                                                       int64_t t, const PinTrainState& st, bool mlp_trains) {
     int64_t r;
     float qx, qy, qz;
     if (st.sorted_rows) {
@@ -509,8 +444,7 @@ __device__ __forceinline__ void train_forward_eik_body(const Src& src, const Pin
         S = S + u[j];
     }
     const float invS = nn > 0 ? 1.f / S : 0.f;
-    qts_out = (ts && r < c.n_main) ? ts[r] : -1;
-    float x[kD], J[kD][3], C[3] = {0.f, 0.f, 0.f}, Wr[3][3], cc[kK][3];
+    float x[kD], J[kD][3], C[3] = {0.f, 0.f, 0.f}, Wr[3][3], cc[kK][3], cw[kK];
     float A[3] = {0.f, 0.f, 0.f}, G[3] = {0.f, 0.f, 0.f}, sdf = 0.f;
 #pragma unroll
     for (int d = 0; d < kD; ++d) { x[d] = 0.f; J[d][0] = J[d][1] = J[d][2] = 0.f; }
@@ -543,7 +477,6 @@ __device__ __forceinline__ void train_forward_eik_body(const Src& src, const Pin
             st.ids[t * nn_k + j] = id;
             st.weights[t * nn_k + j] = w;
         }
-        cid[j] = id;
         cw[j] = w;
         const float cu = valid ? -2.f * u[j] * u[j] * invS : 0.f;
 #pragma unroll
@@ -655,13 +588,7 @@ __device__ __forceinline__ void train_forward_eik_kernel_body(const Src& src, co
                                                               const float* coord, const int64_t* ts, PinTrainCfg c,
                                                               PinTrainState st, bool mlp_trains) {
     const int64_t t = xcd_block() * kBlock + threadIdx.x;
-    int cid[kK];
-    float cw[kK];
-    int64_t qts = -1;
-#pragma unroll
-    for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains, cid, cw, qts);
-    flush_rows(c, st, xcd_block() * kBlock, c.n_main, cid, cw, qts, false);
+    if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains);
 }
 
 template <bool WF>
@@ -680,6 +607,94 @@ k_train_forward_eik_grid(const PinGrid g, const PinPoints p, const PinMlp m, con
     __shared__ float s_mlp[kWSize];
     const MlpW mw = stage_mlp(m, s_mlp);
     train_forward_eik_kernel_body<WF>(GridSource<false, false>(g, p), p, mw, coord, ts, c, st, mlp_trains != 0);
+}
+
+// The training side effects of the iteration's training-mode query (neural_points.py:640
+// certainty scatter_add of the IDW weights, :644 ts_update amax with the batch rows' ts), applied
+// at the end of the backward from the saved ids / weights (all threads of the block):
+//  1. every (row, neighbour) of the block's rows writes its id as the tag of slot id & (S-1) of
+//     an LDS table; after a barrier the pairs whose id kept the slot add their weight (LDS float
+//     add) and max their row's ts (LDS int max) into it -- no returning atomics -- and a pair
+//     whose slot went to another id goes to memory directly;
+//  2. the table goes out slot by slot: one memory-side atomic (and one ts_update read) per
+//     distinct point of the block, each instruction covering consecutive slots, i.e. ids that
+//     differ in their low bits only.
+// In the forward, one atomic per (row, neighbour) pair scattered over the rows' neighbourhoods
+// cost ~115 us of the 1.68M-row iteration (the same atomics at contiguous addresses: ~17 us).
+constexpr int kCertSlots = 1024;
+
+__device__ __forceinline__ void ts_amax(int64_t* __restrict__ ts_update, int id, int64_t q) {
+    if (ts_update[id] < q) atomicMax((unsigned long long*)(ts_update + id), (unsigned long long)q);
+}
+
+constexpr int kSideBufInts = 3 * kCertSlots + 2 * kBlock;   // tag, val, ts per slot + the rows' int64 ts
+
+// The table in buf (kSideBufInts ints of the block's LDS): tag, weight sum and max ts per slot,
+// then the block's rows' ts.
+struct SideTable {
+    int* tag;
+    float* val;
+    int* ts;
+    int64_t* rts;
+    float* cert;
+    int64_t* ts_update;
+    __device__ SideTable(int* buf, const PinTrainState& st)
+        : tag(buf), val((float*)(buf + kCertSlots)), ts(buf + 2 * kCertSlots), rts((int64_t*)(buf + 3 * kCertSlots)),
+          cert(st.certainties), ts_update(st.row_ts ? st.ts_update : nullptr) {}
+    // all threads, then a barrier before any claim: empty slots; thread tid's row ts (batch rows
+    // only -- the stencil rows' query carries none)
+    __device__ void init(const PinTrainCfg& c, const PinTrainState& st, int nrow_blk, int64_t row) const {
+        const int tid = threadIdx.x;
+        rts[tid] = (ts_update && tid < nrow_blk && row < c.n_main) ? st.row_ts[row] : -1;
+        for (int k = tid; k < kCertSlots; k += kBlock) {
+            tag[k] = -1;
+            val[k] = 0.f;
+            ts[k] = -1;
+        }
+    }
+    __device__ void claim(int id) const {
+        if (id >= 0) tag[id & (kCertSlots - 1)] = id;
+    }
+    // after a barrier that follows every claim: pair (id, w) of local row lr
+    __device__ void add(int id, float w, int lr) const {
+        if (id < 0) return;
+        const int k = id & (kCertSlots - 1);
+        const int64_t q = rts[lr];
+        if (tag[k] == id && q <= 0x7fffffff) {
+            if (cert) atomicAdd(val + k, w);
+            if (q >= 0) atomicMax(ts + k, (int)q);
+        } else {   // the slot went to another id (or a ts beyond int32): straight to memory
+            if (cert) atomicAdd(cert + id, w);
+            if (ts_update && q >= 0) ts_amax(ts_update, id, q);
+        }
+    }
+    // after a barrier that follows every add: one memory-side atomic per occupied slot
+    __device__ void flush() const {
+        for (int k = threadIdx.x; k < kCertSlots; k += kBlock) {
+            const int id = tag[k];
+            if (id < 0) continue;
+            if (cert) atomicAdd(cert + id, val[k]);
+            if (ts_update && ts[k] >= 0) ts_amax(ts_update, id, ts[k]);
+        }
+    }
+};
+
+// The side effects on their own (no feature scatter to ride on): the block's ids / weights read
+// from memory.  All threads.
+__device__ __forceinline__ void train_side_effects(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
+                                                   int nrow_blk, int64_t row, int* buf) {
+    const SideTable tb(buf, st);
+    tb.init(c, st, nrow_blk, row);
+    __syncthreads();
+    const int nn_k = c.nn_k;
+    const int npair = nrow_blk * nn_k;
+    const int* __restrict__ ids = st.ids + row0 * nn_k;
+    const float* __restrict__ ws = st.weights + row0 * nn_k;
+    for (int e = threadIdx.x; e < npair; e += kBlock) tb.claim(ids[e]);
+    __syncthreads();
+    for (int e = threadIdx.x; e < npair; e += kBlock) tb.add(ids[e], ws[e], e / nn_k);
+    __syncthreads();
+    tb.flush();
 }
 
 // backward: one row per lane for the decoder; the row's k x 8 feature-gradient terms are staged
@@ -831,6 +846,52 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
         for (int d = 0; d < kF; ++d) gf[d] = fmaf(delta, wr[d], gf[d]);
     }
 }
+
+// Scatter of the block's weighted_first feature-gradient rows (all threads; after a barrier):
+// element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour) pairs x 32
+// contiguous bytes, one memory-side request each -- the cheapest atomic shape measured (LDS
+// pre-aggregation per block, and 64-B rows carrying the certainty, were slower).  The block's ids
+// and weights are staged in LDS first with coalesced loads, so the scatter loop issues its
+// atomics back to back instead of waiting on a load per element.
+// buf: (2 + EIK) kBlock kK ints of the block's LDS
+// se (optional, initialised, a barrier since): the training side effects ride on the scatter --
+// the staging pass claims the table slots, the scatter's d = 0 lane of each pair adds its weight.
+template <bool EIK>
+__device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
+                                                int nrow_blk, const float* gst, const float* s_dsdf,
+                                                float* __restrict__ grad_features, int* buf, const SideTable* se) {
+    int* const s_ids = buf;
+    float* const s_wt = (float*)(buf + kBlock * kK);
+    float* const s_al = (float*)(buf + 2 * kBlock * kK);
+    const int nn_k = c.nn_k;
+    const int npair = nrow_blk * nn_k;
+    for (int e = threadIdx.x; e < npair; e += kBlock) {
+        const int id = st.ids[row0 * nn_k + e];
+        s_ids[e] = id;
+        s_wt[e] = st.weights[row0 * nn_k + e];
+        if (EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
+        if (se) se->claim(id);
+    }
+    __syncthreads();
+    const int total = npair * kF;
+    for (int e = threadIdx.x; e < total; e += kBlock) {
+        const int d = e & (kF - 1);
+        const int rj = e >> 3;
+        const int id = s_ids[rj];
+        if (id < 0) continue;
+        const int lr = rj / nn_k;
+        float g;
+        if (EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
+        else g = s_wt[rj] * gst[lr * kF + d];
+        atomicAdd(grad_features + (int64_t)id * kF + d, g);
+        if (se && d == 0) se->add(id, s_wt[rj], lr);
+    }
+    if (se) {
+        __syncthreads();
+        se->flush();
+    }
+}
+
 
 // MF, frozen decoder (no MLP_GRAD), mlp->packed:
 //   weighted_first (PIN_TRAIN_DX): x holds s dsdf/dx[0:8] per slot from the forward; the feature
@@ -1035,36 +1096,35 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     }
     if constexpr (MLP_GRAD) mlp_grad_flush<EIK>(s_mg, s_so, accT, accE, so_sum, mlp_part + (int64_t)blockIdx.x * kMlpPart);
     __syncthreads();
-    if (!WF || !grad_features) return;   // per-neighbour: scattered in the neighbour loop
-    // scatter: element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour)
-    // pairs x 32 contiguous bytes, one memory-side request each -- the cheapest atomic shape
-    // measured (LDS pre-aggregation per block, and 64-B rows carrying the certainty, were slower).
-    // The block's ids (and WF weights) are staged in LDS first with coalesced loads, so the
-    // scatter loop issues its atomics back to back instead of waiting on a load per element.
-    __shared__ int s_ids[WF ? kBlock * kK : 1];
-    __shared__ float s_wt[WF ? kBlock * kK : 1];
-    __shared__ float s_al[WF && EIK ? kBlock * kK : 1];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int nrow_blk = (int)(nrows - row0 < kBlock ? nrows - row0 : kBlock);
-    const int npair = nrow_blk * nn_k;
-    for (int e = threadIdx.x; e < npair; e += kBlock) {
-        s_ids[e] = st.ids[row0 * nn_k + e];
-        if (WF) s_wt[e] = st.weights[row0 * nn_k + e];
-        if (WF && EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
+    // LDS of the scatter's staging and of the side-effect table: buffers the kernel is done with
+    // where they fit (the block's scan lists after the per-neighbour matrix-core decodes, the
+    // decoder-gradient staging s_mg after mlp_grad_flush), else buffers of their own
+    constexpr int kScat = WF ? (EIK ? 3 : 2) * kBlock * kK : 0;
+    constexpr int kMg = kWaves * kMgWave;
+    constexpr bool kTabMg = MLP_GRAD && kScat + kSideBufInts <= kMg;
+    constexpr int kOwnScat = MLP_GRAD ? 0 : kScat;
+    constexpr int kOwnTab = (kDecode || kTabMg) ? 0 : kSideBufInts;
+    static_assert(!kDecode || kSideBufInts <= kBlock * kListSeg, "side-effect table must fit the scan lists");
+    static_assert(!MLP_GRAD || kScat <= kMg, "scatter staging must fit the decoder-gradient staging");
+    __shared__ int s_scat[kOwnScat > 0 ? kOwnScat : 1];
+    __shared__ int s_tab[kOwnTab > 0 ? kOwnTab : 1];
+    int* const s_pair = MLP_GRAD ? (int*)&s_mg[0][0] : s_scat;
+    int* const tab = kDecode ? block_list() : (kTabMg ? (int*)&s_mg[0][0] + kScat : s_tab);
+    const bool side = st.certainties || (st.ts_update && st.row_ts);
+    const SideTable se(tab, st);
+    if constexpr (WF) {
+        if (grad_features) {
+            if (side) {
+                se.init(c, st, nrow_blk, row);
+                __syncthreads();
+            }
+            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, grad_features, s_pair, side ? &se : nullptr);
+            return;
+        }
     }
-    __syncthreads();
-    const int total = npair * kF;
-    for (int e = threadIdx.x; e < total; e += kBlock) {
-        const int d = e & (kF - 1);
-        const int rj = e >> 3;
-        const int id = s_ids[rj];
-        if (id < 0) continue;
-        const int lr = rj / nn_k;
-        float g;
-        if (WF && EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
-        else g = s_wt[rj] * gst[lr * kF + d];
-        atomicAdd(grad_features + (int64_t)id * kF + d, g);
-    }
+    if (side) train_side_effects(c, st, row0, nrow_blk, row, tab);
 }
 
 __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ part, int64_t n,

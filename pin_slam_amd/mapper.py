@@ -681,7 +681,7 @@ class Mapper:
                                 sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                 ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
                                 order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None,
-                                row_weight=_lib.ptr(wrow))
+                                row_weight=_lib.ptr(wrow), row_ts=_lib.ptr(ts64))
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK and not analytic

@@ -17,7 +17,8 @@ tests/test_gpu_mapper.py::test_whole_mapping_call_fixture.)
 
 Tolerances, checked per frame:
   * preprocessed cloud / source point counts, tracking validity, draw-stream position: exact;
-  * pose within max(5 cm, 3 x spread) and max(0.1 deg, 3 x spread) of the reference's estimate,
+  * pose within max(5 cm, 3 x spread) and max(0.1 deg, 3 x spread) of the reference's estimate
+    (spread: the largest 1- vs 8-thread difference of the reference up to that frame),
     and within max(5 cm, the reference's own error + that tolerance) of the ground truth;
   * neural-point / local-map counts within max(1 %, 3 x spread), pool size within 0.1 %, new
     samples within max(15 %, 3 x spread) (they follow the certainty threshold);
@@ -129,8 +130,11 @@ def test_slam_sequence_matches_reference(golden, dev):
         dt, dr = _pose_err(loop.cur_pose_ref, z["hist_pose"][k])
         dt_true, _ = _pose_err(loop.cur_pose_ref, z["truth_poses"][k])
         report.append((k, round(dt, 4), round(dr, 4), round(dt_true, 4), counts, want))
-        tol_t = max(0.05, 3 * float(z["spread_pose_dt"][k]))
-        tol_r = max(0.1, 3 * float(z["spread_pose_dr"][k]))
+        # the reference's own 1- vs 8-thread runs differ by up to 3.3 cm by frame 13 and re-converge
+        # and diverge again afterwards: the spread up to frame k bounds how far two legitimate runs
+        # may be apart at frame k
+        tol_t = max(0.05, 3 * float(np.max(z["spread_pose_dt"][:k + 1])))
+        tol_r = max(0.1, 3 * float(np.max(z["spread_pose_dr"][:k + 1])))
         assert dt <= tol_t and dr <= tol_r, f"frame {k}: pose differs from the reference by {dt:.4f} m / {dr:.4f} deg"
         # the reference itself drifts from the truth over the 30 frames (6-7 cm by frame 29)
         ref_true, _ = _pose_err(z["hist_pose"][k], z["truth_poses"][k])

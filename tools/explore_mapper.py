@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Timing attribution for one mapper iteration as mapping() runs it (GPU only): the forward with
-and without its training side effects, the backward with and without the feature scatter, on
-the rows of a real iteration (tile-sorted, PIN_TRAIN_DX when the decoder is frozen)."""
+"""Timing attribution for one mapper iteration as mapping() runs it (GPU only): the forward, the
+backward with and without the training side effects (certainty / ts, applied there) and without
+the feature scatter, on the rows of a real iteration (tile-sorted, PIN_TRAIN_DX when the decoder
+is frozen)."""
 import ctypes
 import os
 import sys
@@ -54,22 +55,28 @@ def main():
         mv = mlp_view(dec, packed=dx)
         fg = torch.zeros_like(nm.local_geo_features.data)
         res = {}
-        for tag, cert, tsp in (("full", nm.local_point_certainties, b.ts), ("no_ts", nm.local_point_certainties, None),
-                               ("no_side", None, None)):
-            st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
-                                    sdf=b.sdf.data_ptr(), certainties=cert.data_ptr() if cert is not None else None,
-                                    ts_update=nm.local_point_ts_update.data_ptr() if tsp is not None else None,
-                                    order=None, sorted_rows=b.rows4.data_ptr())
 
-            def fwd():
-                _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(b.rows), _lib.ptr(tsp),
-                          ctypes.byref(cfg), ctypes.byref(st), _lib.stream())
-            res[f"fwd_{tag}"] = timeit(fwd)
+        def state(side, cert=True, ts=True):
+            return _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
+                                      sdf=b.sdf.data_ptr(),
+                                      certainties=nm.local_point_certainties.data_ptr() if side and cert else None,
+                                      ts_update=nm.local_point_ts_update.data_ptr() if side and ts else None,
+                                      order=None, sorted_rows=b.rows4.data_ptr(),
+                                      row_ts=b.ts.data_ptr() if side and ts else None)
+        st = state(False)
 
-        def bwd():
-            _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(b.label), ctypes.byref(cfg),
-                      ctypes.byref(st), _lib.ptr(fg), None, _lib.ptr(b.workspace), _lib.ptr(b.loss), _lib.stream())
-        res["bwd"] = timeit(bwd)
+        def fwd():
+            _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(b.rows), _lib.ptr(b.ts),
+                      ctypes.byref(cfg), ctypes.byref(st), _lib.stream())
+        res["fwd"] = timeit(fwd)
+        for tag, sb in (("bwd", state(True)), ("bwd_cert_only", state(True, ts=False)),
+                        ("bwd_ts_only", state(True, cert=False)), ("bwd_no_side", state(False))):
+
+            def bwd():
+                _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(b.label), ctypes.byref(cfg),
+                          ctypes.byref(sb), _lib.ptr(fg), None, _lib.ptr(b.workspace), _lib.ptr(b.loss),
+                          _lib.stream())
+            res[tag] = timeit(bwd)
 
         def bwd_nofeat():
             _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(b.label), ctypes.byref(cfg),
