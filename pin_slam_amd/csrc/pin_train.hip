@@ -684,15 +684,25 @@ struct SideTable {
 __device__ __forceinline__ void train_side_effects(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
                                                    int nrow_blk, int64_t row, int* buf) {
     const SideTable tb(buf, st);
-    tb.init(c, st, nrow_blk, row);
-    __syncthreads();
     const int nn_k = c.nn_k;
-    const int npair = nrow_blk * nn_k;
+    const int npair = nrow_blk * nn_k;   // <= kBlock * kK: kK pairs per thread, held in registers
     const int* __restrict__ ids = st.ids + row0 * nn_k;
     const float* __restrict__ ws = st.weights + row0 * nn_k;
-    for (int e = threadIdx.x; e < npair; e += kBlock) tb.claim(ids[e]);
+    int pid[kK];
+    float pw[kK];
+#pragma unroll
+    for (int u = 0; u < kK; ++u) {
+        const int e = threadIdx.x + u * kBlock;
+        pid[u] = e < npair ? ids[e] : -1;
+        pw[u] = e < npair ? ws[e] : 0.f;
+    }
+    tb.init(c, st, nrow_blk, row);
     __syncthreads();
-    for (int e = threadIdx.x; e < npair; e += kBlock) tb.add(ids[e], ws[e], e / nn_k);
+#pragma unroll
+    for (int u = 0; u < kK; ++u) tb.claim(pid[u]);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kK; ++u) tb.add(pid[u], pw[u], (threadIdx.x + u * kBlock) / nn_k);
     __syncthreads();
     tb.flush();
 }
@@ -854,23 +864,19 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
 // and weights are staged in LDS first with coalesced loads, so the scatter loop issues its
 // atomics back to back instead of waiting on a load per element.
 // buf: (2 + EIK) kBlock kK ints of the block's LDS
-// se (optional, initialised, a barrier since): the training side effects ride on the scatter --
-// the staging pass claims the table slots, the scatter's d = 0 lane of each pair adds its weight.
 template <bool EIK>
 __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
                                                 int nrow_blk, const float* gst, const float* s_dsdf,
-                                                float* __restrict__ grad_features, int* buf, const SideTable* se) {
+                                                float* __restrict__ grad_features, int* buf) {
     int* const s_ids = buf;
     float* const s_wt = (float*)(buf + kBlock * kK);
     float* const s_al = (float*)(buf + 2 * kBlock * kK);
     const int nn_k = c.nn_k;
     const int npair = nrow_blk * nn_k;
     for (int e = threadIdx.x; e < npair; e += kBlock) {
-        const int id = st.ids[row0 * nn_k + e];
-        s_ids[e] = id;
+        s_ids[e] = st.ids[row0 * nn_k + e];
         s_wt[e] = st.weights[row0 * nn_k + e];
         if (EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
-        if (se) se->claim(id);
     }
     __syncthreads();
     const int total = npair * kF;
@@ -884,11 +890,6 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
         if (EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
         else g = s_wt[rj] * gst[lr * kF + d];
         atomicAdd(grad_features + (int64_t)id * kF + d, g);
-        if (se && d == 0) se->add(id, s_wt[rj], lr);
-    }
-    if (se) {
-        __syncthreads();
-        se->flush();
     }
 }
 
@@ -1098,33 +1099,25 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     __syncthreads();
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int nrow_blk = (int)(nrows - row0 < kBlock ? nrows - row0 : kBlock);
-    // LDS of the scatter's staging and of the side-effect table: buffers the kernel is done with
-    // where they fit (the block's scan lists after the per-neighbour matrix-core decodes, the
-    // decoder-gradient staging s_mg after mlp_grad_flush), else buffers of their own
+    // One LDS buffer for the scatter's staging and, after it, the side-effect table: a buffer the
+    // kernel is done with where one fits (the block's scan lists after the per-neighbour
+    // matrix-core decodes, the decoder-gradient staging s_mg after mlp_grad_flush), else its own.
+    // (A table of its own beside the staging, claimed in the staging pass, measured slower: the
+    // larger LDS footprint costs the atomic-bound scatter more occupancy than the reloads it saves.)
     constexpr int kScat = WF ? (EIK ? 3 : 2) * kBlock * kK : 0;
-    constexpr int kMg = kWaves * kMgWave;
-    constexpr bool kTabMg = MLP_GRAD && kScat + kSideBufInts <= kMg;
-    constexpr int kOwnScat = MLP_GRAD ? 0 : kScat;
-    constexpr int kOwnTab = (kDecode || kTabMg) ? 0 : kSideBufInts;
-    static_assert(!kDecode || kSideBufInts <= kBlock * kListSeg, "side-effect table must fit the scan lists");
-    static_assert(!MLP_GRAD || kScat <= kMg, "scatter staging must fit the decoder-gradient staging");
-    __shared__ int s_scat[kOwnScat > 0 ? kOwnScat : 1];
-    __shared__ int s_tab[kOwnTab > 0 ? kOwnTab : 1];
-    int* const s_pair = MLP_GRAD ? (int*)&s_mg[0][0] : s_scat;
-    int* const tab = kDecode ? block_list() : (kTabMg ? (int*)&s_mg[0][0] + kScat : s_tab);
-    const bool side = st.certainties || (st.ts_update && st.row_ts);
-    const SideTable se(tab, st);
+    constexpr int kNeed = kScat > kSideBufInts ? kScat : kSideBufInts;
+    constexpr int kOwn = (MLP_GRAD || kDecode) ? 0 : kNeed;
+    static_assert(!kDecode || kNeed <= kBlock * kListSeg, "scatter staging / side-effect table must fit the scan lists");
+    static_assert(!MLP_GRAD || kNeed <= kWaves * kMgWave, "scatter staging must fit the decoder-gradient staging");
+    __shared__ int s_own[kOwn > 0 ? kOwn : 1];
+    int* const s_pair = MLP_GRAD ? (int*)&s_mg[0][0] : (kDecode ? block_list() : s_own);
     if constexpr (WF) {
         if (grad_features) {
-            if (side) {
-                se.init(c, st, nrow_blk, row);
-                __syncthreads();
-            }
-            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, grad_features, s_pair, side ? &se : nullptr);
-            return;
+            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, grad_features, s_pair);
+            __syncthreads();   // the staging is read: the table takes the buffer
         }
     }
-    if (side) train_side_effects(c, st, row0, nrow_blk, row, tab);
+    if (st.certainties || (st.ts_update && st.row_ts)) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
 }
 
 __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ part, int64_t n,
