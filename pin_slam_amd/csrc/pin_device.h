@@ -860,7 +860,10 @@ __device__ __forceinline__ uint32_t mask_f16x2(float a, float b) {
 // Returns sdf; gx = the NOUT input gradients from input OFF on (GRAD); mask (may be NULL): the
 // lane's query's 64 ReLU masks, bit c = [pre_c > 0] (the decoder-parameter products of the
 // training backward).
-template <bool GRAD, int OFF, int NOUT>
+// NT: the query tile as the outer GEMM loop (fewer live VGPRs, the A tiles re-read from LDS per
+// tile): slower where the kernel fits its register budget anyway, faster where it would spill
+// (the weighted-first after-PGO query, compiled for 2 waves/SIMD: 97 -> 70 us per 262K step).
+template <bool GRAD, int OFF, int NOUT, bool NT = (PIN_MF_NT_OUTER != 0)>
 __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT],
                                                 uint64_t* mask = nullptr) {
     static_assert(OFF + NOUT <= kD, "decoder input range");
@@ -898,7 +901,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
     wave_lds_sync();
     // B operands of the four query tiles (lane group 3 reads lo-row halves; its A slots are 0)
     uint32_t mbits[4][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}, {0u, 0u}};   // ReLU masks: [query tile][hidden half]
-#if PIN_MF_NT_OUTER
+    if constexpr (NT) {
     // query tile outer: one tile's B operands, masks and GEMM2 accumulator live at a time (the A
     // tiles are re-read from LDS per tile); g of tile nt is written over its own, consumed B rows
 #pragma unroll
@@ -938,7 +941,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
         if (grp < 3) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc;
     }
     wave_lds_sync();
-#else
+    } else {
     f16x8 bh[4];
     f16x8 bl[4];   // x-lo rows: groups 2, 3 re-read group 1's slots (their A slots are 0)
 #pragma unroll
@@ -991,7 +994,7 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
         for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
     }
     wave_lds_sync();
-#endif
+    }
     if (mask) {
         // OR over the four lane groups (grp) holding a query's hidden rows; lane q = col + 16 grp
         // then holds query 16 nt + col's whole mask for every nt -- its own query at nt = grp

@@ -254,7 +254,7 @@ __device__ __forceinline__ void query_sdf_epilogue(const Src& src, const PinPoin
 #pragma unroll
         for (int d = 0; d < kD; ++d) { gx[d] = 0.01f * (float)(d + 1); sdf = fmaf(x[d], gx[d], sdf); }
 #else
-        if constexpr (MF) sdf = mlp_sdf_mfma16<GRAD, 0, kD>(m, x, gx);
+        if constexpr (MF) sdf = mlp_sdf_mfma16<GRAD, 0, kD, PGO>(m, x, gx);   // after PGO: tile-outer GEMM order
         else sdf = mlp_sdf<GRAD, 0, kD>(m, x, gx);
 #endif
         if (nn == 0 && zero_empty) sdf = 0.f;
@@ -401,6 +401,9 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
 #ifndef PIN_SDF_WAVES_NWF
 #define PIN_SDF_WAVES_NWF PIN_SDF_WAVES   // the same for per-neighbour decoding
 #endif
+#ifndef PIN_SDF_WAVES_PGO
+#define PIN_SDF_WAVES_PGO 2   // after pose-graph optimisation (quaternion-rotated neighbour vectors):
+#endif                        // 1 wave/SIMD at 256 VGPRs + 37 AGPRs before
 
 // q4 != NULL: the queries pre-sorted by pin_query_sort, {x, y, z, bits(original index)} each
 // (one coalesced 16-B load, no order -> coordinate dependency); otherwise q [n,3] processed in
@@ -408,7 +411,7 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
 // MF: decoder on the f16 matrix cores (mlp_sdf_mfma16, m.packed from pin_mlp_pack).
 template <bool WF, bool PGO, bool GRAD, bool FAT, bool MF>
 __global__ void __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(PGO ? 1 : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES_NWF))))
+__attribute__((amdgpu_waves_per_eu(PGO ? PIN_SDF_WAVES_PGO : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES_NWF))))
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q,
                  const float4* __restrict__ q4, int64_t n, int nn_k, int zero_empty, float* __restrict__ sdf_out,
                  float* __restrict__ grad_out, int* __restrict__ nn_out, float* __restrict__ cert_out,
