@@ -564,8 +564,10 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
 
 /* Workspace bytes of pin_train_backward for rows = n_main + 6 n_stencil. */
 static inline int64_t pin_train_workspace_bytes(int64_t rows) {
-    const int64_t nblk = (rows + 255) / 256;
-    return nblk * 4 * 8 + nblk * PIN_MLP_PART_FLOATS * 4;
+    /* a loss double per 64-row wave and a decoder-gradient partial per block, for blocks of
+       down to one wave (small batches run one-wave blocks) */
+    const int64_t nblk = (rows + 63) / 64;
+    return nblk * 8 + nblk * PIN_MLP_PART_FLOATS * 4;
 }
 
 /*

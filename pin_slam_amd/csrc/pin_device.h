@@ -27,7 +27,10 @@ constexpr int kF = PIN_FEATURE_DIM;      // feature_dim
 constexpr int kD = kF + 3;               // decoder input: feature + neighbour vector
 constexpr int kH = PIN_HIDDEN_DIM;       // geo_mlp_hidden_dim
 constexpr int kK = PIN_MAX_NN_K;         // top-k capacity
-constexpr int kBlock = 256;
+#ifndef PIN_BLOCK
+#define PIN_BLOCK 256
+#endif
+constexpr int kBlock = PIN_BLOCK;   // threads per block of the per-row kernels
 constexpr int kIdMask = PIN_RECORD_UNFAITHFUL - 1;
 constexpr int64_t kP0 = 73856093LL, kP1 = 19349669LL, kP2 = 83492791LL;  // neural_points.py:69
 constexpr float kInvalidDist2 = 9e3f;    // neural_points.py:561

@@ -21,7 +21,13 @@ using namespace pin;
 
 namespace {
 
-inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+#ifndef PIN_TRAIN_BLOCK
+#define PIN_TRAIN_BLOCK 256
+#endif
+constexpr int kTBlock = PIN_TRAIN_BLOCK;   // threads (rows) per block of the training kernels
+static_assert(kTBlock % 64 == 0 && kTBlock <= kBlock, "training blocks are whole waves, at most kBlock threads");
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kTBlock - 1) / kTBlock)); }
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline int launch_status() { return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP; }
 
@@ -204,13 +210,13 @@ __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainS
 }
 
 template <bool WF, bool MF>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
     const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
-    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    const int64_t t = xcd_block() * kTBlock + threadIdx.x;
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
@@ -220,17 +226,17 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
         const HashSource src(h, p);
         train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, t < rows);
     }
-    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw);
+    flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
 }
 
 template <bool WF, bool MF>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
     const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
-    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    const int64_t t = xcd_block() * kTBlock + threadIdx.x;
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
@@ -241,12 +247,12 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
         train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw,
                                                                      t < rows);
     }
-    flush_rows(c, st, xcd_block() * kBlock, rows, cid, cw);
+    flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
 }
 
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_rows(const float* __restrict__ coord, PinTrainCfg c, float* __restrict__ out) {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (r >= c.n_main + 6 * c.n_stencil) return;
     c.flags &= ~PIN_TRAIN_ROWS;
     row_coord(coord, c, r, out[3 * r], out[3 * r + 1], out[3 * r + 2]);
@@ -255,12 +261,12 @@ k_train_rows(const float* __restrict__ coord, PinTrainCfg c, float* __restrict__
 // one thread per batch row: the row, its label and ts gathered from the pool and, for every
 // decimation-th row, its six stencil rows pool[index[k*dec]] +- eps e_a (mapper.py:697-702) --
 // the pool is read once per batch row
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool, const int64_t* __restrict__ tpool,
                const float* __restrict__ wpool, int64_t pool_rows, const int64_t* __restrict__ index, PinTrainCfg c,
                float* __restrict__ rows, float* __restrict__ label, int64_t* __restrict__ ts,
                float* __restrict__ weight, int* __restrict__ error) {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (r >= c.n_main) return;
     int64_t i = index[r];
     if (i < 0 || i >= pool_rows) {   // never gather outside the pool: clamp and report
@@ -296,10 +302,10 @@ k_train_gather(const float* __restrict__ cpool, const float* __restrict__ lpool,
 // The sample pool as one 32-B record per sample, {x, y, z, label} {ts lo, ts hi, weight, 0}, so a
 // batch row costs ONE line gathered from a pool far larger than L2 instead of four (coordinates,
 // label, ts, weight live in separate tensors in the reference's layout).
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_pool_pack(const float* __restrict__ coord, const float* __restrict__ label, const int64_t* __restrict__ ts,
             const float* __restrict__ weight, int64_t n, float4* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (i >= n) return;
     const int64_t t = ts ? ts[i] : 0;
     out[2 * i] = make_float4(coord[3 * i], coord[3 * i + 1], coord[3 * i + 2], label[i]);
@@ -308,13 +314,13 @@ k_pool_pack(const float* __restrict__ coord, const float* __restrict__ label, co
 }
 
 // k_train_gather over the packed pool: the row's two 16-B halves of one 32-B record
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_gather_packed(const float4* __restrict__ pool, int64_t pool_rows, const int64_t* __restrict__ index,
                       int64_t n_index, const int64_t* __restrict__ new_idx, int64_t new_count,
                       const int64_t* __restrict__ index_new, PinTrainCfg c, float* __restrict__ rows,
                       float* __restrict__ label, int64_t* __restrict__ ts, float* __restrict__ weight,
                       int* __restrict__ error) {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (r >= c.n_main) return;
     int64_t i;
     if (r < n_index) {
@@ -587,12 +593,12 @@ template <bool WF, class Src>
 __device__ __forceinline__ void train_forward_eik_kernel_body(const Src& src, const PinPoints& p, const MlpW& mw,
                                                               const float* coord, const int64_t* ts, PinTrainCfg c,
                                                               PinTrainState st, bool mlp_trains) {
-    const int64_t t = xcd_block() * kBlock + threadIdx.x;
+    const int64_t t = xcd_block() * kTBlock + threadIdx.x;
     if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains);
 }
 
 template <bool WF>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_forward_eik_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                          const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st, int mlp_trains) {
     __shared__ float s_mlp[kWSize];
@@ -601,7 +607,7 @@ k_train_forward_eik_hash(const PinHash h, const PinPoints p, const PinMlp m, con
 }
 
 template <bool WF>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_forward_eik_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                          const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st, int mlp_trains) {
     __shared__ float s_mlp[kWSize];
@@ -621,13 +627,13 @@ k_train_forward_eik_grid(const PinGrid g, const PinPoints p, const PinMlp m, con
 //     differ in their low bits only.
 // In the forward, one atomic per (row, neighbour) pair scattered over the rows' neighbourhoods
 // cost ~115 us of the 1.68M-row iteration (the same atomics at contiguous addresses: ~17 us).
-constexpr int kCertSlots = 1024;
+constexpr int kCertSlots = 4 * kTBlock;   // 1,024 slots for the 256-row block's <= 2,048 pairs
 
 __device__ __forceinline__ void ts_amax(int64_t* __restrict__ ts_update, int id, int64_t q) {
     if (ts_update[id] < q) atomicMax((unsigned long long*)(ts_update + id), (unsigned long long)q);
 }
 
-constexpr int kSideBufInts = 3 * kCertSlots + 2 * kBlock;   // tag, val, ts per slot + the rows' int64 ts
+constexpr int kSideBufInts = 3 * kCertSlots + 2 * kTBlock;   // tag, val, ts per slot + the rows' int64 ts
 
 // The table in buf (kSideBufInts ints of the block's LDS): tag, weight sum and max ts per slot,
 // then the block's rows' ts.
@@ -646,7 +652,7 @@ struct SideTable {
     __device__ void init(const PinTrainCfg& c, const PinTrainState& st, int nrow_blk, int64_t row) const {
         const int tid = threadIdx.x;
         rts[tid] = (ts_update && tid < nrow_blk && row < c.n_main) ? st.row_ts[row] : -1;
-        for (int k = tid; k < kCertSlots; k += kBlock) {
+        for (int k = tid; k < kCertSlots; k += kTBlock) {
             tag[k] = -1;
             val[k] = 0.f;
             ts[k] = -1;
@@ -670,7 +676,7 @@ struct SideTable {
     }
     // after a barrier that follows every add: one memory-side atomic per occupied slot
     __device__ void flush() const {
-        for (int k = threadIdx.x; k < kCertSlots; k += kBlock) {
+        for (int k = threadIdx.x; k < kCertSlots; k += kTBlock) {
             const int id = tag[k];
             if (id < 0) continue;
             if (cert) atomicAdd(cert + id, val[k]);
@@ -685,14 +691,14 @@ __device__ __forceinline__ void train_side_effects(const PinTrainCfg& c, const P
                                                    int nrow_blk, int64_t row, int* buf) {
     const SideTable tb(buf, st);
     const int nn_k = c.nn_k;
-    const int npair = nrow_blk * nn_k;   // <= kBlock * kK: kK pairs per thread, held in registers
+    const int npair = nrow_blk * nn_k;   // <= kTBlock * kK: kK pairs per thread, held in registers
     const int* __restrict__ ids = st.ids + row0 * nn_k;
     const float* __restrict__ ws = st.weights + row0 * nn_k;
     int pid[kK];
     float pw[kK];
 #pragma unroll
     for (int u = 0; u < kK; ++u) {
-        const int e = threadIdx.x + u * kBlock;
+        const int e = threadIdx.x + u * kTBlock;
         pid[u] = e < npair ? ids[e] : -1;
         pw[u] = e < npair ? ws[e] : 0.f;
     }
@@ -702,7 +708,7 @@ __device__ __forceinline__ void train_side_effects(const PinTrainCfg& c, const P
     for (int u = 0; u < kK; ++u) tb.claim(pid[u]);
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kK; ++u) tb.add(pid[u], pw[u], (threadIdx.x + u * kBlock) / nn_k);
+    for (int u = 0; u < kK; ++u) tb.add(pid[u], pw[u], (threadIdx.x + u * kTBlock) / nn_k);
     __syncthreads();
     tb.flush();
 }
@@ -713,7 +719,7 @@ __device__ __forceinline__ void train_side_effects(const PinTrainCfg& c, const P
 // (mlp_grad_mfma) -> per-block partials (fixed order, no same-address atomics) ->
 // k_mlp_grad_final, which also turns the reduced products into dW1, db1, dW2, db2.
 constexpr int kMlpGrad = PIN_MLP_GRAD_SIZE;
-constexpr int kWaves = kBlock / 64;
+constexpr int kWaves = kTBlock / 64;
 constexpr int kTSize = kH * 16;                 // T[c][i], i < 16 (12 used)
 constexpr int kMlpPart = PIN_MLP_PART_FLOATS;   // per block: T, T' (analytic eikonal), sum so
 static_assert(kMlpPart >= 2 * kTSize + 1, "decoder-gradient partial layout");
@@ -826,7 +832,7 @@ __device__ __forceinline__ void mlp_grad_flush(float (*s_mg)[kMgWave], float* s_
     if (lane == 0) s_so[wave] = s;
     __syncthreads();
     constexpr int nval = EXTRA ? 2 * kTSize : kTSize;
-    for (int e = threadIdx.x; e < nval; e += kBlock) {
+    for (int e = threadIdx.x; e < nval; e += kTBlock) {
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v += s_mg[w][128 + e];
@@ -863,24 +869,24 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
 // pre-aggregation per block, and 64-B rows carrying the certainty, were slower).  The block's ids
 // and weights are staged in LDS first with coalesced loads, so the scatter loop issues its
 // atomics back to back instead of waiting on a load per element.
-// buf: (2 + EIK) kBlock kK ints of the block's LDS
+// buf: (2 + EIK) kTBlock kK ints of the block's LDS
 template <bool EIK>
 __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
                                                 int nrow_blk, const float* gst, const float* s_dsdf,
                                                 float* __restrict__ grad_features, int* buf) {
     int* const s_ids = buf;
-    float* const s_wt = (float*)(buf + kBlock * kK);
-    float* const s_al = (float*)(buf + 2 * kBlock * kK);
+    float* const s_wt = (float*)(buf + kTBlock * kK);
+    float* const s_al = (float*)(buf + 2 * kTBlock * kK);
     const int nn_k = c.nn_k;
     const int npair = nrow_blk * nn_k;
-    for (int e = threadIdx.x; e < npair; e += kBlock) {
+    for (int e = threadIdx.x; e < npair; e += kTBlock) {
         s_ids[e] = st.ids[row0 * nn_k + e];
         s_wt[e] = st.weights[row0 * nn_k + e];
         if (EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
     }
     __syncthreads();
     const int total = npair * kF;
-    for (int e = threadIdx.x; e < total; e += kBlock) {
+    for (int e = threadIdx.x; e < total; e += kTBlock) {
         const int d = e & (kF - 1);
         const int rj = e >> 3;
         const int id = s_ids[rj];
@@ -902,7 +908,7 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 // (A per-block LDS pre-sum of the scatter -- hash table on the feature row, 512 tile-sorted slots,
 // ~2.7 references per row -- measured slower: 683 vs 467 us, the LDS float atomics alone 470 us.)
 template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
                  double* __restrict__ loss_part) {
@@ -914,17 +920,17 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     // per-neighbour: each neighbour's rows are staged and scattered by their own wave inside the
     // neighbour loop (s_nwf: 64 rows x 8 floats + 64 ids per wave, no block barrier), so the block
     // does not hold all k x 8 floats per row (64 KB at k = 8: one wave per SIMD)
-    __shared__ float gst[WF ? kBlock * kF : 1];
+    __shared__ float gst[WF ? kTBlock * kF : 1];
     __shared__ float s_nwf[WF ? 1 : kWaves][WF ? 1 : 64 * kF + 64];
     __shared__ float s_mg[MLP_GRAD ? kWaves : 1][MLP_GRAD ? kMgWave : 1];
     __shared__ float s_so[kWaves];
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[kDecode || kRowDecode ? kPkBytes / 16 : 1];
-    __shared__ float s_dsdf[WF && EIK ? kBlock : 1];
+    __shared__ float s_dsdf[WF && EIK ? kTBlock : 1];
     MlpW mlpw;
     if constexpr (kRowDecode) {   // the decoder scratch is the wave's slice of s_mg (used in turn)
         const uint4* src = (const uint4*)m.packed;
-        for (int e = threadIdx.x; e < kPkBytes / 16; e += kBlock) s_pk[e] = src[e];
+        for (int e = threadIdx.x; e < kPkBytes / 16; e += kTBlock) s_pk[e] = src[e];
         __syncthreads();
         mlpw = MlpW{nullptr, m.sdf_scale, s_mg[threadIdx.x >> 6], (const unsigned char*)s_pk};
     } else {
@@ -932,7 +938,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                        : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
     }
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;   // processing slot (per-slot state)
+    const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
     // the row it holds (sdf, label)
     const int64_t row = !live ? r : st.sorted_rows ? (int64_t)__float_as_int(((const float4*)st.sorted_rows)[r].w)
@@ -1095,28 +1101,37 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
         }();
         if ((threadIdx.x & 63) == 0 && loss_part) loss_part[(int64_t)blockIdx.x * kWaves + wave] = v;
     }
+#if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 3   // profiling variant: decode (and loss) only
+    return;
+#endif
     if constexpr (MLP_GRAD) mlp_grad_flush<EIK>(s_mg, s_so, accT, accE, so_sum, mlp_part + (int64_t)blockIdx.x * kMlpPart);
     __syncthreads();
-    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int nrow_blk = (int)(nrows - row0 < kBlock ? nrows - row0 : kBlock);
+    const int64_t row0 = (int64_t)blockIdx.x * kTBlock;
+    const int nrow_blk = (int)(nrows - row0 < kTBlock ? nrows - row0 : kTBlock);
     // One LDS buffer for the scatter's staging and, after it, the side-effect table: a buffer the
     // kernel is done with where one fits (the block's scan lists after the per-neighbour
     // matrix-core decodes, the decoder-gradient staging s_mg after mlp_grad_flush), else its own.
     // (A table of its own beside the staging, claimed in the staging pass, measured slower: the
     // larger LDS footprint costs the atomic-bound scatter more occupancy than the reloads it saves.)
-    constexpr int kScat = WF ? (EIK ? 3 : 2) * kBlock * kK : 0;
+    constexpr int kScat = WF ? (EIK ? 3 : 2) * kTBlock * kK : 0;
     constexpr int kNeed = kScat > kSideBufInts ? kScat : kSideBufInts;
     constexpr int kOwn = (MLP_GRAD || kDecode) ? 0 : kNeed;
-    static_assert(!kDecode || kNeed <= kBlock * kListSeg, "scatter staging / side-effect table must fit the scan lists");
+    static_assert(!kDecode || kNeed <= kTBlock * kListSeg, "scatter staging / side-effect table must fit the scan lists");
     static_assert(!MLP_GRAD || kNeed <= kWaves * kMgWave, "scatter staging must fit the decoder-gradient staging");
     __shared__ int s_own[kOwn > 0 ? kOwn : 1];
     int* const s_pair = MLP_GRAD ? (int*)&s_mg[0][0] : (kDecode ? block_list() : s_own);
+#if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 2   // profiling variant: no feature scatter, no side effects
+    return;
+#endif
     if constexpr (WF) {
         if (grad_features) {
             feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, grad_features, s_pair);
             __syncthreads();   // the staging is read: the table takes the buffer
         }
     }
+#if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1   // profiling variant: no side effects
+    return;
+#endif
     if (st.certainties || (st.ts_update && st.row_ts)) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
 }
 
@@ -1141,7 +1156,7 @@ __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ 
 // dW2 = rowwise W1 . (T + s T')[:, 0:11] + b1 o T[:, 11]; block 0 also adds db2 = sum so.
 // Block kH / 4 (launched when loss_out is wanted) reduces the loss partials instead, so that a
 // training-decoder backward ends with one launch, not k_loss_final + this.
-__global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk, int extra,
+__global__ void __launch_bounds__(kTBlock) k_mlp_grad_final(const float* __restrict__ part, int64_t nblk, int extra,
                                                            PinMlp m, float* __restrict__ out,
                                                            const double* __restrict__ lpart, int64_t nl,
                                                            double* __restrict__ loss_out) {
@@ -1151,7 +1166,7 @@ __global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restri
     if (blockIdx.x == kH / 4) {   // the loss: fixed-order sum of the per-wave partials
         __shared__ double lred[kWaves];
         double v = 0.0;
-        for (int64_t k = threadIdx.x; k < nl; k += kBlock) v += lpart[k];
+        for (int64_t k = threadIdx.x; k < nl; k += kTBlock) v += lpart[k];
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (lane == 0) lred[wave] = v;
         __syncthreads();
@@ -1172,7 +1187,7 @@ __global__ void __launch_bounds__(kBlock) k_mlp_grad_final(const float* __restri
         if (extra) te += pb[kTSize + e];
     }
     if (blockIdx.x == 0) {
-        for (int64_t b = threadIdx.x; b < nblk; b += kBlock) b2 += part[b * kMlpPart + 2 * kTSize];
+        for (int64_t b = threadIdx.x; b < nblk; b += kTBlock) b2 += part[b * kMlpPart + 2 * kTSize];
         b2 = wave_sum_f(b2);
         if (lane == 0) s_b2[wave] = b2;
     }
@@ -1249,18 +1264,18 @@ __device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ p
     }
 }
 
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_adam(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, int64_t n,
        PinAdamStep a) {
-    adam_dense_body((int64_t)blockIdx.x * kBlock + threadIdx.x, prm, grad, m_, v_, n, a);
+    adam_dense_body((int64_t)blockIdx.x * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
 }
 
 // Adam on listed rows of a [rows, 8] parameter (the owned rows of a spatially sharded mapper):
 // one thread per (row, half row), the same arithmetic as k_adam; the rows' gradients are zeroed
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_adam_rows(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_,
             const int64_t* __restrict__ rows, int64_t nrows, PinAdamStep a) {
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t t = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (t >= 2 * nrows) return;
     const int64_t i0 = rows[t >> 1] * kF + 4 * (t & 1);
     float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + i0), m = *(float4*)(m_ + i0), v = *(float4*)(v_ + i0);
@@ -1300,19 +1315,19 @@ __device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg,
     if (a.zero_grad) grad[t] = 0.f;
 }
 
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_adam_segments(AdamSegs sg, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_, PinAdamStep a) {
-    adam_segment_body((int64_t)blockIdx.x * kBlock + threadIdx.x, sg, grad, m_, v_, a);
+    adam_segment_body((int64_t)blockIdx.x * kTBlock + threadIdx.x, sg, grad, m_, v_, a);
 }
 
 // The feature Adam and the decoder's segments in one launch (a training mapper iteration): the
 // first nb_dense blocks run k_adam's body, the rest k_adam_segments' (the same scalars).
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kTBlock)
 k_adam_step_segments(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_,
                      float* __restrict__ v_, int64_t n, int64_t nb_dense, AdamSegs sg, float* __restrict__ sgrad,
                      float* __restrict__ sm, float* __restrict__ sv, PinAdamStep a) {
-    if ((int64_t)blockIdx.x < nb_dense) adam_dense_body((int64_t)blockIdx.x * kBlock + threadIdx.x, prm, grad, m_, v_, n, a);
-    else adam_segment_body(((int64_t)blockIdx.x - nb_dense) * kBlock + threadIdx.x, sg, sgrad, sm, sv, a);
+    if ((int64_t)blockIdx.x < nb_dense) adam_dense_body((int64_t)blockIdx.x * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
+    else adam_segment_body(((int64_t)blockIdx.x - nb_dense) * kTBlock + threadIdx.x, sg, sgrad, sm, sv, a);
 }
 
 }  // namespace
@@ -1342,10 +1357,10 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
     AdamSegs sg;
     const int rc = adam_segs(params, sizes, nseg, sg);
     if (rc != PIN_OK) return rc;
-    const int64_t nb_dense = (n + 4 * kBlock - 1) / (4 * kBlock);
-    const int64_t nb_seg = (sg.off[nseg] + kBlock - 1) / kBlock;
+    const int64_t nb_dense = (n + 4 * kTBlock - 1) / (4 * kTBlock);
+    const int64_t nb_seg = (sg.off[nseg] + kTBlock - 1) / kTBlock;
     if (nb_dense + nb_seg == 0) return PIN_OK;
-    hipLaunchKernelGGL(k_adam_step_segments, dim3((unsigned)(nb_dense + nb_seg)), dim3(kBlock), 0, as_stream(stream),
+    hipLaunchKernelGGL(k_adam_step_segments, dim3((unsigned)(nb_dense + nb_seg)), dim3(kTBlock), 0, as_stream(stream),
                        param, grad, exp_avg, exp_avg_sq, n, nb_dense, sg, seg_grad, seg_exp_avg, seg_exp_avg_sq, *a);
     return launch_status();
 }
@@ -1358,7 +1373,7 @@ int pin_adam_segments(float* const* params, const int64_t* sizes, int nseg, floa
     const int rc = adam_segs(params, sizes, nseg, sg);
     if (rc != PIN_OK) return rc;
     if (sg.off[nseg] == 0) return PIN_OK;
-    hipLaunchKernelGGL(k_adam_segments, grid_for(sg.off[nseg]), dim3(kBlock), 0, as_stream(stream), sg, grad, exp_avg,
+    hipLaunchKernelGGL(k_adam_segments, grid_for(sg.off[nseg]), dim3(kTBlock), 0, as_stream(stream), sg, grad, exp_avg,
                        exp_avg_sq, *a);
     return launch_status();
 }
@@ -1369,7 +1384,7 @@ int pin_adam_rows(float* param, float* grad, float* exp_avg, float* exp_avg_sq, 
     if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
     if (nrows == 0) return PIN_OK;
     if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return PIN_ERR_ARG;
-    hipLaunchKernelGGL(k_adam_rows, grid_for(2 * nrows), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg,
+    hipLaunchKernelGGL(k_adam_rows, grid_for(2 * nrows), dim3(kTBlock), 0, as_stream(stream), param, grad, exp_avg,
                        exp_avg_sq, rows, nrows, *a);
     return launch_status();
 }
@@ -1379,7 +1394,7 @@ int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, 
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     if (!coord || !rows_out) return PIN_ERR_ARG;
-    hipLaunchKernelGGL(k_train_rows, grid_for(rows), dim3(kBlock), 0, as_stream(stream), coord, *cfg, rows_out);
+    hipLaunchKernelGGL(k_train_rows, grid_for(rows), dim3(kTBlock), 0, as_stream(stream), coord, *cfg, rows_out);
     return launch_status();
 }
 
@@ -1387,7 +1402,7 @@ int pin_pool_pack(const float* coord, const float* label, const int64_t* ts, con
                   float* packed, void* stream) {
     if (n < 0 || (n > 0 && (!coord || !label || !packed)) || ((uintptr_t)packed & 15)) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
-    hipLaunchKernelGGL(k_pool_pack, grid_for(n), dim3(kBlock), 0, as_stream(stream), coord, label, ts, weight, n,
+    hipLaunchKernelGGL(k_pool_pack, grid_for(n), dim3(kTBlock), 0, as_stream(stream), coord, label, ts, weight, n,
                        (float4*)packed);
     return launch_status();
 }
@@ -1407,7 +1422,7 @@ int pin_train_gather_packed(const float* packed_pool, int64_t pool_rows, const i
     const int rc = gather_packed_args(packed_pool, pool_rows, cfg, rows_out, label_out);
     if (rc != PIN_OK || cfg->n_main == 0) return rc;
     if (!index) return PIN_ERR_ARG;
-    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream),
+    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kTBlock), 0, as_stream(stream),
                        (const float4*)packed_pool, pool_rows, index, cfg->n_main, nullptr, (int64_t)0, nullptr, *cfg,
                        rows_out, label_out, ts_out, weight_out, (int*)error);
     return launch_status();
@@ -1422,7 +1437,7 @@ int pin_train_gather_packed_split(const float* packed_pool, int64_t pool_rows, c
     if (n_index > 0 && !index) return PIN_ERR_ARG;
     const int rc = gather_packed_args(packed_pool, pool_rows, cfg, rows_out, label_out);
     if (rc != PIN_OK || cfg->n_main == 0) return rc;
-    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream),
+    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kTBlock), 0, as_stream(stream),
                        (const float4*)packed_pool, pool_rows, index, n_index, new_idx, new_count, index_new, *cfg,
                        rows_out, label_out, ts_out, weight_out, (int*)error);
     return launch_status();
@@ -1439,7 +1454,7 @@ int pin_train_gather(const float* coord_pool, const float* label_pool, const int
     if (!coord_pool || !label_pool || !index || !rows_out || !label_out || (ts_pool && !ts_out) ||
         (weight_pool && !weight_out) || pool_rows < 1)
         return PIN_ERR_ARG;
-    hipLaunchKernelGGL(k_train_gather, grid_for(cfg->n_main), dim3(kBlock), 0, as_stream(stream), coord_pool,
+    hipLaunchKernelGGL(k_train_gather, grid_for(cfg->n_main), dim3(kTBlock), 0, as_stream(stream), coord_pool,
                        label_pool, ts_pool, weight_pool, pool_rows, index, *cfg, rows_out, label_out, ts_out,
                        weight_out, (int*)error);
     return launch_status();
@@ -1461,27 +1476,27 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     if (eik) {
         const bool wf = cfg->weighted_first != 0;
         if (grid) {
-            if (wf) hipLaunchKernelGGL(k_train_forward_eik_grid<true>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts,
+            if (wf) hipLaunchKernelGGL(k_train_forward_eik_grid<true>, grid_for(rows), dim3(kTBlock), 0, s, *grid, *pts,
                                        *mlp, coord, ts, *cfg, *st, 1);
-            else hipLaunchKernelGGL(k_train_forward_eik_grid<false>, grid_for(rows), dim3(kBlock), 0, s, *grid, *pts,
+            else hipLaunchKernelGGL(k_train_forward_eik_grid<false>, grid_for(rows), dim3(kTBlock), 0, s, *grid, *pts,
                                     *mlp, coord, ts, *cfg, *st, 1);
         } else {
-            if (wf) hipLaunchKernelGGL(k_train_forward_eik_hash<true>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts,
+            if (wf) hipLaunchKernelGGL(k_train_forward_eik_hash<true>, grid_for(rows), dim3(kTBlock), 0, s, *hash, *pts,
                                        *mlp, coord, ts, *cfg, *st, 1);
-            else hipLaunchKernelGGL(k_train_forward_eik_hash<false>, grid_for(rows), dim3(kBlock), 0, s, *hash, *pts,
+            else hipLaunchKernelGGL(k_train_forward_eik_hash<false>, grid_for(rows), dim3(kTBlock), 0, s, *hash, *pts,
                                     *mlp, coord, ts, *cfg, *st, 1);
         }
         return launch_status();
     }
 #define PIN_LAUNCH_FWD(KERNEL, SRC)                                                                             \
     do {                                                                                                        \
-        if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp, \
+        if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp, \
                                    coord, ts, *cfg, *st);                                                       \
         else if (cfg->weighted_first)                                                                           \
-            hipLaunchKernelGGL((KERNEL<true, false>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp,     \
+            hipLaunchKernelGGL((KERNEL<true, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,     \
                                coord, ts, *cfg, *st);                                                           \
         else                                                                                                    \
-            hipLaunchKernelGGL((KERNEL<false, false>), grid_for(rows), dim3(kBlock), 0, s, *SRC, *pts, *mlp,    \
+            hipLaunchKernelGGL((KERNEL<false, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,    \
                                coord, ts, *cfg, *st);                                                           \
     } while (0)
     if (grid) PIN_LAUNCH_FWD(k_train_forward_grid, grid);
@@ -1505,10 +1520,10 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     float* mpart = mlp_grad ? (float*)((char*)workspace + nblk * kWaves * sizeof(double)) : nullptr;
     const int extra = (cfg->flags & PIN_TRAIN_EIK) ? 1 : 0;
 #define PIN_LAUNCH_BWD(WF, MG)                                                                               \
-    hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
+    hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
 #define PIN_LAUNCH_BWD_EIK(WF, MG, MF)                                                                                 \
-    hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
+    hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
     if (cfg->flags & PIN_TRAIN_EIK) {
         if ((cfg->flags & PIN_TRAIN_DX) || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec) return PIN_ERR_ARG;
@@ -1521,25 +1536,25 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         }
     } else if (cfg->flags & PIN_TRAIN_DX) {
         if (mlp_grad || !cfg->weighted_first) return PIN_ERR_UNSUPPORTED;
-        hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg, *st,
+        hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st,
                            grad_features, mpart, lpart);
     } else if (cfg->weighted_first) {
         if (mlp_grad && mlp->packed)   // a training decoder decoded on the matrix cores
-            hipLaunchKernelGGL((k_train_backward<true, true, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg,
+            hipLaunchKernelGGL((k_train_backward<true, true, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
                                *st, grad_features, mpart, lpart);
         else if (mlp_grad) PIN_LAUNCH_BWD(true, true);
         else PIN_LAUNCH_BWD(true, false);
     } else {
         if (mlp_grad) PIN_LAUNCH_BWD(false, true);
         else if (mlp->packed)
-            hipLaunchKernelGGL((k_train_backward<false, false, true>), g, dim3(kBlock), 0, s, *pts, *mlp, label, *cfg,
+            hipLaunchKernelGGL((k_train_backward<false, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
                                *st, grad_features, mpart, lpart);
         else PIN_LAUNCH_BWD(false, false);
     }
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
     if (mlp_grad)   // decoder gradients (+ the loss in one more block)
-        hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4 + (loss_out ? 1 : 0)), dim3(kBlock), 0, s, mpart, nblk, extra,
+        hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4 + (loss_out ? 1 : 0)), dim3(kTBlock), 0, s, mpart, nblk, extra,
                            *mlp, mlp_grad, lpart, nblk * kWaves, loss_out);
     else if (loss_out)
         hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(1024), 0, s, lpart, nblk * kWaves, loss_out);
@@ -1552,7 +1567,7 @@ int pin_adam_step(float* param, float* grad, float* exp_avg, float* exp_avg_sq, 
     if (a->grad_stride != 8 && (a->grad_stride < 8 || n % 8)) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
     if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) return PIN_ERR_ARG;
-    hipLaunchKernelGGL(k_adam, grid_for((n + 3) / 4), dim3(kBlock), 0, as_stream(stream), param, grad, exp_avg,
+    hipLaunchKernelGGL(k_adam, grid_for((n + 3) / 4), dim3(kTBlock), 0, as_stream(stream), param, grad, exp_avg,
                        exp_avg_sq, n, *a);
     return launch_status();
 }

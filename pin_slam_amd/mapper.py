@@ -85,8 +85,10 @@ class _TrainBuffers:
             self.rows4 = torch.empty((rows, 4), dtype=torch.float32, device=device)
             self.label = torch.empty((rows,), dtype=torch.float32, device=device)
             self.ts = torch.empty((rows,), dtype=torch.int64, device=device)
-            nblk = (rows + 255) // 256
-            self.workspace = torch.empty((nblk * 4 * 8 + nblk * _lib.MLP_PART_FLOATS * 4,), dtype=torch.uint8,
+            # pin_train_backward's partials: a loss double per wave and a decoder-gradient partial
+            # per block, sized for the smallest training block (one wave)
+            nblk = (rows + 63) // 64
+            self.workspace = torch.empty((nblk * 8 + nblk * _lib.MLP_PART_FLOATS * 4,), dtype=torch.uint8,
                                          device=device)
             self.loss = torch.zeros((1,), dtype=torch.float64, device=device)
             self.wrow = torch.empty((rows,), dtype=torch.float32, device=device)
