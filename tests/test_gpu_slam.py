@@ -130,6 +130,7 @@ def test_slam_sequence_matches_reference(golden, dev):
         dt, dr = _pose_err(loop.cur_pose_ref, z["hist_pose"][k])
         dt_true, _ = _pose_err(loop.cur_pose_ref, z["truth_poses"][k])
         report.append((k, round(dt, 4), round(dr, 4), round(dt_true, 4), counts, want))
+        print("frame", *report[-1], flush=True)
         # the reference's own 1- vs 8-thread runs differ by up to 3.3 cm by frame 13 and re-converge
         # and diverge again afterwards: the spread up to frame k bounds how far two legitimate runs
         # may be apart at frame k
@@ -139,8 +140,14 @@ def test_slam_sequence_matches_reference(golden, dev):
         # the reference itself drifts from the truth over the 30 frames (6-7 cm by frame 29)
         ref_true, _ = _pose_err(z["hist_pose"][k], z["truth_poses"][k])
         assert dt_true <= max(0.05, ref_true + tol_t), f"frame {k}: pose {dt_true:.4f} m from the ground truth"
+        filt = k % int(cfg.pool_filter_freq) == int(cfg.pool_filter_freq) - 1   # the pool's window filter ran
         for name, g, w, rel in zip(("map_count", "local_count", "pool", "new"), counts, want, (0.01, 0.01, 0.001, 0.15)):
             rel = max(rel, 3 * float(z[f"spread_rel_{name}"][k]))
+            if name == "pool" and filt:
+                # the filter drops every sample beyond the window radius of the CURRENT position: the
+                # samples near that sphere move in or out with the pose, ~0.025 % of the pool per cm at
+                # frame 29 (the dense early frames lie on the sphere); 0.05 % per cm of pose difference
+                rel = max(rel, 0.0005 * 100.0 * dt)
             assert _within(g, w, rel), f"frame {k}: {name} {g} vs reference {w}"
         if k == 0:
             _surface_check(nm, dec, z, dev, "f0_surface_probes", "f0_surface_sdf")
