@@ -36,6 +36,8 @@ from .sharding import all_reduce
 # weighted_first with a training decoder: decode each row in the backward on the matrix cores
 # (PIN_TRAIN_ROW_DECODE=0: the f32 VALU decoder backward, for A/B runs)
 _ROW_DECODE = os.environ.get("PIN_TRAIN_ROW_DECODE", "1") != "0"
+# training batches from this many rows (batch + stencil) up are tile-sorted before the forward
+_TRAIN_TILE_MIN = int(os.environ.get("PIN_TRAIN_TILE_MIN", str(_TILE_MIN)))
 # the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
 _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 
@@ -675,7 +677,7 @@ class Mapper:
         cfg.flags = _lib.PIN_TRAIN_ROWS
         q = rows_xyz
         sorted_rows = None
-        if grid and _TILE_QUERIES and rows >= _TILE_MIN:
+        if grid and _TILE_QUERIES and rows >= _TRAIN_TILE_MIN:
             # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates)
             sorted_rows = query_sort(gv, rows_xyz, out=b.rows4)
         self._order = sorted_rows
@@ -722,7 +724,15 @@ class Mapper:
         self._adam_t = (getattr(self, "_adam_t", 0) + 1) if step is None else step
         st = adam_scalars(c.lr, self._adam_t, c.adam_eps)
         s = _lib.stream()
-        segs = self._adam_segments(mlp_params, m_grad) if m_grad is not None else None
+        segs = None
+        if m_grad is not None:
+            # the pointer / size arrays cached on the parameters' storage
+            skey = (tuple(p.data.data_ptr() for p in mlp_params), m_grad.numel())
+            hit = self.__dict__.get("_adam_segs")
+            if hit is None or hit[0] != skey:
+                hit = (skey, self._adam_segments(mlp_params, m_grad))
+                self._adam_segs = hit
+            segs = hit[1]
         if partition is None and segs is not None:
             # the features and the decoder's four tensors in one launch (same scalars)
             _lib.call("pin_adam_step_segments", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),

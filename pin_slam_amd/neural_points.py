@@ -130,6 +130,16 @@ def hash_slots(points: torch.Tensor, resolution: float, buffer_size: int) -> tor
     return torch.remainder(h, int(buffer_size))
 
 
+def _view_key(t):
+    """View-cache key of a tensor the raw-pointer views read: identity and storage, plus the
+    version when the view holds a converted copy instead of the tensor itself."""
+    if t is None:
+        return None
+    d = t.data if isinstance(t, nn.Parameter) else t
+    inplace = d.dtype == torch.float32 and d.is_contiguous()
+    return (id(t), d.data_ptr(), None if inplace else d._version)
+
+
 class NeuralPoints(nn.Module):
 
     def __init__(self, config) -> None:
@@ -772,29 +782,31 @@ class NeuralPoints(nn.Module):
     # ------------------------------------------------------------------ queries
     def _views(self, mode: str, query_locally: bool):
         """(PinHash view, PinPoints view) of a query mode, reused while every tensor they are built
-        from is unchanged (tensor_key) -- a query call then costs no view rebuild."""
+        from is the same (see the key below) -- a query call then costs no view rebuild."""
         rec = self.records(mode)
         if query_locally:
             src = (self.local_geo_features, self.local_neural_points, self.local_point_orientations,
                    self.local_point_certainties)
         else:
             src = (self.geo_features, self.neural_points, self.point_orientations, self.point_certainties)
-        key = (mode, bool(query_locally), bool(self.after_pgo), tensor_key((rec, self.buffer_pt_index) + src),
-               float(self.resolution), int(self.buffer_size), int(self.neighbor_K), float(self.max_valid_dist2),
-               id(self._cells))
-        hit = self.__dict__.setdefault("_view_cache", {}).get((mode, bool(query_locally)))
-        if hit is not None and hit[0] == key:
-            return hit[1]
-        hv = hash_view(self)
-        f = src[0].data if isinstance(src[0], nn.Parameter) else src[0]
         # the local map's positions also as 16-B rows: the training forward (mapping, local rows)
-        # reads every neighbour's position by id beside its feature rows
-        # (cached on the positions alone: the view itself is rebuilt whenever the features move)
+        # reads every neighbour's position by id beside its feature rows (cached on the positions)
         p4 = None
         if query_locally and src[1] is not None and src[1].shape[0] > 0:
             pos = src[1]
             p4 = self._cached("positions4_local", (pos,), (),
                               lambda: torch.nn.functional.pad(pos.detach().to(torch.float32), (0, 1)).contiguous())
+        # the views hold raw pointers: a tensor the kernels read in place keys the view by identity
+        # and storage only (its content may change -- Adam writes the features every iteration
+        # -- without a rebuild); one the view copies (not f32-contiguous) by its version too
+        key = (mode, bool(query_locally), bool(self.after_pgo), tensor_key((rec, self.buffer_pt_index)),
+               tuple(_view_key(t) for t in src), id(p4), float(self.resolution), int(self.buffer_size),
+               int(self.neighbor_K), float(self.max_valid_dist2), id(self._cells))
+        hit = self.__dict__.setdefault("_view_cache", {}).get((mode, bool(query_locally)))
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        hv = hash_view(self)
+        f = src[0].data if isinstance(src[0], nn.Parameter) else src[0]
         pv = points_view(rec, f, src[1], src[2], src[3], self.after_pgo, positions4=p4)
         # the key is taken after hash_view, which may build the cell table
         key = key[:-1] + (id(self._cells),)

@@ -89,7 +89,14 @@ def mlp_view(decoder, packed=False) -> _View:
     else:
         v = _mlp_view(decoder)
     if packed and _MLP_PACK and not v.struct.packed:
-        buf = torch.empty(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=v.keep[0].device)
+        # one operand image per decoder, rewritten in stream order when the parameters change (a
+        # training decoder's view is rebuilt every iteration; an older view reads the same
+        # parameters in place, so it stays consistent with the image)
+        buf = decoder.__dict__.get("_pin_mlp_pack_buf") if ps is not None else None
+        if buf is None or buf.device != v.keep[0].device:
+            buf = torch.empty(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=v.keep[0].device)
+            if ps is not None:
+                decoder.__dict__["_pin_mlp_pack_buf"] = buf
         _lib.call("pin_mlp_pack", v.ref(), _lib.ptr(buf), _lib.stream(buf.device))
         v.struct.packed = buf.data_ptr()
         v.keep = v.keep + (buf,)
