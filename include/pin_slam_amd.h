@@ -491,6 +491,14 @@ typedef struct PinTrainState {
                                     the decoder trains); per-neighbour: [rows, 3] u */
     const int64_t* row_ts;       /* [n_main] the batch rows' ts (the `ts` of pin_train_forward), read by
                                     pin_train_backward for the ts_update side effect; NULL: none */
+    float* grad_replicas;        /* optional, with replicas > 1: [replicas, L+1, 8] f32 scratch, zero on the
+                                    first call; pin_train_backward scatters block b's feature terms into
+                                    replica b % replicas, then adds the replicas into grad_features and
+                                    zeroes them again.  For small batches on small maps, whose most
+                                    referenced points serialise the memory-side float atomics on one
+                                    address line; NULL / replicas <= 1: straight into grad_features */
+    int32_t replicas;
+    int32_t reserved_r;          /* 0 */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */

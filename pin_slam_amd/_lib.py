@@ -94,7 +94,8 @@ class PinTrainCfg(ctypes.Structure):
 class PinTrainState(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
                 ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p), ("sorted_rows", c_void_p),
-                ("row_weight", c_void_p), ("eik_coef", c_void_p), ("eik_vec", c_void_p), ("row_ts", c_void_p)]
+                ("row_weight", c_void_p), ("eik_coef", c_void_p), ("eik_vec", c_void_p), ("row_ts", c_void_p),
+                ("grad_replicas", c_void_p), ("replicas", i32), ("reserved_r", i32)]
 
 
 class PinAdamStep(ctypes.Structure):

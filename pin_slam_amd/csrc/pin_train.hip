@@ -873,7 +873,7 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
 template <bool EIK>
 __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
                                                 int nrow_blk, const float* gst, const float* s_dsdf,
-                                                float* __restrict__ grad_features, int* buf) {
+                                                float* __restrict__ grad_features, int* buf, int64_t frows = 1) {
     int* const s_ids = buf;
     float* const s_wt = (float*)(buf + kTBlock * kK);
     float* const s_al = (float*)(buf + 2 * kTBlock * kK);
@@ -889,7 +889,13 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
     for (int e = threadIdx.x; e < total; e += kTBlock) {
         const int d = e & (kF - 1);
         const int rj = e >> 3;
+#if defined(PIN_EXP_SCAT2) && PIN_EXP_SCAT2 == 1   // timing variant: contiguous rows (wrong sums)
+        const int id = s_ids[rj] < 0 ? -1 : (int)((row0 * nn_k + rj) % frows);
+#elif defined(PIN_EXP_SCAT2) && PIN_EXP_SCAT2 == 2   // timing variant: the block's pairs onto one point (wrong sums)
+        const int id = s_ids[rj] < 0 ? -1 : (int)(blockIdx.x % frows);
+#else
         const int id = s_ids[rj];
+#endif
         if (id < 0) continue;
         const int lr = rj / nn_k;
         float g;
@@ -938,6 +944,11 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                        : MF ? MlpW{nullptr, m.sdf_scale, nullptr} : stage_mlp(m, s_mlp);
     }
     const int64_t nrows = c.n_main + 6 * c.n_stencil;
+    // the feature terms' destination: grad_features, or this block's replica of it (small batches:
+    // the popular points' address lines take 1/replicas of the memory-side atomics each)
+    float* const gdst = (grad_features && st.grad_replicas && st.replicas > 1)
+                            ? st.grad_replicas + (int64_t)(blockIdx.x % st.replicas) * p.rows * kF
+                            : grad_features;
     const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
     // the row it holds (sdf, label)
@@ -1082,13 +1093,13 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                 wave_lds_sync();   // the previous neighbour's scatter has read the slots
 #pragma unroll
                 for (int d = 0; d < kF; ++d) wg[lane * kF + d] = gf[d];
-                wid[lane] = ok && grad_features ? id : -1;
+                wid[lane] = ok && gdst ? id : -1;
                 wave_lds_sync();
 #pragma unroll
                 for (int u = 0; u < kF; ++u) {
                     const int e = u * 64 + lane;
                     const int rid = wid[e >> 3];
-                    if (rid >= 0) atomicAdd(grad_features + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
+                    if (rid >= 0) atomicAdd(gdst + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
                 }
             }
         }
@@ -1125,7 +1136,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
 #endif
     if constexpr (WF) {
         if (grad_features) {
-            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, grad_features, s_pair);
+            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, s_pair, p.rows);
             __syncthreads();   // the staging is read: the table takes the buffer
         }
     }
@@ -1133,6 +1144,24 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     return;
 #endif
     if (st.certainties || (st.ts_update && st.row_ts)) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
+}
+
+// grad += sum of the replicas, which are zeroed again (pin_train_backward with st.replicas > 1):
+// n4 float4 per replica, read once, coalesced
+__global__ void __launch_bounds__(kTBlock)
+k_replica_reduce(float4* __restrict__ rep, int nrep, int64_t n4, float4* __restrict__ grad) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t e = (int64_t)blockIdx.x * kTBlock + threadIdx.x; e < n4; e += (int64_t)gridDim.x * kTBlock) {
+        float4 a = z;
+        for (int k = 0; k < nrep; ++k) {
+            const float4 v = rep[k * n4 + e];
+            rep[k * n4 + e] = z;
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        float4 g = grad[e];
+        g.x += a.x; g.y += a.y; g.z += a.z; g.w += a.w;
+        grad[e] = g;
+    }
 }
 
 __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ part, int64_t n,
@@ -1553,6 +1582,12 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     }
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
+    if (grad_features && st->grad_replicas && st->replicas > 1) {
+        const int64_t n4 = pts->rows * kF / 4;
+        const int64_t nb = (n4 + kTBlock - 1) / kTBlock;
+        hipLaunchKernelGGL(k_replica_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, s,
+                           (float4*)st->grad_replicas, st->replicas, n4, (float4*)grad_features);
+    }
     if (mlp_grad)   // decoder gradients (+ the loss in one more block)
         hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4 + (loss_out ? 1 : 0)), dim3(kTBlock), 0, s, mpart, nblk, extra,
                            *mlp, mlp_grad, lpart, nblk * kWaves, loss_out);

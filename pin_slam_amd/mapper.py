@@ -38,6 +38,11 @@ from .sharding import all_reduce
 _ROW_DECODE = os.environ.get("PIN_TRAIN_ROW_DECODE", "1") != "0"
 # training batches from this many rows (batch + stencil) up are tile-sorted before the forward
 _TRAIN_TILE_MIN = int(os.environ.get("PIN_TRAIN_TILE_MIN", str(_TILE_MIN)))
+# batches below this many rows (batch + stencil) scatter their feature terms into this many replicas
+# of the gradient, summed after the backward: a SLAM frame's 26K rows put up to ~65 (row, neighbour)
+# pairs on one point, whose memory-side float atomics serialise on its address line
+_REPLICA_ROWS = int(os.environ.get("PIN_TRAIN_REPLICA_ROWS", str(1 << 18)))
+_REPLICAS = int(os.environ.get("PIN_TRAIN_REPLICAS", "8"))
 # the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
 _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 
@@ -74,6 +79,14 @@ class _TrainBuffers:
             self.eik_vec = torch.empty((rows, 20 if wf else 4), dtype=torch.float32, device=dev)
             self._eik_key = key
         return self.eik_coef, self.eik_vec
+
+    def replicas(self, n_floats, device):
+        """Zeroed scratch of n_floats for PinTrainState.grad_replicas (pin_train_backward re-zeroes
+        it after every use; grown, never shrunk)."""
+        buf = getattr(self, "grad_replicas", None)
+        if buf is None or buf.numel() < n_floats or buf.device != torch.device(device):
+            self.grad_replicas = buf = torch.zeros((max(n_floats, 1 << 16),), dtype=torch.float32, device=device)
+        return buf
 
     def get(self, rows, nn_k, wf, device):
         key = (rows, nn_k, wf, str(device))
@@ -686,6 +699,10 @@ class Mapper:
                                 ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
                                 order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None,
                                 row_weight=_lib.ptr(wrow), row_ts=_lib.ptr(ts64))
+        if (grad_features is not None and rows < _REPLICA_ROWS and _REPLICAS > 1
+                and grad_features.shape[0] == pv.features.shape[0]):
+            rep = b.replicas(_REPLICAS * grad_features.numel(), q.device)
+            st.grad_replicas, st.replicas = rep.data_ptr(), _REPLICAS
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK and not analytic

@@ -39,7 +39,26 @@ def main(frames=12):
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t0)
     print("mapping(15) wall ms:", [round(w * 1e3, 3) for w in walls])
-    # host-side only: the same call with the GPU work already queued behind a long sleep kernel
+    # host-side only: the calls queued behind a long sleep kernel (the GPU never waits on the host)
+    def host_ms(fn, reps=3):
+        best = 1e9
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            torch.cuda._sleep(200_000_000)
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+            torch.cuda.synchronize()
+        return best * 1e3
+    print(f"host only: mapping(15) {host_ms(lambda: mapper.mapping(15)):.3f} ms")
+    idx = mapper._batch_parts
+    print(f"host only: 15 x _batch_parts {host_ms(lambda: [idx() for _ in range(15)]):.3f} ms")
+    print(f"host only: 15 x torch.randint pair {host_ms(lambda: [(torch.randint(0, 1000, (16384,), device=dev), torch.randint(0, 100, (100,), device=dev)) for _ in range(15)]):.3f} ms")
+    nm.mark_modified(nm.local_geo_features)
+    print(f"host only: 15 x _views {host_ms(lambda: [nm._views('local', True) for _ in range(15)]):.3f} ms")
+    from pin_slam_amd.query import mlp_view
+    print(f"host only: 15 x mlp_view(packed) after a decoder step "
+          f"{host_ms(lambda: [(torch.autograd.graph.increment_version(dec.lout.bias), mlp_view(dec, packed=True)) for _ in range(15)]):.3f} ms")
     pr = cProfile.Profile()
     torch.cuda.synchronize()
     pr.enable()
