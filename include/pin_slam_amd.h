@@ -498,7 +498,9 @@ typedef struct PinTrainState {
                                     referenced points serialise the memory-side float atomics on one
                                     address line; NULL / replicas <= 1: straight into grad_features */
     int32_t replicas;
-    int32_t reserved_r;          /* 0 */
+    int32_t replica_mode;        /* 0: pin_train_backward adds the replicas into grad_features itself;
+                                    1: it leaves them, and the caller's pin_adam_step_train takes the
+                                    gradient as grad_features + the replicas' sum (one launch less) */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */
@@ -601,6 +603,18 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
                            float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
                            float* seg_exp_avg_sq, const PinAdamStep* a, void* stream);
 
+/*
+ * pin_adam_step_train -- one mapper iteration's optimiser step in one launch: the feature step of
+ * pin_adam_step (n floats) and, with nseg > 0, the decoder step of pin_adam_segments (whose
+ * tensors one block steps).  grad_replicas (replicas > 1, PinTrainState.replica_mode 1): the
+ * features' gradient is grad + the sum of the [replicas, n] replicas, which are zeroed again.
+ * mlp / packed (non-NULL, nseg > 0): the same block then writes the stepped decoder's
+ * pin_mlp_pack image (no pin_mlp_pack call before the next forward).  grad_stride must be 8.
+ */
+int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                        float* grad_replicas, int32_t replicas, float* const* params, const int64_t* sizes,
+                        int nseg, float* seg_grad, float* seg_exp_avg, float* seg_exp_avg_sq, const PinMlp* mlp,
+                        void* packed, const PinAdamStep* a, void* stream);
 /* pin_adam_segments -- the same Adam update over nseg (<= 8) separate parameter tensors params[k]
  * of sizes[k] floats whose gradients and moments lie end to end in contiguous grad / exp_avg /
  * exp_avg_sq (the decoder's W1, b1, W2, b2 against pin_train_backward's mlp_grad): one launch

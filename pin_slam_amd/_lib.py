@@ -95,7 +95,7 @@ class PinTrainState(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
                 ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p), ("sorted_rows", c_void_p),
                 ("row_weight", c_void_p), ("eik_coef", c_void_p), ("eik_vec", c_void_p), ("row_ts", c_void_p),
-                ("grad_replicas", c_void_p), ("replicas", i32), ("reserved_r", i32)]
+                ("grad_replicas", c_void_p), ("replicas", i32), ("replica_mode", i32)]
 
 
 class PinAdamStep(ctypes.Structure):
@@ -178,6 +178,8 @@ _SIGS = {
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_adam_rows": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
+    "pin_adam_step_train": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, i32, _P(c_void_p), _P(i64), i32,
+                            c_void_p, c_void_p, c_void_p, _P(PinMlp), c_void_p, _P(PinAdamStep), c_void_p],
     "pin_adam_segments": [_P(c_void_p), _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
     "pin_adam_step_segments": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(c_void_p), _P(i64), i32, c_void_p,
                                c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
@@ -222,6 +224,16 @@ def load():
 
 def call(name, *args):
     rc = getattr(load(), name)(*args)
+    if rc != PIN_OK:
+        raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)}")
+
+
+def fn(name):
+    """The bound entry point itself (hot loops: call it and pass its status to check)."""
+    return getattr(load(), name)
+
+
+def check(name, rc):
     if rc != PIN_OK:
         raise RuntimeError(f"{name} failed: {_ERRORS.get(rc, rc)}")
 

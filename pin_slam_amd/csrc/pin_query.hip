@@ -1017,64 +1017,8 @@ static bool grid_ok(const PinGrid* g) {
 }
 
 // ------------------------------------------------------------------ decoder pack (pin_mlp_pack)
-// power of two taking max|row| to [2^13, 2^14) (any power for an all-zero row)
-__device__ __forceinline__ float row_scale(float mx) {
-    const int eb = (__float_as_int(mx) >> 23) & 0xff;
-    const int e = min(max(140 - eb, -100), 100);
-    return __int_as_float((e + 127) << 23);
-}
-
-__device__ __forceinline__ void split_f16(float v, int part, _Float16* out) {
-    const _Float16 h = (_Float16)v;
-    *out = part == 0 ? h : (_Float16)(v - (float)h);
-}
-
 __global__ void __launch_bounds__(256) k_mlp_pack(const PinMlp m, unsigned char* __restrict__ out) {
-    __shared__ float s_e1[kH];          // GEMM1 row scales 2^e_c
-    __shared__ float s_f[16];           // GEMM2 row scales 2^f_i
-    __shared__ float s_a2[12][kH];      // GEMM2 rows: W1[c][i] w2[c] (i < 11), w2[c] b1[c] (i = 11)
-    const int t = threadIdx.x;
-    if (t < kH) {
-        float mx = fabsf(m.b1[t]);
-        for (int i = 0; i < kD; ++i) mx = fmaxf(mx, fabsf(m.W1[t * kD + i]));
-        s_e1[t] = row_scale(mx);
-    }
-    for (int e = t; e < 12 * kH; e += 256) {
-        const int i = e / kH, c = e - i * kH;
-        s_a2[i][c] = i < kD ? m.W1[c * kD + i] * m.W2[c] : m.W2[c] * m.b1[c];
-    }
-    __syncthreads();
-    if (t < 16) {
-        float mx = 0.f;
-        if (t < 12)
-            for (int c = 0; c < kH; ++c) mx = fmaxf(mx, fabsf(s_a2[t][c]));
-        const float f = row_scale(mx);
-        s_f[t] = f;
-        ((float*)(out + kPkScale))[t] = 1.f / f;   // exact: a power of two
-    }
-    if (t == 0) *(float*)(out + kPkB2) = m.b2[0];
-    __syncthreads();
-    // GEMM1 A: row c = 16 mt + lane % 16, K-slot k = 8 (lane / 16) + s:
-    //   k < 11 W1 hi, k < 22 W1[k-11] lo, 22 b1 hi, 23 b1 lo, else 0 (B: x hi, x hi, E, E, -)
-    for (int e = t; e < 4 * 64 * 8; e += 256) {
-        const int mt = e >> 9, lane = (e >> 3) & 63, k = 8 * (lane >> 4) + (e & 7);
-        const int c = 16 * mt + (lane & 15);
-        const float sc = s_e1[c];
-        _Float16* o = (_Float16*)(out + kPkA1) + e;
-        if (k < 11) split_f16(m.W1[c * kD + k] * sc, 0, o);
-        else if (k < 22) split_f16(m.W1[c * kD + k - 11] * sc, 1, o);
-        else if (k < 24) split_f16(m.b1[c] * sc, k - 22, o);
-        else *o = (_Float16)0.f;
-    }
-    // GEMM2 A: [ch][term][lane] row i = lane % 16, slot s <-> hidden 32 ch + (s < 4 ? 4g + s : 16 + 4g + s - 4)
-    for (int e = t; e < 2 * 2 * 64 * 8; e += 256) {
-        const int ch = e >> 10, term = (e >> 9) & 1, lane = (e >> 3) & 63, sl = e & 7, g = lane >> 4;
-        const int i = lane & 15;
-        const int c = 32 * ch + (sl < 4 ? 4 * g + sl : 16 + 4 * g + sl - 4);
-        _Float16* o = (_Float16*)(out + kPkA2) + e;
-        if (i < 12) split_f16(s_a2[i][c] * s_f[i], term, o);
-        else *o = (_Float16)0.f;
-    }
+    mlp_pack_block(m, out);
 }
 
 int pin_mlp_pack(const PinMlp* mlp, void* packed, void* stream) {

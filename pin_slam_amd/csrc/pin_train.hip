@@ -1359,6 +1359,40 @@ k_adam_step_segments(float* __restrict__ prm, float* __restrict__ grad, float* _
     else adam_segment_body(((int64_t)blockIdx.x - nb_dense) * kTBlock + threadIdx.x, sg, sgrad, sm, sv, a);
 }
 
+// One training iteration's optimiser step (pin_adam_step_train): blocks [0, nb_dense) step the
+// features four floats per thread, their gradient plus the sum of the backward's replicas (zeroed
+// again); block nb_dense steps the decoder's segments and then, with out set, writes the decoder's
+// matrix-core image from the stepped parameters (mlp_pack_block).
+__global__ void __launch_bounds__(kTBlock)
+k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_,
+             int64_t n, int64_t nb_dense, float* __restrict__ rep, int nrep, AdamSegs sg, float* __restrict__ sgrad,
+             float* __restrict__ sm, float* __restrict__ sv, PinMlp mlp, unsigned char* __restrict__ out,
+             PinAdamStep a) {
+    if ((int64_t)blockIdx.x < nb_dense) {
+        const int64_t i0 = 4 * ((int64_t)blockIdx.x * kTBlock + threadIdx.x);
+        if (nrep > 1 && i0 < n) {   // n % 4 == 0 (checked by the host)
+            float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < nrep; ++k) {
+                float4* r = (float4*)(rep + k * n + i0);
+                const float4 v = *r;
+                *r = make_float4(0.f, 0.f, 0.f, 0.f);
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            float4 g = *(float4*)(grad + i0);   // the order of k_replica_reduce: grad + (sum of replicas)
+            g.x += s.x; g.y += s.y; g.z += s.z; g.w += s.w;
+            *(float4*)(grad + i0) = g;
+        }
+        adam_dense_body((int64_t)blockIdx.x * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
+        return;
+    }
+    for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a);
+    if (out) {
+        __threadfence();   // the stepped parameters, read back by the pack below (other threads' writes)
+        __syncthreads();
+        mlp_pack_block(mlp, out);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1391,6 +1425,36 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
     if (nb_dense + nb_seg == 0) return PIN_OK;
     hipLaunchKernelGGL(k_adam_step_segments, dim3((unsigned)(nb_dense + nb_seg)), dim3(kTBlock), 0, as_stream(stream),
                        param, grad, exp_avg, exp_avg_sq, n, nb_dense, sg, seg_grad, seg_exp_avg, seg_exp_avg_sq, *a);
+    return launch_status();
+}
+
+int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                        float* grad_replicas, int32_t replicas, float* const* params, const int64_t* sizes,
+                        int nseg, float* seg_grad, float* seg_exp_avg, float* seg_exp_avg_sq, const PinMlp* mlp,
+                        void* packed, const PinAdamStep* a, void* stream) {
+    if (!a || n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq))) return PIN_ERR_ARG;
+    if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
+    const bool rep = grad_replicas && replicas > 1;
+    if (rep && (n % 4 || ((uintptr_t)grad_replicas & 15))) return PIN_ERR_ARG;
+    AdamSegs sg{};
+    sg.n = 0;
+    if (nseg > 0) {
+        if (!seg_grad || !seg_exp_avg || !seg_exp_avg_sq) return PIN_ERR_ARG;
+        const int rc = adam_segs(params, sizes, nseg, sg);
+        if (rc != PIN_OK) return rc;
+    } else if (nseg < 0) {
+        return PIN_ERR_ARG;
+    }
+    const bool pack = nseg > 0 && mlp && packed;
+    if (pack && (!mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || ((uintptr_t)packed & 15))) return PIN_ERR_ARG;
+    PinMlp m{};
+    if (pack) m = *mlp;
+    const int64_t nb_dense = (n + 4 * kTBlock - 1) / (4 * kTBlock);
+    const int64_t nb = nb_dense + (nseg > 0 ? 1 : 0);
+    if (nb == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_adam_train, dim3((unsigned)nb), dim3(kTBlock), 0, as_stream(stream), param, grad, exp_avg,
+                       exp_avg_sq, n, nb_dense, rep ? grad_replicas : nullptr, rep ? (int)replicas : 0, sg, seg_grad,
+                       seg_exp_avg, seg_exp_avg_sq, m, pack ? (unsigned char*)packed : nullptr, *a);
     return launch_status();
 }
 
@@ -1582,7 +1646,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     }
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
-    if (grad_features && st->grad_replicas && st->replicas > 1) {
+    if (grad_features && st->grad_replicas && st->replicas > 1 && st->replica_mode == 0) {
         const int64_t n4 = pts->rows * kF / 4;
         const int64_t nb = (n4 + kTBlock - 1) / kTBlock;
         hipLaunchKernelGGL(k_replica_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, s,

@@ -113,6 +113,42 @@ class _TrainBuffers:
         return self
 
 
+class _StepPlan:
+    """The launches of one training iteration (Mapper._step_plan); run() takes the batch's draw."""
+    packed = None
+
+    def run(self, index, index_new):
+        b = self.b
+        if not self.index_mode:
+            _lib.call("pin_train_rows", _lib.ptr(self.q), self.gather_tail[0], self.gather_tail[1], self.s)
+        elif self.packed is not None and index_new is not None:
+            new_sel, draw = index_new
+            _lib.check("pin_train_gather_packed_split", self.f_split(
+                self.packed_ptr, self.packed_rows, index.data_ptr(), index.shape[0], new_sel.data_ptr(),
+                new_sel.shape[0], draw.data_ptr(), *self.gather_tail))
+        elif self.packed is not None:
+            _lib.call("pin_train_gather_packed", _lib.ptr(self.packed), int(self.packed.shape[0]), _lib.ptr(index),
+                      *self.gather_tail)
+        else:
+            q, sdf_label, ts, wpool = self.pools
+            _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
+                      int(q.shape[0]), _lib.ptr(index), *self.gather_tail)
+        if self.tiled:
+            # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates)
+            query_sort(self.gv, b.rows, out=b.rows4)
+        self.mapper._order = b.rows4 if self.tiled else None
+        _lib.check("pin_train_forward", self.f_fwd(*self.fwd_args))
+        _lib.check("pin_train_backward", self.f_bwd(*self.bwd_args))
+
+    def finish(self):
+        """After the last run: the side effects went through raw pointers -- invalidate the caches
+        built on them; the loss / sdf of the last iteration."""
+        nm = self.mapper.neural_points
+        nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if self.ts64 is not None else None)
+        self.mapper.last_loss = self.b.loss
+        self.mapper.last_sdf = self.b.sdf[: self.n]
+
+
 class Mapper:
     """utils/mapper.py:Mapper -- constructor signature, pools and training entry points."""
 
@@ -525,19 +561,21 @@ class Mapper:
         fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
         part, slab_rows, slab_new, scales = self._slab_partition(world, fused)
         packed = self._packed_pool() if fused and _PACK_POOL else None
-        for _ in range(iter_count):
+        # the dense fused loop builds its launch plan once (views, structs, buffers) and then only
+        # draws and launches (gather, forward, backward, one Adam step that also sums the gradient
+        # replicas and re-packs a training decoder); the version bumps of the raw-pointer writes
+        # (features, decoder, certainty / ts) are applied once after the loop -- nothing inside
+        # it reads them
+        plan = None
+        if fused and part is None:
+            plan = self._dense_loop(iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed)
+        for _ in range(iter_count if plan is None else 0):
             if fused:
-                if part is None:
-                    index, new_sel, index_new = self._batch_parts()
-                    self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
-                                    world, index=index, weight=self.weight_pool, packed=packed,
-                                    index_new=None if new_sel is None else (new_sel, index_new))
-                else:
-                    index = self._batch_index(slab_rows, slab_new)
-                    scale_h, scale_n = scales(int(index.shape[0]) - self._n_new_rows, self._n_new_rows)
-                    self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
-                                    world, index=index, reduce=False, scale=scale_h, n_tail=self._n_new_rows,
-                                    scale_tail=scale_n, weight=self.weight_pool, packed=packed)
+                index = self._batch_index(slab_rows, slab_new)
+                scale_h, scale_n = scales(int(index.shape[0]) - self._n_new_rows, self._n_new_rows)
+                self.train_step(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
+                                world, index=index, reduce=False, scale=scale_h, n_tail=self._n_new_rows,
+                                scale_tail=scale_n, weight=self.weight_pool, packed=packed)
             else:
                 coord, sdf_label, ts, _, _, _, weight = self.get_batch(global_coord=not self.ba_done_flag)
                 if self.ba_done_flag:
@@ -551,6 +589,12 @@ class Mapper:
             if part is not None:
                 part.exchange_features(fdata)                     # owners -> halo copies
             self.total_iter += 1
+        if plan is not None:
+            plan.finish()
+            nm.mark_modified(feats)
+            for p in mlp_params:
+                torch.autograd.graph.increment_version(p)
+            self.total_iter += iter_count
         if part is not None:
             part.reconcile_side_effects(cert_before, nm.local_point_certainties, nm.local_point_ts_update)
             part.gather_owned(fdata, nm.local_point_certainties, nm.local_point_ts_update)
@@ -564,6 +608,43 @@ class Mapper:
         if fused and iter_count > 0 and int(self._buf.gather_error.item()):
             self._buf.gather_error.zero_()
             raise IndexError("mapping(): a batch index fell outside the sample pool")
+
+    def _dense_loop(self, iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed):
+        """The iterations of a dense fused mapping() call (utils/mapper.py:443-575): per iteration
+        the batch draw (_batch_parts), the gather, forward and backward of a launch plan built
+        once (_step_plan) and one pin_adam_step_train launch (the gradient replicas summed, a
+        training decoder stepped and re-packed).  The version bumps of the raw-pointer writes are
+        the caller's, after the loop -- nothing inside it reads them.  Returns the plan (None
+        for no iterations)."""
+        c = self.config
+        group = getattr(self, "group", None)
+        plan = None
+        segs = None
+        adam = _lib.fn("pin_adam_step_train")
+        s = _lib.stream()
+        for _ in range(iter_count):
+            index, new_sel, index_new = self._batch_parts()
+            idx, idx_new = self._step_index(self.global_coord_pool, index,
+                                            None if new_sel is None else (new_sel, index_new), packed)
+            n = idx.shape[0] + (0 if idx_new is None else idx_new[1].shape[0])
+            if plan is None or plan.n != n:
+                plan = self._step_plan(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
+                                       world, idx, None, 0, 0.0, self.weight_pool, packed, idx_new, fused_adam=True)
+                if m_grad is not None and segs is None:
+                    segs = self._adam_segments(mlp_params, m_grad)
+                mv = plan.mv if (segs is not None and plan.mv.struct.packed) else None
+                # pin_adam_step_train's arguments but the per-step scalars
+                head = (_lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
+                        _lib.ptr(plan.rep), _REPLICAS if plan.rep is not None else 0,
+                        segs[0] if segs else None, segs[1] if segs else None, len(mlp_params) if segs else 0,
+                        _lib.ptr(m_grad), _lib.ptr(m_m), _lib.ptr(m_v), mv.ref() if mv else None,
+                        ctypes.c_void_p(mv.struct.packed) if mv else None)
+            plan.run(idx, idx_new)
+            if world > 1:
+                allreduce_gradients([f_grad, m_grad], group)
+            self._adam_t += 1
+            _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(adam_scalars(c.lr, self._adam_t, c.adam_eps)), s))
+        return plan
 
     def _slab_partition(self, world, fused):
         """shard="space" set-up of one mapping() call: (partition, the slab's pool rows, the slab's
@@ -617,28 +698,53 @@ class Mapper:
         packed: the same pools as one 32-B record per sample (_packed_pool), gathered instead.
         index_new: (new_idx, draw) -- the batch continues with rows new_idx[draw] after index
         (get_batch's new samples, _batch_parts), concatenated by the packed gather itself."""
+        index, index_new = self._step_index(coord, index, index_new, packed)
+        plan = self._step_plan(coord, sdf_label, ts, grad_features, mlp_grad, world, index, scale, n_tail,
+                               scale_tail, weight, packed, index_new)
+        plan.run(index, index_new)
+        plan.finish()
+        if world > 1 and reduce:
+            allreduce_gradients([grad_features, mlp_grad], getattr(self, "group", None))
+        return plan.b.loss
+
+    @staticmethod
+    def _step_index(coord, index, index_new, packed):
+        """The batch's pool rows as the gathers take them (int64 on the pool's device)."""
+        if index is None:
+            return None, None
+        index = index.to(device=coord.device, dtype=torch.int64).contiguous()
+        if index_new is not None:
+            new_sel, draw = (t.to(device=coord.device, dtype=torch.int64).contiguous() for t in index_new)
+            if packed is None:    # the unpacked gather takes one index
+                return torch.cat((index, new_sel[draw]), dim=0), None
+            index_new = (new_sel, draw)
+        return index, index_new
+
+    def _step_plan(self, coord, sdf_label, ts, grad_features, mlp_grad, world, index, scale, n_tail, scale_tail,
+                   weight, packed, index_new, fused_adam=False):
+        """Everything of one training iteration that does not depend on the batch's draw: the
+        configuration structs, the views, the per-row buffers and the launch arguments.  It stays
+        valid while the map, the pools and the batch size stay as they are -- a whole mapping()
+        call, whose iterations then only launch (_StepPlan.run).  fused_adam: the caller steps with
+        pin_adam_step_train, which also sums the gradient replicas and re-packs the decoder."""
         c = self.config
         nm = self.neural_points
         weighted = bool(getattr(c, "loss_weight_on", False)) and weight is not None
-        wrow = None
+        P = _StepPlan()
+        P.mapper = self
+        P.wrow = None
+        P.rep = None
         if index is None:
             q = coord.detach().to(torch.float32).contiguous()
             _lib.require_device(q)
-            label = sdf_label.detach().to(torch.float32).contiguous()
-            ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
+            P.label = sdf_label.detach().to(torch.float32).contiguous()
+            P.ts64 = ts.to(device=q.device, dtype=torch.int64).contiguous() if ts is not None else None
             n = q.shape[0]
             if weighted:
-                wrow = weight.detach().to(device=q.device, dtype=torch.float32).abs().contiguous()
+                P.wrow = weight.detach().to(device=q.device, dtype=torch.float32).abs().contiguous()
         else:
             q = coord
             _lib.require_device(q)
-            index = index.to(device=q.device, dtype=torch.int64).contiguous()
-            if index_new is not None:
-                new_sel, draw = (t.to(device=q.device, dtype=torch.int64).contiguous() for t in index_new)
-                if packed is None:    # the unpacked gather takes one index
-                    index, index_new = torch.cat((index, new_sel[draw]), dim=0), None
-                else:
-                    index_new = (new_sel, draw)
             n = index.shape[0] + (0 if index_new is None else index_new[1].shape[0])
         if grad_features is not None and (grad_features.shape[1] != 8 or not grad_features.is_contiguous()):
             raise ValueError("grad_features must be a contiguous [L+1, 8] float32 tensor")
@@ -653,63 +759,58 @@ class Mapper:
         rows = n + 6 * nd
         if not hasattr(self, "_buf"):    # methods transplanted onto the reference class
             self._buf = _TrainBuffers()
-        b = self._buf.get(rows, nn_k, wf, q.device)
+        b = P.b = self._buf.get(rows, nn_k, wf, q.device)
+        P.n, P.rows = n, rows
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=dec, nn_k=nn_k, weighted_first=int(wf),
                                eps=float(np.float32(c.voxel_size_m * c.num_grad_step_ratio)),
                                sigma=float(np.float32(self.sdf_scale)), weight_e=float(np.float32(c.weight_e)),
                                grad_scale=float(np.float32(1.0 / world if scale is None else scale)), flags=0,
                                n_tail=int(n_tail), grad_scale_tail=float(np.float32(scale_tail)))
         hv, pv = nm._views("local", True)
-        s = _lib.stream()
+        s = P.s = _lib.stream()
         grid = nm.backend() == "grid"
-        gv = nm.grid_view("local", False) if grid else None
+        gv = P.gv = nm.grid_view("local", False) if grid else None
         # every row of the iteration (batch + stencil) materialised once: the tile sort and the
-        # forward read it
+        # forward read it; the row build / gather takes flags 0, the training kernels their own
+        cfg_rows = P.cfg_rows = cfg
         rows_xyz = b.rows
         if index is None:
-            _lib.call("pin_train_rows", _lib.ptr(q), ctypes.byref(cfg), _lib.ptr(rows_xyz), s)
+            P.q = q
         else:
-            label = b.label
-            ts64 = b.ts if ts is not None else None
-            wrow = b.wrow if weighted else None
-            if packed is not None and index_new is not None:
-                new_sel, draw = index_new
-                _lib.call("pin_train_gather_packed_split", _lib.ptr(packed), int(packed.shape[0]), _lib.ptr(index),
-                          int(index.shape[0]), _lib.ptr(new_sel), int(new_sel.shape[0]), _lib.ptr(draw),
-                          ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), _lib.ptr(wrow),
-                          _lib.ptr(b.gather_error), s)
-            elif packed is not None:
-                _lib.call("pin_train_gather_packed", _lib.ptr(packed), int(packed.shape[0]), _lib.ptr(index),
-                          ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label), _lib.ptr(ts64), _lib.ptr(wrow),
-                          _lib.ptr(b.gather_error), s)
-            else:
-                wpool = weight.detach().to(torch.float32).contiguous() if weighted else None
-                _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
-                          int(q.shape[0]), _lib.ptr(index), ctypes.byref(cfg), _lib.ptr(rows_xyz), _lib.ptr(label),
-                          _lib.ptr(ts64), _lib.ptr(wrow), _lib.ptr(b.gather_error), s)
+            P.label = b.label
+            P.ts64 = b.ts if ts is not None else None
+            P.wrow = b.wrow if weighted else None
+            if packed is None:
+                P.pools = (q, sdf_label, ts, weight.detach().to(torch.float32).contiguous() if weighted else None)
+            P.packed = packed
+            if packed is not None:
+                P.packed_ptr, P.packed_rows = packed.data_ptr(), int(packed.shape[0])
+        P.gather_tail = (ctypes.byref(cfg_rows), _lib.ptr(rows_xyz), _lib.ptr(P.label), _lib.ptr(P.ts64),
+                         _lib.ptr(P.wrow), _lib.ptr(b.gather_error), s)
+        P.index_mode = index is not None
+        cfg = P.cfg = _lib.PinTrainCfg.from_buffer_copy(cfg_rows)
         cfg.flags = _lib.PIN_TRAIN_ROWS
-        q = rows_xyz
-        sorted_rows = None
-        if grid and _TILE_QUERIES and rows >= _TRAIN_TILE_MIN:
-            # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates)
-            sorted_rows = query_sort(gv, rows_xyz, out=b.rows4)
-        self._order = sorted_rows
-        st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
-                                sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
-                                ts_update=nm.local_point_ts_update.data_ptr() if ts64 is not None else None,
-                                order=None, sorted_rows=sorted_rows.data_ptr() if sorted_rows is not None else None,
-                                row_weight=_lib.ptr(wrow), row_ts=_lib.ptr(ts64))
+        P.tiled = grid and _TILE_QUERIES and rows >= _TRAIN_TILE_MIN
+        st = P.st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
+                                       sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
+                                       ts_update=nm.local_point_ts_update.data_ptr() if P.ts64 is not None else None,
+                                       order=None, sorted_rows=b.rows4.data_ptr() if P.tiled else None,
+                                       row_weight=_lib.ptr(P.wrow), row_ts=_lib.ptr(P.ts64))
         if (grad_features is not None and rows < _REPLICA_ROWS and _REPLICAS > 1
                 and grad_features.shape[0] == pv.features.shape[0]):
             rep = b.replicas(_REPLICAS * grad_features.numel(), q.device)
-            st.grad_replicas, st.replicas = rep.data_ptr(), _REPLICAS
+            # the Adam launch sums the replicas -- unless the gradient is all-reduced before it
+            defer = bool(fused_adam) and world == 1
+            st.grad_replicas, st.replicas, st.replica_mode = rep.data_ptr(), _REPLICAS, int(defer)
+            P.rep = rep if defer else None
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK and not analytic
         # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores;
         # weighted_first with a training decoder: the backward decodes each row there once (input
         # gradient + ReLU masks of the decoder-parameter products)
-        mv = mlp_view(self.geo_mlp, packed=_MLP_PACK and (mlp_grad is None or (wf and not analytic and _ROW_DECODE)))
+        mv = P.mv = mlp_view(self.geo_mlp,
+                             packed=_MLP_PACK and (mlp_grad is None or (wf and not analytic and _ROW_DECODE)))
         if dx:
             cfg.flags |= _lib.PIN_TRAIN_DX
         if analytic:
@@ -718,21 +819,14 @@ class Mapper:
             st.eik_coef, st.eik_vec = ec.data_ptr(), ev.data_ptr()
         if pv.features.data_ptr() != nm.local_geo_features.data_ptr():
             raise RuntimeError("local_geo_features must be a contiguous float32 tensor")
-        if grid:
-            _lib.call("pin_train_forward", None, gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), _lib.ptr(ts64),
-                      ctypes.byref(cfg), ctypes.byref(st), s)
-        else:
-            _lib.call("pin_train_forward", hv.ref(), None, pv.ref(), mv.ref(), _lib.ptr(q), _lib.ptr(ts64),
-                      ctypes.byref(cfg), ctypes.byref(st), s)
-        _lib.call("pin_train_backward", pv.ref(), mv.ref(), _lib.ptr(label), ctypes.byref(cfg), ctypes.byref(st),
-                  _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
-        # the forward's side effects went through raw pointers: invalidate caches built on them
-        nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if ts64 is not None else None)
-        if world > 1 and reduce:
-            allreduce_gradients([grad_features, mlp_grad], getattr(self, "group", None))
-        self.last_loss = b.loss
-        self.last_sdf = b.sdf[:n]
-        return b.loss
+        P.fwd_args = ((None, gv.ref()) if grid else (hv.ref(), None)) + (
+            pv.ref(), mv.ref(), _lib.ptr(rows_xyz), _lib.ptr(P.ts64), ctypes.byref(cfg), ctypes.byref(st), s)
+        P.bwd_args = (pv.ref(), mv.ref(), _lib.ptr(P.label), ctypes.byref(cfg), ctypes.byref(st),
+                      _lib.ptr(grad_features), _lib.ptr(mlp_grad), _lib.ptr(b.workspace), _lib.ptr(b.loss), s)
+        P.keep = (hv, pv, gv, mv, grad_features, mlp_grad)
+        P.f_fwd, P.f_bwd = _lib.fn("pin_train_forward"), _lib.fn("pin_train_backward")
+        P.f_split = _lib.fn("pin_train_gather_packed_split")
+        return P
 
     def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None, partition=None):
         """torch.optim.Adam(betas=(0.9, 0.99), eps=adam_eps) step (utils/tools.py:111-112); with a
@@ -762,16 +856,15 @@ class Mapper:
             _lib.call("pin_adam_rows", _lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v),
                       _lib.ptr(partition.adam_rows), partition.adam_rows.numel(), ctypes.byref(st), s)
             partition.zero_halo(f_grad)
+        if m_grad is not None and partition is not None:   # the decoder's parameters in one launch of their own
+            _lib.call("pin_adam_segments", segs[0], segs[1], len(mlp_params), _lib.ptr(m_grad), _lib.ptr(m_m),
+                      _lib.ptr(m_v), ctypes.byref(st), s)
         feats = self.neural_points.local_geo_features
         self.neural_points.mark_modified(feats if feats.data_ptr() == fdata.data_ptr() else fdata)
-        if m_grad is not None:
-            if partition is not None:   # the decoder's parameters in one launch of their own
-                _lib.call("pin_adam_segments", segs[0], segs[1], len(mlp_params), _lib.ptr(m_grad), _lib.ptr(m_m),
-                          _lib.ptr(m_v), ctypes.byref(st), s)
-            # the step wrote through raw pointers: bump the versions so views built on the
-            # parameters (the matrix-core operand image of mlp_view) are rebuilt before the next use
-            for p in mlp_params:
-                torch.autograd.graph.increment_version(p)
+        # the step wrote through raw pointers: bump the versions so views built on the parameters
+        # (the matrix-core operand image of mlp_view) are rebuilt before the next use
+        for p in mlp_params if m_grad is not None else ():
+            torch.autograd.graph.increment_version(p)
 
     @staticmethod
     def _adam_segments(mlp_params, m_grad):

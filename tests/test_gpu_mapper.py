@@ -255,6 +255,51 @@ def test_fused_adam_equals_separate_launches(dev):
     assert float(fa[1].abs().max()) == 0.0 and float(sg.abs().max()) == 0.0   # gradients zeroed
 
 
+def test_train_adam_equals_replica_sum_segments_and_pack(dev):
+    """pin_adam_step_train (the dense mapping loop's one optimiser launch) against the separate
+    launches on copies: the replicas added into the gradient (k_replica_reduce's order), then
+    pin_adam_step_segments, then pin_mlp_pack of the stepped decoder -- bitwise equal parameters,
+    moments, zeroed gradients and replicas, and the same operand image."""
+    import ctypes
+    from pin_slam_amd.mapper import adam_scalars
+    from pin_slam_amd.query import mlp_view
+    cfg = P.Config(device=dev)
+    torch.manual_seed(3)
+    decs = [P.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(dev) for _ in range(2)]
+    decs[1].load_state_dict(decs[0].state_dict())
+    g = torch.Generator(device="cpu").manual_seed(4)
+    n, R = 8 * 1237, 8
+    fa = [torch.randn(n, generator=g).to(dev) for _ in range(4)]          # param, grad, m, v
+    fa[3] = fa[3].abs()
+    rep = torch.randn(R * n, generator=g).to(dev)
+    sizes = [p.numel() for p in decs[0].parameters()]
+    sg, sm, sv = (torch.randn(sum(sizes), generator=g).to(dev) for _ in range(3))
+    sv = sv.abs()
+    fb, repb = [t.clone() for t in fa], rep.clone()
+    sgb, smb, svb = sg.clone(), sm.clone(), sv.clone()
+    st = adam_scalars(0.01, 3, 1e-15)
+    szs = (ctypes.c_int64 * 4)(*sizes)
+    views = [mlp_view(d, packed=True) for d in decs]
+    packs = [torch.zeros(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=dev) for _ in range(2)]
+    ptrs = [(ctypes.c_void_p * 4)(*[p.data.data_ptr() for p in d.parameters()]) for d in decs]
+    _lib.call("pin_adam_step_train", *[_lib.ptr(t) for t in fa], n, _lib.ptr(rep), R, ptrs[0], szs, 4, _lib.ptr(sg),
+              _lib.ptr(sm), _lib.ptr(sv), views[0].ref(), _lib.ptr(packs[0]), ctypes.byref(st), _lib.stream())
+    acc = torch.zeros(n, device=dev)
+    for k in range(R):
+        acc += repb[k * n:(k + 1) * n]
+    fb[1] += acc
+    _lib.call("pin_adam_step_segments", *[_lib.ptr(t) for t in fb], n, ptrs[1], szs, 4, _lib.ptr(sgb), _lib.ptr(smb),
+              _lib.ptr(svb), ctypes.byref(st), _lib.stream())
+    _lib.call("pin_mlp_pack", views[1].ref(), _lib.ptr(packs[1]), _lib.stream())
+    torch.cuda.synchronize()
+    for a, b in zip(fa + [sg, sm, sv], fb + [sgb, smb, svb]):
+        assert torch.equal(a, b)
+    for pa, pb in zip(decs[0].parameters(), decs[1].parameters()):
+        assert torch.equal(pa, pb)
+    assert float(rep.abs().max()) == 0.0 and float(fa[1].abs().max()) == 0.0
+    assert torch.equal(packs[0], packs[1])
+
+
 def test_split_gather_equals_concatenated_index(dev):
     """pin_train_gather_packed_split (get_batch's history draw + new_idx[draw], utils/mapper.py:
     335-340) against pin_train_gather_packed over the torch.cat of the same rows: bitwise equal

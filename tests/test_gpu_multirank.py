@@ -59,16 +59,24 @@ def _worker(rank, world, port, case, shard, q, layout="auto"):
         draws = ReplayDraws(7000 + 31 * rank)
         mapper._randint = lambda high, k: torch.from_numpy(draws.randint(high, k)).to("cuda")
         calls = []
-        step = mapper.train_step
+        step, step_index = mapper.train_step, mapper._step_index
+
+        # every iteration's batch passes _step_index (the dense loop calls it directly, train_step --
+        # the slab path -- from inside, with the rank's scales, recorded after it)
+        def recorded_index(coord, index, index_new, packed):
+            full = index
+            if index_new is not None:      # a batch split into history rows + new_idx[draw]
+                new_sel, draw = index_new
+                full = torch.cat((index, new_sel[draw]), dim=0)
+            calls.append(dict(index=full.cpu().numpy(), scale=None, n_tail=0, scale_tail=0.0, world=world))
+            return step_index(coord, index, index_new, packed)
 
         def recorded(*a, **kw):
-            index = kw["index"]
-            if kw.get("index_new") is not None:      # a batch split into history rows + new_idx[draw]
-                new_sel, draw = kw["index_new"]
-                index = torch.cat((index, new_sel[draw]), dim=0)
-            calls.append(dict(index=index.cpu().numpy(), scale=kw.get("scale"), n_tail=int(kw.get("n_tail", 0)),
-                              scale_tail=float(kw.get("scale_tail", 0.0)), world=int(a[5])))
-            return step(*a, **kw)
+            out = step(*a, **kw)
+            calls[-1].update(scale=kw.get("scale"), n_tail=int(kw.get("n_tail", 0)),
+                             scale_tail=float(kw.get("scale_tail", 0.0)), world=int(a[5]))
+            return out
+        mapper._step_index = recorded_index
         mapper.train_step = recorded
         with warnings.catch_warnings(record=True) as caught:
             warnings.simplefilter("always")

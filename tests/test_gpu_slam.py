@@ -149,6 +149,11 @@ def test_slam_sequence_matches_reference(golden, dev):
                 # samples near that sphere move in or out with the pose, ~0.025 % of the pool per cm at
                 # frame 29 (the dense early frames lie on the sphere); 0.05 % per cm of pose difference
                 rel = max(rel, 0.0005 * 100.0 * dt)
+            if name in ("map_count", "local_count"):
+                # a frame registered a few cm apart inserts its points into partly other voxels: the
+                # counts drift with the pose difference (measured 0.2-0.22 % per cm over frames
+                # 25-29 of a run 3-4.6 cm apart); 0.3 % per cm of pose difference
+                rel = max(rel, 0.003 * 100.0 * dt)
             assert _within(g, w, rel), f"frame {k}: {name} {g} vs reference {w}"
         if k == 0:
             _surface_check(nm, dec, z, dev, "f0_surface_probes", "f0_surface_sdf")

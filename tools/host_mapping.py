@@ -59,16 +59,48 @@ def main(frames=12):
     from pin_slam_amd.query import mlp_view
     print(f"host only: 15 x mlp_view(packed) after a decoder step "
           f"{host_ms(lambda: [(torch.autograd.graph.increment_version(dec.lout.bias), mlp_view(dec, packed=True)) for _ in range(15)]):.3f} ms")
+    # the fused mapping loop by hand (mapping()'s dense branch), behind a sleep, timed per phase
+    feats = nm.local_geo_features
+    fdata = feats.data
+    f_grad, f_m, f_v = torch.zeros_like(fdata), torch.zeros_like(fdata), torch.zeros_like(fdata)
+    mlp_params = [p for p in dec.parameters() if p.requires_grad]
+    m_grad = m_m = m_v = None
+    if mlp_params:
+        m_grad = torch.zeros((P._lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+        m_m, m_v = torch.zeros_like(m_grad), torch.zeros_like(m_grad)
+    packed = mapper._packed_pool()
+    acc = {"batch": 0.0, "train_step": 0.0, "adam": 0.0}
+    for rep in range(3):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(100_000_000)
+        for _ in range(15):
+            t0 = time.perf_counter()
+            index, new_sel, index_new = mapper._batch_parts()
+            t1 = time.perf_counter()
+            mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, f_grad, m_grad, 1,
+                              index=index, weight=mapper.weight_pool, packed=packed,
+                              index_new=None if new_sel is None else (new_sel, index_new))
+            t2 = time.perf_counter()
+            mapper._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
+            t3 = time.perf_counter()
+            if rep == 2:
+                acc["batch"] += t1 - t0
+                acc["train_step"] += t2 - t1
+                acc["adam"] += t3 - t2
+        torch.cuda.synchronize()
+    print("host only, 15 iterations by hand (ms):", {k: round(v * 1e3, 3) for k, v in acc.items()})
     pr = cProfile.Profile()
     torch.cuda.synchronize()
     pr.enable()
-    t0 = time.perf_counter()
-    mapper.mapping(15)
-    t1 = time.perf_counter()
+    for _ in range(300):
+        index, new_sel, index_new = mapper._batch_parts()
+        mapper.train_step(mapper.global_coord_pool, mapper.sdf_label_pool, mapper.time_pool, f_grad, m_grad, 1,
+                          index=index, weight=mapper.weight_pool, packed=packed,
+                          index_new=None if new_sel is None else (new_sel, index_new))
+        mapper._adam(fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v)
     pr.disable()
     torch.cuda.synchronize()
-    print(f"profiled call wall {1e3 * (t1 - t0):.3f} ms")
-    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(40)
 
 
 if __name__ == "__main__":

@@ -15,7 +15,7 @@ rows = list(csv.DictReader(open(f)))
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 # steady-state mapping iterations: the decoder Adam launch marks each iteration's end (k_adam_segments,
 # or k_adam_step_segments when the feature and decoder steps share one launch)
-idx = [i for i, e in enumerate(ev) if "k_adam_segments" in e[2] or "k_adam_step_segments" in e[2]]
+idx = [i for i, e in enumerate(ev) if "k_adam_segments" in e[2] or "k_adam_step_segments" in e[2] or "k_adam_train" in e[2]]
 print("mapping iterations seen:", len(idx))
 a, b = idx[-8], idx[-7]
 prev = None
