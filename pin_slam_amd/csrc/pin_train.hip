@@ -1359,17 +1359,19 @@ k_adam_step_segments(float* __restrict__ prm, float* __restrict__ grad, float* _
     else adam_segment_body(((int64_t)blockIdx.x - nb_dense) * kTBlock + threadIdx.x, sg, sgrad, sm, sv, a);
 }
 
-// One training iteration's optimiser step (pin_adam_step_train): blocks [0, nb_dense) step the
-// features four floats per thread, their gradient plus the sum of the backward's replicas (zeroed
-// again); block nb_dense steps the decoder's segments and then, with out set, writes the decoder's
-// matrix-core image from the stepped parameters (mlp_pack_block).
+// One training iteration's optimiser step (pin_adam_step_train): with decoder segments, block 0
+// steps them and then, with out set, writes the decoder's matrix-core image from the stepped
+// parameters (mlp_pack_block); the other nb_dense blocks step the features four floats per thread,
+// their gradient plus the sum of the backward's replicas (zeroed again).
 __global__ void __launch_bounds__(kTBlock)
 k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_,
              int64_t n, int64_t nb_dense, float* __restrict__ rep, int nrep, AdamSegs sg, float* __restrict__ sgrad,
              float* __restrict__ sm, float* __restrict__ sv, PinMlp mlp, unsigned char* __restrict__ out,
              PinAdamStep a) {
-    if ((int64_t)blockIdx.x < nb_dense) {
-        const int64_t i0 = 4 * ((int64_t)blockIdx.x * kTBlock + threadIdx.x);
+    // the decoder's block first (dispatched first: the pack after its step is the longest chain)
+    const int64_t bid = (int64_t)blockIdx.x - (sg.n > 0 ? 1 : 0);
+    if (bid >= 0) {
+        const int64_t i0 = 4 * (bid * kTBlock + threadIdx.x);
         if (nrep > 1 && i0 < n) {   // n % 4 == 0 (checked by the host)
             float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int k = 0; k < nrep; ++k) {
@@ -1382,7 +1384,7 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
             g.x += s.x; g.y += s.y; g.z += s.z; g.w += s.w;
             *(float4*)(grad + i0) = g;
         }
-        adam_dense_body((int64_t)blockIdx.x * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
+        adam_dense_body(bid * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
         return;
     }
     for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a);
