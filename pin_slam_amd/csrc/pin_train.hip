@@ -52,6 +52,11 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
     else qz = (blk & 1) ? qz - c.eps : qz + c.eps;
 }
 
+#ifndef PIN_TRAIN_FWD_MF
+#define PIN_TRAIN_FWD_MF 1   // weighted_first, not PIN_TRAIN_DX, mlp->packed: the forward's sdf on the matrix cores
+#endif
+constexpr bool kTrainFwdMf = PIN_TRAIN_FWD_MF != 0;
+
 #ifndef PIN_TRAIN_IDP
 #define PIN_TRAIN_IDP 1   // training forward: top-k payload = feature-row id (GridSource IDP)
 #endif
@@ -60,7 +65,7 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 // the last row that runs slot 0 and writes nothing.  The neighbours' ids and weights are returned
 // in cid / cw (-1 / 0 invalid); the block's flush_rows stores them (coalesced) and applies the
 // training side effects.
-template <bool WF, class Src, bool MF = false>
+template <bool WF, class Src, bool MF = false, bool DX = MF>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
@@ -151,7 +156,14 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         }
     }
     if (WF) {
-        if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX: [rows, 8])
+        if constexpr (MF && !DX) {   // a training decoder: the sdf on the matrix cores, x [rows, 11] saved
+            float gx[kF];
+            sdf = mlp_sdf_mfma16<false, 0, kF>(m, x, gx);
+            if (live) {
+#pragma unroll
+                for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+            }
+        } else if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX: [rows, 8])
             float gx[kF];
             sdf = mlp_sdf_mfma16<true, 0, kF>(m, x, gx);
             if (live) {
@@ -209,7 +221,7 @@ __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainS
     }
 }
 
-template <bool WF, bool MF>
+template <bool WF, bool MF, bool DX = MF>
 __global__ void __launch_bounds__(kTBlock)
 k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
@@ -224,12 +236,12 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const HashSource src(h, p);
-        train_forward_body<WF, HashSource, MF>(src, p, mw, coord, ts, c, t, st, cid, cw, t < rows);
+        train_forward_body<WF, HashSource, MF, DX>(src, p, mw, coord, ts, c, t, st, cid, cw, t < rows);
     }
     flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
 }
 
-template <bool WF, bool MF>
+template <bool WF, bool MF, bool DX = MF>
 __global__ void __launch_bounds__(kTBlock)
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
@@ -244,7 +256,7 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
     if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
         const GridSource<false, PIN_TRAIN_IDP> src(g, p);
-        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF>(src, p, mw, coord, ts, c, t, st, cid, cw,
+        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF, DX>(src, p, mw, coord, ts, c, t, st, cid, cw,
                                                                      t < rows);
     }
     flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
@@ -1587,6 +1599,9 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     do {                                                                                                        \
         if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp, \
                                    coord, ts, *cfg, *st);                                                       \
+        else if (cfg->weighted_first && mlp->packed && kTrainFwdMf)                                             \
+            hipLaunchKernelGGL((KERNEL<true, true, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts,     \
+                               *mlp, coord, ts, *cfg, *st);                                                     \
         else if (cfg->weighted_first)                                                                           \
             hipLaunchKernelGGL((KERNEL<true, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,     \
                                coord, ts, *cfg, *st);                                                           \
