@@ -875,6 +875,10 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
     }
 }
 
+#ifndef PIN_SCAT_UNROLL
+#define PIN_SCAT_UNROLL 1
+#endif
+
 // Scatter of the block's weighted_first feature-gradient rows (all threads; after a barrier):
 // element e = (row, j, d), d fastest: a wave instruction covers 8 (row, neighbour) pairs x 32
 // contiguous bytes, one memory-side request each -- the cheapest atomic shape measured (LDS
@@ -898,6 +902,7 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
     }
     __syncthreads();
     const int total = npair * kF;
+#pragma unroll PIN_SCAT_UNROLL
     for (int e = threadIdx.x; e < total; e += kTBlock) {
         const int d = e & (kF - 1);
         const int rj = e >> 3;

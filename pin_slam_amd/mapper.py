@@ -546,14 +546,13 @@ class Mapper:
         dev = feats.device
         # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441)
         fdata = feats.data
-        f_grad = torch.zeros_like(fdata)
-        f_m = torch.zeros_like(fdata)
-        f_v = torch.zeros_like(fdata)
+        # gradient and moments (and the decoder's) zeroed in one fill
+        nf, nmg = fdata.numel(), (_lib.MLP_GRAD_SIZE if train_mlp else 0)
+        state = torch.zeros((3 * nf + 3 * nmg,), dtype=torch.float32, device=dev)
+        f_grad, f_m, f_v = (state[k * nf:(k + 1) * nf].view_as(fdata) for k in range(3))
         m_grad = m_m = m_v = None
         if train_mlp:
-            m_grad = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
-            m_m = torch.zeros_like(m_grad)
-            m_v = torch.zeros_like(m_grad)
+            m_grad, m_m, m_v = (state[3 * nf + k * nmg:3 * nf + (k + 1) * nmg] for k in range(3))
         cert_before = nm.local_point_certainties.clone() if world > 1 else None
         self._adam_t = 0
         # get_batch's gathers fused into the row build (pin_train_gather) when the pools allow it;
