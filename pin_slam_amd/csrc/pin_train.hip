@@ -1185,6 +1185,7 @@ __global__ void __launch_bounds__(1024) k_loss_final(const double* __restrict__ 
                                                      double* __restrict__ out) {
     __shared__ double red[16];
     double v = 0.0;
+#pragma unroll 8   // the loads in flight together (the adds keep their order)
     for (int64_t i = threadIdx.x; i < n; i += 1024) v += part[i];
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
