@@ -26,3 +26,11 @@ for s, e, n in ev[first - 14:first]:
     print(f"  before {n.replace('(anonymous namespace)::', '')[:70]:70s} {(e - s) / 1e3:7.2f} us  ends {(ev[first][0] - e) / 1e3:8.2f} us before")
 for s, e, n in ev[call[-1] + 1:call[-1] + 10]:
     print(f"  after  {n.replace('(anonymous namespace)::', '')[:70]:70s} {(e - s) / 1e3:7.2f} us  starts {(s - ev[call[-1]][1]) / 1e3:8.2f} us after")
+
+# the frame's work before the call (process_frame and the grid rebuild): every kernel in the
+# 1.6 ms before the call's first gather, with its start relative to that gather
+t_first = ev[first][0]
+print("kernels in the 1.6 ms before the call (start relative to its first gather, duration):")
+for s, e, n in ev:
+    if t_first - 1.6e6 <= s < t_first:
+        print(f"  {(s - t_first) / 1e3:9.1f} us  {(e - s) / 1e3:7.2f} us  {n.replace('(anonymous namespace)::', '')[:80]}")
