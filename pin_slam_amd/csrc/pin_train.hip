@@ -241,8 +241,13 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
 }
 
+#ifdef PIN_TRAIN_FWD_WAVES   // experiment: the grid training forward compiled for this many waves per SIMD
+#define PIN_FWD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(PIN_TRAIN_FWD_WAVES)))
+#else
+#define PIN_FWD_WAVES_ATTR
+#endif
 template <bool WF, bool MF, bool DX = MF>
-__global__ void __launch_bounds__(kTBlock)
+__global__ void __launch_bounds__(kTBlock) PIN_FWD_WAVES_ATTR
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
