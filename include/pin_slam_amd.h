@@ -465,6 +465,11 @@ typedef struct PinTrainCfg {
 #define PIN_TRAIN_ROWS 1
 #define PIN_TRAIN_DX 2
 #define PIN_TRAIN_EIK 4
+/* PIN_TRAIN_PAIR: pin_train_forward runs two lanes per row where it can (grid backend with the
+ * column scan, weighted_first, a packed decoder): the row's candidate list split between the two,
+ * the halves merged in reference order -- the same neighbours, ids, weights, sdf and saved state
+ * as one lane per row, with twice the waves for a batch of ~1 wave per SIMD (small batches). */
+#define PIN_TRAIN_PAIR 8
 
 /* Per-row buffers saved by pin_train_forward for pin_train_backward (rows = n_main + 6 n_stencil). */
 typedef struct PinTrainState {

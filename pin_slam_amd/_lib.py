@@ -16,6 +16,7 @@ PIN_OK = 0
 PIN_TRAIN_ROWS = 1   # PinTrainCfg.flags: coord holds every row of the iteration
 PIN_TRAIN_DX = 2     # PinTrainCfg.flags: forward saves s dsdf/dx (matrix-core decoder), backward applies it
 PIN_TRAIN_EIK = 4    # PinTrainCfg.flags: analytic-gradient eikonal (double backward in closed form)
+PIN_TRAIN_PAIR = 8   # PinTrainCfg.flags: two lanes per row in the forward (small batches)
 PIN_RECORD_UNFAITHFUL = 1 << 30   # record id flag (pin_build_records)
 PIN_QUERY_OUT_TILE = 1   # outputs in tile order (pin_query_sdf_grid_*_ex)
 PIN_GRID_TABLE_TRUSTED = 1   # pin_grid_mark_ex: skip the table count

@@ -100,6 +100,32 @@ struct TopK {
     }
 };
 
+// Pair mode (two lanes per query, the even lane's candidates before the odd lane's in the
+// reference order): both lanes end with the even lane's list and the odd lane's candidates
+// inserted after it -- the sequential scan's result, ties included (insert keeps arrival order).
+__device__ __forceinline__ void topk_pair_merge(TopK& tk, int ph) {
+    float od[kK];
+    int og[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        od[j] = __shfl_xor(tk.d[j], 1);
+        og[j] = __shfl_xor(tk.g[j], 1);
+    }
+    TopK base;
+    float ad[kK];
+    int ag[kK];
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        base.d[j] = ph ? od[j] : tk.d[j];
+        base.g[j] = ph ? og[j] : tk.g[j];
+        ad[j] = ph ? tk.d[j] : od[j];
+        ag[j] = ph ? tk.g[j] : og[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kK; ++j) base.insert(ad[j], ag[j]);
+    tk = base;
+}
+
 // ---------------------------------------------------------------------------------------
 // Candidate sources.  Both enumerate the neighbour cells of q in the reference's cell order
 // (model/neural_points.py:430-439), reject empty / filtered / too-far candidates, keep the
@@ -343,6 +369,123 @@ struct GridSource {
             records_from_list<CH>(s_list, cnt, crec, qx, qy, qz, maxd2, tk, nn);
         }
         return nn;
+    }
+
+    // Pair mode (small training batches, two lanes per query; ph = lane & 1): both lanes list the
+    // same occupied cells, the even lane takes the first half of each list segment and the odd
+    // lane the second, and the lists are merged in reference order at every segment flush (the
+    // odd lane then restarts empty) and at the end.  Returns nn over both halves.  Outside the
+    // column scan both lanes run the whole scan and the odd lane's result is dropped.
+    template <int CH>
+    __device__ __forceinline__ int scan_pair(float qx, float qy, float qz, TopK& tk, int ph) const {
+        if (!(gr.window <= 2 && gr.num_columns > 0)) {
+            int nn = scan<CH>(qx, qy, qz, tk);
+            if (ph) {
+                tk.init();
+                nn = 0;
+            }
+            topk_pair_merge(tk, ph);
+            return nn + __shfl_xor(nn, 1);
+        }
+        int* const s_list = wave_list();
+        const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
+        const float4* __restrict__ crec = (const float4*)gr.crec;
+        const int32_t* __restrict__ offs = gr.offsets;
+        const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
+        const int nbx = gr.dims.nbx, nby = gr.dims.nby, nbz = gr.dims.nbz;
+        const int lx = rel(qx, res, gr.dims.ox, 4 * nbx);
+        const int ly = rel(qy, res, gr.dims.oy, 4 * nby);
+        const int lz = rel(qz, res, gr.dims.oz, 4 * nbz);
+        const int bx0 = (lx - 2) >> 2, by0 = (ly - 2) >> 2, bz0 = (lz - 2) >> 2;
+        uint32_t wl[8], wh[8], wp[8];
+        {
+            uint4 w[8];
+            bool in[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int bx = bx0 + (k & 1), by = by0 + ((k >> 1) & 1), bz = bz0 + (k >> 2);
+                in[k] = (unsigned)bx < (unsigned)nbx && (unsigned)by < (unsigned)nby && (unsigned)bz < (unsigned)nbz;
+                w[k] = bricks[in[k] ? ((int64_t)bz * nby + by) * nbx + bx : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                wl[k] = in[k] ? w[k].x : 0u;
+                wh[k] = in[k] ? w[k].y : 0u;
+                wp[k] = w[k].z;
+            }
+        }
+        const int lane = threadIdx.x & 63;
+        const int Kc = gr.num_cells;
+        int nn = 0;
+        const int32_t* __restrict__ cols = offs + ((Kc + 15) & ~15);
+        const int zr0 = lz - 4 * bz0;
+        int cnt = 0;
+        for (int c = 0; c < gr.num_columns; ++c) {
+            const int col = cols[c];
+            const int nz = (col >> 24) & 255;
+            if (__any(cnt + nz > kSeg)) {   // list full: its two halves, then the merge
+                const int h = (cnt + 1) >> 1;
+                records_from_range<CH>(s_list, ph ? h : 0, ph ? cnt : h, crec, qx, qy, qz, maxd2, tk, nn);
+                topk_pair_merge(tk, ph);
+                if (ph) tk.init();
+                cnt = 0;
+            }
+            const int cx = lx + ((col & 255) - 128);
+            const int cy = ly + (((col >> 8) & 255) - 128);
+            const int kxy = ((cx >> 2) - bx0) | (((cy >> 2) - by0) << 1);
+            const uint32_t lo0 = sel4v(wl[0], wl[1], wl[2], wl[3], kxy);
+            const uint32_t hi0 = sel4v(wh[0], wh[1], wh[2], wh[3], kxy);
+            const uint32_t lo1 = sel4v(wl[4], wl[5], wl[6], wl[7], kxy);
+            const uint32_t hi1 = sel4v(wh[4], wh[5], wh[6], wh[7], kxy);
+            const uint32_t pre0 = sel4v(wp[0], wp[1], wp[2], wp[3], kxy);
+            const uint32_t pre1 = sel4v(wp[4], wp[5], wp[6], wp[7], kxy);
+            const int sh = ((cx & 3) << 4) | ((cy & 3) << 2);
+            const uint32_t n0 = (uint32_t)((((uint64_t)hi0 << 32) | lo0) >> sh) & 15u;
+            const uint32_t n1 = (uint32_t)((((uint64_t)hi1 << 32) | lo1) >> sh) & 15u;
+            const int zs = zr0 + (((col >> 16) & 255) - 128);
+            uint32_t run = ((n0 | (n1 << 4)) >> zs) & ((1u << nz) - 1u);
+            while (run) {
+                const int z = zs + __builtin_ctz(run);
+                run &= run - 1u;
+                const bool up = z >= 4;
+                const uint64_t bits = up ? (((uint64_t)hi1 << 32) | lo1) : (((uint64_t)hi0 << 32) | lo0);
+                const uint32_t pre = up ? pre1 : pre0;
+                const int bit = sh | (z & 3);
+                s_list[cnt * 64 + lane] = (int)(pre + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull)));
+                ++cnt;
+            }
+        }
+        const int h = (cnt + 1) >> 1;
+        records_from_range<CH>(s_list, ph ? h : 0, ph ? cnt : h, crec, qx, qy, qz, maxd2, tk, nn);
+        topk_pair_merge(tk, ph);
+        return nn + __shfl_xor(nn, 1);
+    }
+
+    // Records of list entries [lo, hi) of the lane, CH per round trip (scan_pair)
+    template <int CH>
+    __device__ __forceinline__ static void records_from_range(const int* s_list, int lo, int hi,
+                                                              const float4* __restrict__ crec, float qx, float qy,
+                                                              float qz, float maxd2, TopK& tk, int& nn) {
+        const int lane = threadIdx.x & 63;
+        for (int j0 = lo; __any(j0 < hi); j0 += CH) {
+            int ci[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int v = s_list[(j0 + u < kSeg ? j0 + u : kSeg - 1) * 64 + lane];   // stale slots are masked
+                ci[u] = (j0 + u < hi) ? v : -1;
+            }
+            float4 r[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) r[u] = crec[ci[u] > 0 ? ci[u] : 0];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int id = __float_as_int(r[u].w);
+                const float d2 = dist2(r[u].x, r[u].y, r[u].z, qx, qy, qz);
+                const bool ok = ci[u] >= 0 && id != -1 && d2 <= maxd2;
+                nn += ok ? 1 : 0;
+                tk.insert(ok ? d2 : INFINITY, IDP ? (id & kIdMask) : ci[u]);
+            }
+        }
     }
 
     // Records of the lane's listed candidates, CH gathers per round trip; the trip count is the

@@ -65,7 +65,7 @@ constexpr bool kTrainFwdMf = PIN_TRAIN_FWD_MF != 0;
 // the last row that runs slot 0 and writes nothing.  The neighbours' ids and weights are returned
 // in cid / cw (-1 / 0 invalid); the block's flush_rows stores them (coalesced) and applies the
 // training side effects.
-template <bool WF, class Src, bool MF = false, bool DX = MF>
+template <bool WF, class Src, bool MF = false, bool DX = MF, bool PAIR = false>
 __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoints& p, const MlpW& m,
                                                    const float* __restrict__ coord, const int64_t* __restrict__ ts,
                                                    PinTrainCfg c, int64_t t, PinTrainState st, int (&cid)[kK],
@@ -84,7 +84,11 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     }
     TopK tk;
     tk.init();
-    const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    int nn;
+    if constexpr (PAIR) nn = src.template scan_pair<Src::kChunk>(qx, qy, qz, tk, threadIdx.x & 1);
+    else nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    // pair mode: both lanes of the pair hold the row's neighbours; the even lane writes its outputs
+    const bool writer = live && (!PAIR || !(threadIdx.x & 1));
     const int nn_k = c.nn_k;
     float u[kK];
     float S = 0.f;
@@ -159,14 +163,14 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         if constexpr (MF && !DX) {   // a training decoder: the sdf on the matrix cores, x [rows, 11] saved
             float gx[kF];
             sdf = mlp_sdf_mfma16<false, 0, kF>(m, x, gx);
-            if (live) {
+            if (writer) {
 #pragma unroll
                 for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
             }
         } else if constexpr (MF) {   // save s dsdf/dx over the features for the backward (PIN_TRAIN_DX: [rows, 8])
             float gx[kF];
             sdf = mlp_sdf_mfma16<true, 0, kF>(m, x, gx);
-            if (live) {
+            if (writer) {
                 float4* xo = (float4*)(st.x + t * kF);
                 xo[0] = make_float4(gx[0], gx[1], gx[2], gx[3]);
                 xo[1] = make_float4(gx[4], gx[5], gx[6], gx[7]);
@@ -174,11 +178,13 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         } else {
             float gx[kD];
             sdf = mlp_sdf<false, 0, kD>(m, x, gx);
+            if (writer) {
 #pragma unroll
-            for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+                for (int d = 0; d < kD; ++d) st.x[t * kD + d] = x[d];
+            }
         }
     }
-    if (live) st.sdf[r] = sdf;
+    if (writer) st.sdf[r] = sdf;
 }
 
 // End of a training forward (all lanes of every wave, each wave on its own 64 rows -- no block
@@ -188,23 +194,29 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
 // neighbour at a 4 nn_k-B stride, which cost ~115 us of the 1.68M-row forward).  The training
 // side effects are applied by the backward (train_side_effects) from these arrays.
 // t0: the processing slot of the block's first row.
+template <bool PAIR = false>
 __device__ __forceinline__ void flush_rows(const PinTrainCfg& c, const PinTrainState& st, int64_t t0, int64_t rows,
                                            const int (&cid)[kK], const float (&cw)[kK]) {
+    // pair mode: 32 rows per wave, staged by the even lanes
+    constexpr int R = PAIR ? 32 : 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int* const s_id = wave_list();
     float* const s_w = (float*)(s_id + 64 * kK);
     static_assert(kListSeg * 64 >= 2 * 64 * kK, "flush staging must fit the wave's scan list");
     wave_lds_sync();   // the slice was the scan list / decoder scratch: every lane is past its reads
+    if (!PAIR || !(lane & 1)) {
+        const int lr = PAIR ? lane >> 1 : lane;
 #pragma unroll
-    for (int j = 0; j < kK; ++j) {
-        s_id[lane * kK + j] = cid[j];
-        s_w[lane * kK + j] = cw[j];
+        for (int j = 0; j < kK; ++j) {
+            s_id[lr * kK + j] = cid[j];
+            s_w[lr * kK + j] = cw[j];
+        }
     }
     wave_lds_sync();
-    const int64_t tw = t0 + 64 * wave;   // the wave's first slot
+    const int64_t tw = t0 + R * wave;   // the wave's first slot
     if (tw >= rows) return;
     const int nn_k = c.nn_k;
-    const int nr = (int)(rows - tw < 64 ? rows - tw : 64);
+    const int nr = (int)(rows - tw < R ? rows - tw : R);
     int* __restrict__ ido = st.ids + tw * nn_k;
     float* __restrict__ wo = st.weights + tw * nn_k;
     if (nn_k == kK) {
@@ -246,25 +258,29 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
 #else
 #define PIN_FWD_WAVES_ATTR
 #endif
-template <bool WF, bool MF, bool DX = MF>
+// PAIR (PIN_TRAIN_PAIR, small batches): two lanes per row -- the candidate list split between
+// them (GridSource::scan_pair) -- so a batch of ~1 wave per SIMD runs twice the waves with half
+// the scan chain each.
+template <bool WF, bool MF, bool DX = MF, bool PAIR = false>
 __global__ void __launch_bounds__(kTBlock) PIN_FWD_WAVES_ATTR
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
     const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
-    const int64_t t = xcd_block() * kTBlock + threadIdx.x;
+    const int64_t tl = xcd_block() * kTBlock + threadIdx.x;   // lane slot
+    const int64_t t = PAIR ? tl >> 1 : tl;                     // row slot
     const int64_t rows = c.n_main + 6 * c.n_stencil;
     int cid[kK];
     float cw[kK];
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
+    if ((MF || PAIR) ? (tl & ~(int64_t)63) < (PAIR ? 2 * rows : rows) : t < rows) {
         const GridSource<false, PIN_TRAIN_IDP> src(g, p);
-        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF, DX>(src, p, mw, coord, ts, c, t, st, cid, cw,
-                                                                     t < rows);
+        train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF, DX, PAIR>(src, p, mw, coord, ts, c, t, st, cid,
+                                                                           cw, t < rows);
     }
-    flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
+    flush_rows<PAIR>(c, st, (xcd_block() * kTBlock) >> (PAIR ? 1 : 0), rows, cid, cw);
 }
 
 __global__ void __launch_bounds__(kTBlock)
@@ -1620,8 +1636,17 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
             hipLaunchKernelGGL((KERNEL<false, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,    \
                                coord, ts, *cfg, *st);                                                           \
     } while (0)
-    if (grid) PIN_LAUNCH_FWD(k_train_forward_grid, grid);
-    else PIN_LAUNCH_FWD(k_train_forward_hash, hash);
+    if (grid && (cfg->flags & PIN_TRAIN_PAIR) && cfg->weighted_first && mlp->packed && (dx || kTrainFwdMf)) {
+        // small batch: two lanes per row (k_train_forward_grid's PAIR)
+        if (dx) hipLaunchKernelGGL((k_train_forward_grid<true, true, true, true>), grid_for(2 * rows), dim3(kTBlock), 0,
+                                   s, *grid, *pts, *mlp, coord, ts, *cfg, *st);
+        else hipLaunchKernelGGL((k_train_forward_grid<true, true, false, true>), grid_for(2 * rows), dim3(kTBlock), 0,
+                                s, *grid, *pts, *mlp, coord, ts, *cfg, *st);
+    } else if (grid) {
+        PIN_LAUNCH_FWD(k_train_forward_grid, grid);
+    } else {
+        PIN_LAUNCH_FWD(k_train_forward_hash, hash);
+    }
 #undef PIN_LAUNCH_FWD
     return launch_status();
 }

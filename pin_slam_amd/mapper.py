@@ -43,6 +43,8 @@ _TRAIN_TILE_MIN = int(os.environ.get("PIN_TRAIN_TILE_MIN", str(_TILE_MIN)))
 # pairs on one point, whose memory-side float atomics serialise on its address line
 _REPLICA_ROWS = int(os.environ.get("PIN_TRAIN_REPLICA_ROWS", str(1 << 18)))
 _REPLICAS = int(os.environ.get("PIN_TRAIN_REPLICAS", "8"))
+# batches below this many rows run the forward with two lanes per row (PIN_TRAIN_PAIR)
+_PAIR_ROWS = int(os.environ.get("PIN_TRAIN_PAIR_ROWS", str(1 << 17)))
 # the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
 _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 
@@ -810,6 +812,8 @@ class Mapper:
         # gradient + ReLU masks of the decoder-parameter products)
         mv = P.mv = mlp_view(self.geo_mlp,
                              packed=_MLP_PACK and (mlp_grad is None or (wf and not analytic and _ROW_DECODE)))
+        if rows < _PAIR_ROWS:
+            cfg.flags |= _lib.PIN_TRAIN_PAIR
         if dx:
             cfg.flags |= _lib.PIN_TRAIN_DX
         if analytic:

@@ -125,6 +125,39 @@ def test_mapping_call_fixture(golden, dev, backend, case, monkeypatch):
                                    err_msg=key)
 
 
+@pytest.mark.parametrize("frozen", [True, False])
+def test_pair_forward_equals_one_lane_per_row(dev, frozen, monkeypatch):
+    """PIN_TRAIN_PAIR (two lanes per row, the candidate list split and merged in reference order):
+    the forward's saved state -- neighbour ids, weights, sdf, x -- bitwise that of one lane per
+    row, on a batch with many equal-distance candidates (grid-aligned queries); frozen decoder
+    (PIN_TRAIN_DX) and training decoder (matrix-core sdf, x saved)."""
+    import pin_slam_amd.mapper as M
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    res = []
+    for pair in (False, True):
+        monkeypatch.setattr(M, "_PAIR_ROWS", 1 << 30 if pair else 0)
+        nm, dec, pts = surface_map(300, device=dev, weighted_first=True, buffer_size=1 << 22, query_backend="grid")
+        if frozen:
+            for p in dec.parameters():
+                p.requires_grad_(False)
+        coord, label, ts = surface_pool(pts, 20000, device=dev)
+        # a quarter of the rows on voxel corners: equidistant neighbours (ties in the top-k)
+        r = float(nm.resolution)
+        coord[::4] = torch.round(coord[::4] / r) * r
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        fg = torch.zeros_like(nm.local_geo_features.data)
+        mg = None if frozen else torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev)
+        loss = float(mapper.train_step(coord, label, ts, fg, mg))
+        b = mapper._buf
+        rows = b.sdf.shape[0]
+        used = b.x.view(-1)[: rows * (8 if frozen else 11)]   # PIN_TRAIN_DX: [rows, 8] in the [rows, 11] buffer
+        res.append((loss, b.ids.clone(), b.weights.clone(), b.sdf.clone(), used.clone(), fg))
+    (l0, i0, w0, s0, x0, f0), (l1, i1, w1, s1, x1, f1) = res
+    assert torch.equal(i0, i1) and torch.equal(w0, w1) and torch.equal(s0, s1) and torch.equal(x0, x1)
+    assert l1 == pytest.approx(l0, rel=1e-9)
+    np.testing.assert_allclose(_np(f1), _np(f0), rtol=1e-4, atol=1e-9)
+
+
 @pytest.mark.parametrize("wf", [True, False])
 def test_train_step_tile_order_invisible(dev, wf, monkeypatch):
     """Large batches are processed in tile order (pin_train_rows + pin_query_sort): per-row sdf
