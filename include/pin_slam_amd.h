@@ -516,7 +516,9 @@ typedef struct PinAdamStep {
     float one_minus_beta2;
     float bias_correction2_sqrt; /* float32(sqrt(1 - beta2^t)) */
     float eps;                   /* adam_eps */
-    int32_t zero_grad;           /* 1: grad := 0 after the step (opt.zero_grad of the next iteration) */
+    int32_t zero_grad;           /* bit 0: grad := 0 after the step (opt.zero_grad of the next iteration);
+                                    bit 1: the first step of a fresh optimiser -- exp_avg / exp_avg_sq
+                                    are taken as zero, not read (they may hold anything) */
     int32_t grad_stride;         /* element i's gradient is grad[(i/8)*grad_stride + i%8] (8: contiguous) */
 } PinAdamStep;
 

@@ -1311,7 +1311,9 @@ __device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ p
     if (i0 >= n) return;
     if (i0 + 4 <= n) {
         const int64_t gi = a.grad_stride == 8 ? i0 : (i0 >> 3) * a.grad_stride + (i0 & 7);
-        float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + gi), m = *(float4*)(m_ + i0), v = *(float4*)(v_ + i0);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + gi);
+        float4 m = (a.zero_grad & 2) ? z : *(float4*)(m_ + i0), v = (a.zero_grad & 2) ? z : *(float4*)(v_ + i0);
         adam_one(p.x, g.x, m.x, v.x, a);
         adam_one(p.y, g.y, m.y, v.y, a);
         adam_one(p.z, g.z, m.z, v.z, a);
@@ -1323,7 +1325,7 @@ __device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ p
         return;
     }
     for (int64_t i = i0; i < n; ++i) {   // tail (contiguous layout only: strided needs n % 8 == 0)
-        float p = prm[i], m = m_[i], v = v_[i];
+        float p = prm[i], m = (a.zero_grad & 2) ? 0.f : m_[i], v = (a.zero_grad & 2) ? 0.f : v_[i];
         adam_one(p, grad[i], m, v, a);
         prm[i] = p;
         m_[i] = m;
@@ -1346,7 +1348,9 @@ k_adam_rows(float* __restrict__ prm, float* __restrict__ grad, float* __restrict
     const int64_t t = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (t >= 2 * nrows) return;
     const int64_t i0 = rows[t >> 1] * kF + 4 * (t & 1);
-    float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + i0), m = *(float4*)(m_ + i0), v = *(float4*)(v_ + i0);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p = *(float4*)(prm + i0), g = *(float4*)(grad + i0);
+    float4 m = (a.zero_grad & 2) ? z : *(float4*)(m_ + i0), v = (a.zero_grad & 2) ? z : *(float4*)(v_ + i0);
     adam_one(p.x, g.x, m.x, v.x, a);
     adam_one(p.y, g.y, m.y, v.y, a);
     adam_one(p.z, g.z, m.z, v.z, a);
@@ -1375,7 +1379,7 @@ __device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg,
 #pragma unroll
     for (int k = 1; k < kMaxSeg; ++k) s += (k < sg.n && t >= sg.off[k]) ? 1 : 0;
     float* prm = sg.p[s] + (t - sg.off[s]);
-    float p = *prm, m = m_[t], v = v_[t];
+    float p = *prm, m = (a.zero_grad & 2) ? 0.f : m_[t], v = (a.zero_grad & 2) ? 0.f : v_[t];
     adam_one(p, grad[t], m, v, a);
     *prm = p;
     m_[t] = m;

@@ -548,13 +548,25 @@ class Mapper:
         dev = feats.device
         # fresh optimiser state per call (utils/tools.py:89-116 via mapper.py:441)
         fdata = feats.data
-        # gradient and moments (and the decoder's) zeroed in one fill
+        # gradient and moments (and the decoder's) zeroed in one fill; the dense fused loop's first
+        # Adam step takes the moments as zero (PinAdamStep.zero_grad bit 1), so only the gradients
+        # are filled there
+        fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
+        dense_loop = fused and (world <= 1 or getattr(self, "shard", "dense") != "space")
         nf, nmg = fdata.numel(), (_lib.MLP_GRAD_SIZE if train_mlp else 0)
-        state = torch.zeros((3 * nf + 3 * nmg,), dtype=torch.float32, device=dev)
-        f_grad, f_m, f_v = (state[k * nf:(k + 1) * nf].view_as(fdata) for k in range(3))
-        m_grad = m_m = m_v = None
-        if train_mlp:
-            m_grad, m_m, m_v = (state[3 * nf + k * nmg:3 * nf + (k + 1) * nmg] for k in range(3))
+        if dense_loop:
+            grads = torch.zeros((nf + nmg,), dtype=torch.float32, device=dev)
+            moments = torch.empty((2 * nf + 2 * nmg,), dtype=torch.float32, device=dev)
+            f_grad, f_m, f_v = grads[:nf].view_as(fdata), moments[:nf].view_as(fdata), moments[nf:2 * nf].view_as(fdata)
+            m_grad = m_m = m_v = None
+            if train_mlp:
+                m_grad, m_m, m_v = grads[nf:], moments[2 * nf:2 * nf + nmg], moments[2 * nf + nmg:]
+        else:
+            state = torch.zeros((3 * nf + 3 * nmg,), dtype=torch.float32, device=dev)
+            f_grad, f_m, f_v = (state[k * nf:(k + 1) * nf].view_as(fdata) for k in range(3))
+            m_grad = m_m = m_v = None
+            if train_mlp:
+                m_grad, m_m, m_v = (state[3 * nf + k * nmg:3 * nf + (k + 1) * nmg] for k in range(3))
         cert_before = nm.local_point_certainties.clone() if world > 1 else None
         self._adam_t = 0
         # get_batch's gathers fused into the row build (pin_train_gather) when the pools allow it;
@@ -644,7 +656,10 @@ class Mapper:
             if world > 1:
                 allreduce_gradients([f_grad, m_grad], group)
             self._adam_t += 1
-            _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(adam_scalars(c.lr, self._adam_t, c.adam_eps)), s))
+            # the first step of the call's fresh optimiser: the moments are taken as zero (mapping()
+            # leaves them unfilled for this loop)
+            st = adam_scalars(c.lr, self._adam_t, c.adam_eps, zero_grad=3 if self._adam_t == 1 else 1)
+            _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(st), s))
         return plan
 
     def _slab_partition(self, world, fused):

@@ -333,6 +333,36 @@ def test_train_adam_equals_replica_sum_segments_and_pack(dev):
     assert torch.equal(packs[0], packs[1])
 
 
+def test_fresh_moments_flag_equals_zero_moments(dev):
+    """PinAdamStep.zero_grad bit 1 (the first step of a fresh optimiser): moments holding garbage
+    are taken as zero -- bitwise the step on zeroed moments; features and decoder segments."""
+    import ctypes
+    from pin_slam_amd.mapper import adam_scalars
+    g = torch.Generator(device="cpu").manual_seed(5)
+    n, sizes = 8 * 999, [704, 64, 64, 1]
+    p0, gr = torch.randn(n, generator=g).to(dev), torch.randn(n, generator=g).to(dev)
+    seg0 = [torch.randn(k, generator=g).to(dev) for k in sizes]
+    sgr = torch.randn(sum(sizes), generator=g).to(dev)
+    out = []
+    for fresh in (False, True):
+        p, gg = p0.clone(), gr.clone()
+        m = torch.full_like(p, float("nan")) if fresh else torch.zeros_like(p)
+        v = torch.full_like(p, float("nan")) if fresh else torch.zeros_like(p)
+        seg = [t.clone() for t in seg0]
+        sg = sgr.clone()
+        sm = torch.full_like(sg, float("nan")) if fresh else torch.zeros_like(sg)
+        sv = torch.full_like(sg, float("nan")) if fresh else torch.zeros_like(sg)
+        ptrs = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in seg])
+        szs = (ctypes.c_int64 * 4)(*sizes)
+        st = adam_scalars(0.01, 1, 1e-15, zero_grad=3 if fresh else 1)
+        _lib.call("pin_adam_step_train", _lib.ptr(p), _lib.ptr(gg), _lib.ptr(m), _lib.ptr(v), n, None, 0, ptrs, szs, 4,
+                  _lib.ptr(sg), _lib.ptr(sm), _lib.ptr(sv), None, None, ctypes.byref(st), _lib.stream())
+        torch.cuda.synchronize()
+        out.append([p, m, v, sm, sv] + seg)
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_split_gather_equals_concatenated_index(dev):
     """pin_train_gather_packed_split (get_batch's history draw + new_idx[draw], utils/mapper.py:
     335-340) against pin_train_gather_packed over the torch.cat of the same rows: bitwise equal
