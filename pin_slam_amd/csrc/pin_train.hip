@@ -1373,7 +1373,7 @@ struct AdamSegs {
 // one element of the segments (k_adam_segments, k_adam_step_segments)
 __device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg, float* __restrict__ grad,
                                                   float* __restrict__ m_, float* __restrict__ v_,
-                                                  const PinAdamStep& a) {
+                                                  const PinAdamStep& a, float* copy = nullptr) {
     if (t >= sg.off[sg.n]) return;
     int s = 0;
 #pragma unroll
@@ -1382,6 +1382,7 @@ __device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg,
     float p = *prm, m = (a.zero_grad & 2) ? 0.f : m_[t], v = (a.zero_grad & 2) ? 0.f : v_[t];
     adam_one(p, grad[t], m, v, a);
     *prm = p;
+    if (copy) copy[t] = p;   // the stepped value, also into a block-local copy (k_adam_train)
     m_[t] = m;
     v_[t] = v;
     if (a.zero_grad) grad[t] = 0.f;
@@ -1430,11 +1431,26 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
         adam_dense_body(bid * kTBlock + threadIdx.x, prm, grad, m_, v_, n, a);
         return;
     }
-    for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a);
+    // with the decoder's layout (W1 | b1 | W2 | b2 end to end, checked by the host) the stepped
+    // values also go to LDS, and the pack reads them there (no global round trip behind a fence)
+    __shared__ float s_dec[kMlpGrad];
+    const bool lds = out && sg.n == 4 && sg.off[4] == kMlpGrad && sg.off[1] == kH * kD && sg.off[2] == kH * kD + kH &&
+                     sg.off[3] == kH * kD + 2 * kH;
+    for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a, lds ? s_dec : nullptr);
     if (out) {
-        __threadfence();   // the stepped parameters, read back by the pack below (other threads' writes)
-        __syncthreads();
-        mlp_pack_block(mlp, out);
+        if (lds) {
+            __syncthreads();
+            PinMlp ml = mlp;
+            ml.W1 = s_dec;
+            ml.b1 = s_dec + kH * kD;
+            ml.W2 = s_dec + kH * kD + kH;
+            ml.b2 = s_dec + kH * kD + 2 * kH;
+            mlp_pack_block(ml, out);
+        } else {
+            __threadfence();   // the stepped parameters, read back by the pack below (other threads' writes)
+            __syncthreads();
+            mlp_pack_block(mlp, out);
+        }
     }
 }
 
