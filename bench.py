@@ -47,6 +47,7 @@ N_SIDE = 1000            # 1,000,000 neural points
 N_QUERY = 262144
 BYTES_PER_QUERY = 944    # SURVEY.md 8(d), Kc=33, k=8, F=8
 HBM_PEAK = 8.0e12        # MI355X_MICROARCH.md (spec)
+REF_CPU_QPS = 0.37e6     # the reference's SDF+grad queries/s on 8 Xeon cores (configs[1])
 MAPPER_SIDE = 2000       # 4,000,000 neural points (configs[3])
 MAPPER_BS = 1 << 20      # 1M sampled queries per iteration per GPU
 MAPPER_POOL = 1 << 22    # training-sample pool
@@ -127,9 +128,12 @@ def parse():
     ap.add_argument("--mapper-steps", type=int, default=10)
     ap.add_argument("--no-mapper-nwf", action="store_true",
                     help="skip the per-neighbour-decoding mapper leg (weighted_first False, configs[3] sizes)")
-    ap.add_argument("--mapper-shard", default="space", choices=["space", "dense"],
-                    help="N > 1 mapper data parallelism: owner-partitioned slabs with halo exchange (space) or "
-                         "the dense all-reduce of the feature gradient")
+    ap.add_argument("--mapper-shard", default="dense", choices=["space", "dense"],
+                    help="N > 1 mapper data parallelism of the 'mapper' leg: the dense all-reduce of the feature "
+                         "gradient over RCCL (north_star's design, default) or owner-partitioned cells with halo "
+                         "exchange (space); the other mode is reported beside it unless --no-mapper-alt")
+    ap.add_argument("--no-mapper-alt", action="store_true",
+                    help="N > 1: skip the mapper leg of the other shard mode")
     ap.add_argument("--mapper-warmup", type=int, default=3)
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="PMC-measured HBM bytes per launch (from profiles/), reported as roofline.traffic")
@@ -695,7 +699,12 @@ def _shard_info(mapper):
                      "unbiased estimate of one reference batch (DESIGN.md section 6)"}
 
 
-def mapper_leg(args, dev, world, rank, wf=None):
+def _ar_buckets():
+    from pin_slam_amd.mapper import _AR_BUCKETS
+    return _AR_BUCKETS
+
+
+def mapper_leg(args, dev, world, rank, wf=None, shard=None):
     """configs[3]: Mapper.mapping on a 4M-point map, 1M sampled queries per iteration per GPU
     (+ 6 x 100K numerical-gradient stencil rows), BCE + 0.5 eikonal, Adam on the features
     (decoder frozen, the steady state after freeze_after_frame).  W > 1 (weak scaling, 1M queries
@@ -709,7 +718,7 @@ def mapper_leg(args, dev, world, rank, wf=None):
     for p in dec.parameters():
         p.requires_grad_(False)
     coord, label, ts = surface_pool(pts, MAPPER_POOL, seed=11 + rank, device=dev)
-    shard = args.mapper_shard if world > 1 else "dense"
+    shard = (shard or args.mapper_shard) if world > 1 else "dense"
     mapper = P.Mapper(nm.config, None, nm, dec, group=dist.group.WORLD if world > 1 else None, shard=shard)
     L = int(nm.local_neural_points.shape[0])
     mapper.set_pool(coord, label, ts)
@@ -737,9 +746,10 @@ def mapper_leg(args, dev, world, rank, wf=None):
            "config": {"workload": "Mapper.mapping, 4M-point map, 1M queries/iter/GPU + numerical-gradient "
                                   "stencil (configs[3])", "map_points": int(pts.shape[0]),
                       "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",
-                      "weighted_first": wf,
+                      "weighted_first": wf, "data_parallel": shard if world > 1 else None,
                       "grad_allreduce": (f"{dist.get_backend()} all_reduce SUM of the [L+1,8] f32 gradient "
-                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter)") if world > 1 and shard == "dense"
+                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter) in {_ar_buckets()} row buckets, Adam "
+                                         f"on each bucket as soon as it is reduced") if world > 1 and shard == "dense"
                       else None,
                       "shard": (_shard_info(mapper) if world > 1 and shard == "space" else None),
                       "candidate_backend": backend, "timed": "mapping(K): K iterations + Adam state init + "
@@ -891,9 +901,26 @@ def main():
         out["slam_frame"] = slam_frame_leg(args, dev, world, rank)
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)
+        if world > 1 and not args.no_mapper_alt:
+            # both data-parallel designs in one line: the dense gradient all-reduce (north_star's
+            # RCCL step) and the owner-partitioned cells with halo exchange
+            alt = "space" if args.mapper_shard == "dense" else "dense"
+            out["mapper_" + alt] = mapper_leg(args, dev, world, rank, shard=alt)
     if not args.no_mapper and not args.no_mapper_nwf and not args.nwf:
         # per-neighbour decoding (weighted_first False: run_kitti / mulran / ncd_128 / livox .yaml)
         out["mapper_nwf"] = mapper_leg(args, dev, world, rank, wf=False)
+    # speed-up over the CPU baseline measured in the same run (BASELINE.md's CPU-baseline plan: "speed-up"
+    # per config); at N > 1 no CPU baseline runs, and the headline is set against BASELINE.md's own
+    # measurement of the reference (0.37M SDF+grad queries/s on 8 cores)
+    if "cpu_baseline" in out:
+        out["vs_baseline"] = value / out["cpu_baseline"]["value"]
+        out["vs_baseline_basis"] = "value / cpu_baseline.value (same run)"
+    else:
+        out["vs_baseline"] = value / REF_CPU_QPS
+        out["vs_baseline_basis"] = "value / 0.37M q/s (BASELINE.md: the reference on 8 CPU cores)"
+    for leg in out.values():
+        if isinstance(leg, dict) and isinstance(leg.get("cpu_baseline"), dict) and "value" in leg:
+            leg["vs_baseline"] = leg["value"] / leg["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -380,6 +380,18 @@ int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, in
                    void* stream);
 
 /*
+ * pin_query_sort_stable -- pin_query_sort's tiles (same tile map), but a STABLE sort: inside a
+ * tile the queries keep their input order, so the processing order is a function of the batch
+ * alone (the deterministic training mode: per-block decoder-gradient partials and per-wave loss
+ * partials then sum the same rows in the same order on every run).  A radix sort of the tile keys
+ * (rocPRIM, several launches): slower than the counting sort.  workspace:
+ * pin_query_sort_stable_workspace_bytes(n) bytes, no state kept between calls.
+ */
+int64_t pin_query_sort_stable_workspace_bytes(int64_t n);
+int pin_query_sort_stable(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
+                          void* stream);
+
+/*
  * pin_query_sdf_grid -- pin_query_sdf with candidates from the occupancy grid.  order (n ints,
  * may be NULL = input order): the order in which queries are processed (pin_query_order);
  * outputs always go to each query's own index.
@@ -506,6 +518,20 @@ typedef struct PinTrainState {
     int32_t replica_mode;        /* 0: pin_train_backward adds the replicas into grad_features itself;
                                     1: it leaves them, and the caller's pin_adam_step_train takes the
                                     gradient as grad_features + the replicas' sum (one launch less) */
+    /* Deterministic accumulation: with grad_fixed non-NULL the feature
+     * terms are added as 64-bit fixed-point integers, round(term * 2^fixed_shift), into
+     * grad_fixed [max(replicas, 1), L+1, 8] (zero on the first call) instead of float atomics into
+     * grad_features / grad_replicas.  Integer addition is associative, so the sum does not depend on
+     * the order the atomics arrive in: the gradient is a function of the batch alone, bitwise.  It
+     * reaches grad_features as float(sum * 2^-fixed_shift) through pin_train_backward (replica_mode
+     * 0) or pin_adam_step_train (replica_mode 1), which zero the integers again.  With cert_fixed
+     * non-NULL the certainty side effect goes the same way into cert_fixed [L] (shift cert_shift),
+     * and the caller folds it into the certainties with pin_fixed_accumulate (certainties is then
+     * not written).  Terms beyond +-2^(62 - shift) saturate. */
+    int64_t* grad_fixed;
+    int64_t* cert_fixed;
+    int32_t fixed_shift;         /* e.g. 50: resolution 8.9e-16, range +-8192 */
+    int32_t cert_shift;          /* e.g. 32 */
 } PinTrainState;
 
 /* Scalars of one torch.optim.Adam step (utils/tools.py:111-112; betas (0.9, 0.99)). */
@@ -617,11 +643,19 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
  * features' gradient is grad + the sum of the [replicas, n] replicas, which are zeroed again.
  * mlp / packed (non-NULL, nseg > 0): the same block then writes the stepped decoder's
  * pin_mlp_pack image (no pin_mlp_pack call before the next forward).  grad_stride must be 8.
+ * grad_fixed (non-NULL; grad_replicas must then be NULL): the deterministic mode's fixed-point
+ * replicas of PinTrainState.grad_fixed, [max(replicas, 1), n] int64 at shift fixed_shift: the
+ * gradient is grad + float(their integer sum * 2^-fixed_shift), and they are zeroed again.
  */
 int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                        float* grad_replicas, int32_t replicas, float* const* params, const int64_t* sizes,
-                        int nseg, float* seg_grad, float* seg_exp_avg, float* seg_exp_avg_sq, const PinMlp* mlp,
-                        void* packed, const PinAdamStep* a, void* stream);
+                        float* grad_replicas, int32_t replicas, int64_t* grad_fixed, int32_t fixed_shift,
+                        float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
+                        float* seg_exp_avg_sq, const PinMlp* mlp, void* packed, const PinAdamStep* a, void* stream);
+
+/* pin_fixed_accumulate -- out[i] += float((sum_k acc[k n + i]) * 2^-shift) for k < max(nrep, 1),
+ * then acc := 0: folds the deterministic mode's fixed-point accumulators (PinTrainState.grad_fixed
+ * / cert_fixed) into a float array.  The integer sum is exact; the result is rounded once. */
+int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, float* out, void* stream);
 /* pin_adam_segments -- the same Adam update over nseg (<= 8) separate parameter tensors params[k]
  * of sizes[k] floats whose gradients and moments lie end to end in contiguous grad / exp_avg /
  * exp_avg_sq (the decoder's W1, b1, W2, b2 against pin_train_backward's mlp_grad): one launch

@@ -96,7 +96,8 @@ class PinTrainState(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("weights", c_void_p), ("x", c_void_p), ("sdf", c_void_p),
                 ("certainties", c_void_p), ("ts_update", c_void_p), ("order", c_void_p), ("sorted_rows", c_void_p),
                 ("row_weight", c_void_p), ("eik_coef", c_void_p), ("eik_vec", c_void_p), ("row_ts", c_void_p),
-                ("grad_replicas", c_void_p), ("replicas", i32), ("replica_mode", i32)]
+                ("grad_replicas", c_void_p), ("replicas", i32), ("replica_mode", i32),
+                ("grad_fixed", c_void_p), ("cert_fixed", c_void_p), ("fixed_shift", i32), ("cert_shift", i32)]
 
 
 class PinAdamStep(ctypes.Structure):
@@ -149,6 +150,8 @@ _SIGS = {
     "pin_mlp_pack": [_P(PinMlp), c_void_p, c_void_p],
     "pin_query_order": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p],
     "pin_query_sort": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_sort_stable_workspace_bytes": [i64],
+    "pin_query_sort_stable": [_P(PinGrid), c_void_p, i64, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_tiled": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_sdf_grid_sorted": [_P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, i64, i32, i32, i32, c_void_p,
@@ -179,8 +182,9 @@ _SIGS = {
                            c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
     "pin_adam_rows": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(PinAdamStep), c_void_p],
-    "pin_adam_step_train": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, i32, _P(c_void_p), _P(i64), i32,
-                            c_void_p, c_void_p, c_void_p, _P(PinMlp), c_void_p, _P(PinAdamStep), c_void_p],
+    "pin_adam_step_train": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, i32, c_void_p, i32, _P(c_void_p),
+                            _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinMlp), c_void_p, _P(PinAdamStep), c_void_p],
+    "pin_fixed_accumulate": [c_void_p, i32, i64, i32, c_void_p, c_void_p],
     "pin_adam_segments": [_P(c_void_p), _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
     "pin_adam_step_segments": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(c_void_p), _P(i64), i32, c_void_p,
                                c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
@@ -197,7 +201,8 @@ _SIGS = {
     "pin_map_adjust": [_P(PinMapArrays), c_void_p, i64, i32, c_void_p],
 }
 # functions whose return value is not a status code
-_RESTYPES = {"pin_map_workspace_bytes": i64, "pin_mc_workspace_bytes": i64}
+_RESTYPES = {"pin_map_workspace_bytes": i64, "pin_mc_workspace_bytes": i64,
+             "pin_query_sort_stable_workspace_bytes": i64}
 
 _lib = None
 

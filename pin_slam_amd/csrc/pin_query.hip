@@ -13,6 +13,8 @@
 #include <type_traits>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "pin_device.h"
 
 // Per-neighbour decoder (weighted_first False) of the fused grid kernel as one f32-MFMA GEMM per
@@ -669,6 +671,61 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
 
+// The stable tile sort (pin_query_sort_stable): tile keys, a rocPRIM radix sort of (key, index)
+// pairs over the key bits -- LSD radix sorting is stable, so a tile keeps its queries in input
+// order -- then the placement.  Same tile map as sort_queries.
+constexpr int kStableKeyBits = 14;
+static_assert((1 << kStableKeyBits) >= kMaxTilesLarge && (1 << kStableKeyBits) >= kMaxTiles, "tile key bits");
+
+__global__ void __launch_bounds__(kBlock)
+k_tile_keys(const float* __restrict__ q, int64_t n, TileMap t, unsigned* __restrict__ keys,
+            unsigned* __restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (unsigned)tile_of(q[3 * i], q[3 * i + 1], q[3 * i + 2], t);
+    vals[i] = (unsigned)i;
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_tile_place_stable(const float* __restrict__ q, int64_t n, const unsigned* __restrict__ vals,
+                    float4* __restrict__ q4, int* __restrict__ order) {
+    const int64_t pos = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (pos >= n) return;
+    const int64_t i = vals[pos];
+    if (q4) q4[pos] = make_float4(q[3 * i], q[3 * i + 1], q[3 * i + 2], __int_as_float((int)i));
+    if (order) order[pos] = (int)i;
+}
+
+struct StableSortWs {
+    unsigned *k_in, *k_out, *v_in, *v_out;
+    void* temp;
+    size_t temp_bytes;
+};
+
+size_t stable_sort_temp_bytes(int64_t n) {
+    size_t bytes = 0;
+    if (rocprim::radix_sort_pairs(nullptr, bytes, (unsigned*)nullptr, (unsigned*)nullptr, (unsigned*)nullptr,
+                                  (unsigned*)nullptr, (size_t)std::max<int64_t>(n, 1), 0, kStableKeyBits,
+                                  (hipStream_t)0) != hipSuccess)
+        return 0;
+    return bytes;
+}
+
+inline int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+StableSortWs stable_sort_ws(void* ws, int64_t n) {
+    char* p = (char*)ws;
+    const int64_t a = align256(4 * std::max<int64_t>(n, 1));
+    StableSortWs w;
+    w.k_in = (unsigned*)p;
+    w.k_out = (unsigned*)(p + a);
+    w.v_in = (unsigned*)(p + 2 * a);
+    w.v_out = (unsigned*)(p + 3 * a);
+    w.temp = p + 4 * a;
+    w.temp_bytes = stable_sort_temp_bytes(n);
+    return w;
+}
+
 // ------------------------------------------------------------------ drop-in query_feature
 template <bool WF, bool PGO, class Src>
 __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoints& p, const float* __restrict__ q,
@@ -1038,6 +1095,31 @@ int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, in
     if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || !q4 || !workspace)) || n > INT32_MAX) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
     return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
+}
+
+int64_t pin_query_sort_stable_workspace_bytes(int64_t n) {
+    if (n < 0) return PIN_ERR_ARG;
+    const size_t t = stable_sort_temp_bytes(n);
+    if (t == 0) return PIN_ERR_HIP;
+    return 4 * align256(4 * std::max<int64_t>(n, 1)) + (int64_t)t;
+}
+
+int pin_query_sort_stable(const PinGrid* grid, const float* q, int64_t n, float* q4, int32_t* order, void* workspace,
+                          void* stream) {
+    if (!grid_ok(grid) || n < 0 || (n > 0 && (!q || (!q4 && !order) || !workspace)) || n > INT32_MAX)
+        return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    auto s = as_stream(stream);
+    const TileMap t = tile_map(*grid, n >= kLargeBatch ? kMaxTilesLarge : kMaxTiles);
+    StableSortWs w = stable_sort_ws(workspace, n);
+    if (w.temp_bytes == 0) return PIN_ERR_HIP;
+    hipLaunchKernelGGL(k_tile_keys, grid_for(n), dim3(kBlock), 0, s, q, n, t, w.k_in, w.v_in);
+    size_t tb = w.temp_bytes;
+    if (rocprim::radix_sort_pairs(w.temp, tb, w.k_in, w.k_out, w.v_in, w.v_out, (size_t)n, 0, kStableKeyBits, s) !=
+        hipSuccess)
+        return PIN_ERR_HIP;
+    hipLaunchKernelGGL(k_tile_place_stable, grid_for(n), dim3(kBlock), 0, s, q, n, w.v_out, (float4*)q4, (int*)order);
+    return launch_status();
 }
 
 // argument checks of the grid SDF query, before anything is launched (the tiled entry sorts first)

@@ -31,6 +31,18 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kTBlock - 1) / kTB
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline int launch_status() { return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP; }
 
+// Deterministic accumulation (PinTrainState.grad_fixed / cert_fixed): a float term as a 64-bit
+// fixed-point integer round(v * 2^shift) (the product is exact in f64; saturated at +-2^62), added
+// with integer atomics -- associative, so the sums do not depend on arrival order -- and turned
+// back into a float once, after the sum.
+__device__ __forceinline__ unsigned long long to_fixed(float v, double scale) {
+    double t = (double)v * scale;
+    t = fmin(fmax(t, -4.611686018427387904e18), 4.611686018427387904e18);
+    return (unsigned long long)__double2ll_rn(t);
+}
+__device__ __forceinline__ float from_fixed(long long v, double inv_scale) { return (float)((double)v * inv_scale); }
+__device__ __forceinline__ double fixed_scale(int shift) { return (double)(1ull << (shift & 63)); }
+
 // row r of the iteration: a main query or a stencil query (x+,x-,y+,y-,z+,z- blocks)
 __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const PinTrainCfg& c, int64_t r, float& qx,
                                           float& qy, float& qz) {
@@ -675,11 +687,14 @@ struct SideTable {
     float* val;
     int* ts;
     int64_t* rts;
-    float* cert;
+    float* cert;                 // float certainty sums (NULL in the deterministic mode)
+    unsigned long long* cfix;    // deterministic mode: fixed-point certainty sums, one atomic per pair
+    double cscale;
     int64_t* ts_update;
     __device__ SideTable(int* buf, const PinTrainState& st)
         : tag(buf), val((float*)(buf + kCertSlots)), ts(buf + 2 * kCertSlots), rts((int64_t*)(buf + 3 * kCertSlots)),
-          cert(st.certainties), ts_update(st.row_ts ? st.ts_update : nullptr) {}
+          cert(st.cert_fixed ? nullptr : st.certainties), cfix((unsigned long long*)st.cert_fixed),
+          cscale(fixed_scale(st.cert_shift)), ts_update(st.row_ts ? st.ts_update : nullptr) {}
     // all threads, then a barrier before any claim: empty slots; thread tid's row ts (batch rows
     // only -- the stencil rows' query carries none)
     __device__ void init(const PinTrainCfg& c, const PinTrainState& st, int nrow_blk, int64_t row) const {
@@ -697,6 +712,7 @@ struct SideTable {
     // after a barrier that follows every claim: pair (id, w) of local row lr
     __device__ void add(int id, float w, int lr) const {
         if (id < 0) return;
+        if (cfix) atomicAdd(cfix + id, to_fixed(w, cscale));
         const int k = id & (kCertSlots - 1);
         const int64_t q = rts[lr];
         if (tag[k] == id && q <= 0x7fffffff) {
@@ -910,7 +926,8 @@ __device__ __forceinline__ void decoder_backward(const MlpW& m, const float (&x)
 template <bool EIK>
 __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
                                                 int nrow_blk, const float* gst, const float* s_dsdf,
-                                                float* __restrict__ grad_features, int* buf, int64_t frows = 1) {
+                                                float* __restrict__ grad_features, unsigned long long* __restrict__ fdst,
+                                                double fscale, int* buf, int64_t frows = 1) {
     int* const s_ids = buf;
     float* const s_wt = (float*)(buf + kTBlock * kK);
     float* const s_al = (float*)(buf + 2 * kTBlock * kK);
@@ -939,7 +956,8 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
         float g;
         if (EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
         else g = s_wt[rj] * gst[lr * kF + d];
-        atomicAdd(grad_features + (int64_t)id * kF + d, g);
+        if (fdst) atomicAdd(fdst + (int64_t)id * kF + d, to_fixed(g, fscale));   // deterministic mode
+        else atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }
 
@@ -987,6 +1005,12 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     float* const gdst = (grad_features && st.grad_replicas && st.replicas > 1)
                             ? st.grad_replicas + (int64_t)(blockIdx.x % st.replicas) * p.rows * kF
                             : grad_features;
+    // the deterministic mode's fixed-point destination (its replica when replicas > 1)
+    unsigned long long* const fdst =
+        (grad_features && st.grad_fixed)
+            ? (unsigned long long*)st.grad_fixed + (st.replicas > 1 ? (int64_t)(blockIdx.x % st.replicas) * p.rows * kF : 0)
+            : nullptr;
+    const double fscale = fixed_scale(st.fixed_shift);
     const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;   // processing slot (per-slot state)
     const bool live = r < nrows;
     // the row it holds (sdf, label)
@@ -1137,7 +1161,9 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                 for (int u = 0; u < kF; ++u) {
                     const int e = u * 64 + lane;
                     const int rid = wid[e >> 3];
-                    if (rid >= 0) atomicAdd(gdst + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
+                    if (rid < 0) continue;
+                    if (fdst) atomicAdd(fdst + (int64_t)rid * kF + (e & (kF - 1)), to_fixed(wg[e], fscale));
+                    else atomicAdd(gdst + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
                 }
             }
         }
@@ -1174,14 +1200,30 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
 #endif
     if constexpr (WF) {
         if (grad_features) {
-            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, s_pair, p.rows);
+            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, fdst, fscale, s_pair, p.rows);
             __syncthreads();   // the staging is read: the table takes the buffer
         }
     }
 #if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1   // profiling variant: no side effects
     return;
 #endif
-    if (st.certainties || (st.ts_update && st.row_ts)) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
+    if (st.certainties || st.cert_fixed || (st.ts_update && st.row_ts))
+        train_side_effects(c, st, row0, nrow_blk, row, s_pair);
+}
+
+// out[i] += float(sum of the nrep fixed-point accumulators at i * 2^-shift); the accumulators are
+// zeroed (pin_fixed_accumulate, and the deterministic pin_train_backward with replica_mode 0)
+__global__ void __launch_bounds__(kTBlock)
+k_fixed_reduce(long long* __restrict__ acc, int nrep, int64_t n, int shift, float* __restrict__ out) {
+    const double inv = 1.0 / fixed_scale(shift);
+    for (int64_t e = (int64_t)blockIdx.x * kTBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kTBlock) {
+        long long s = 0;
+        for (int k = 0; k < nrep; ++k) {
+            s += acc[k * n + e];
+            acc[k * n + e] = 0;
+        }
+        out[e] += from_fixed(s, inv);
+    }
 }
 
 // grad += sum of the replicas, which are zeroed again (pin_train_backward with st.replicas > 1):
@@ -1321,7 +1363,7 @@ __device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ p
         *(float4*)(prm + i0) = p;
         *(float4*)(m_ + i0) = m;
         *(float4*)(v_ + i0) = v;
-        if (a.zero_grad) *(float4*)(grad + gi) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.zero_grad & 1) *(float4*)(grad + gi) = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
     for (int64_t i = i0; i < n; ++i) {   // tail (contiguous layout only: strided needs n % 8 == 0)
@@ -1330,7 +1372,7 @@ __device__ __forceinline__ void adam_dense_body(int64_t t, float* __restrict__ p
         prm[i] = p;
         m_[i] = m;
         v_[i] = v;
-        if (a.zero_grad) grad[i] = 0.f;
+        if (a.zero_grad & 1) grad[i] = 0.f;
     }
 }
 
@@ -1358,7 +1400,7 @@ k_adam_rows(float* __restrict__ prm, float* __restrict__ grad, float* __restrict
     *(float4*)(prm + i0) = p;
     *(float4*)(m_ + i0) = m;
     *(float4*)(v_ + i0) = v;
-    if (a.zero_grad) *(float4*)(grad + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.zero_grad & 1) *(float4*)(grad + i0) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // Adam over up to kMaxSeg separate parameter tensors whose gradients / moments lie end to end in
@@ -1385,7 +1427,7 @@ __device__ __forceinline__ void adam_segment_body(int64_t t, const AdamSegs& sg,
     if (copy) copy[t] = p;   // the stepped value, also into a block-local copy (k_adam_train)
     m_[t] = m;
     v_[t] = v;
-    if (a.zero_grad) grad[t] = 0.f;
+    if (a.zero_grad & 1) grad[t] = 0.f;
 }
 
 __global__ void __launch_bounds__(kTBlock)
@@ -1409,14 +1451,27 @@ k_adam_step_segments(float* __restrict__ prm, float* __restrict__ grad, float* _
 // their gradient plus the sum of the backward's replicas (zeroed again).
 __global__ void __launch_bounds__(kTBlock)
 k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restrict__ m_, float* __restrict__ v_,
-             int64_t n, int64_t nb_dense, float* __restrict__ rep, int nrep, AdamSegs sg, float* __restrict__ sgrad,
-             float* __restrict__ sm, float* __restrict__ sv, PinMlp mlp, unsigned char* __restrict__ out,
-             PinAdamStep a) {
+             int64_t n, int64_t nb_dense, float* __restrict__ rep, int nrep, long long* __restrict__ fix, int nfix,
+             int fshift, AdamSegs sg, float* __restrict__ sgrad, float* __restrict__ sm, float* __restrict__ sv,
+             PinMlp mlp, unsigned char* __restrict__ out, PinAdamStep a) {
     // the decoder's block first (dispatched first: the pack after its step is the longest chain)
     const int64_t bid = (int64_t)blockIdx.x - (sg.n > 0 ? 1 : 0);
     if (bid >= 0) {
         const int64_t i0 = 4 * (bid * kTBlock + threadIdx.x);
-        if (nrep > 1 && i0 < n) {   // n % 4 == 0 (checked by the host)
+        if (fix && i0 < n) {   // deterministic mode: grad + float(integer sum of the fixed-point replicas)
+            long long s[4] = {0, 0, 0, 0};
+            for (int k = 0; k < nfix; ++k) {
+                longlong2* r = (longlong2*)(fix + k * n + i0);
+                const longlong2 v0 = r[0], v1 = r[1];
+                r[0] = r[1] = make_longlong2(0, 0);
+                s[0] += v0.x; s[1] += v0.y; s[2] += v1.x; s[3] += v1.y;
+            }
+            const double inv = 1.0 / fixed_scale(fshift);
+            float4 g = *(float4*)(grad + i0);
+            g.x += from_fixed(s[0], inv); g.y += from_fixed(s[1], inv);
+            g.z += from_fixed(s[2], inv); g.w += from_fixed(s[3], inv);
+            *(float4*)(grad + i0) = g;
+        } else if (nrep > 1 && i0 < n) {   // n % 4 == 0 (checked by the host)
             float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int k = 0; k < nrep; ++k) {
                 float4* r = (float4*)(rep + k * n + i0);
@@ -1434,8 +1489,10 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
     // with the decoder's layout (W1 | b1 | W2 | b2 end to end, checked by the host) the stepped
     // values also go to LDS, and the pack reads them there (no global round trip behind a fence)
     __shared__ float s_dec[kMlpGrad];
+    // the segments ARE mlp's W1 | b1 | W2 | b2, in that order (sizes alone would not tell b1 from W2)
     const bool lds = out && sg.n == 4 && sg.off[4] == kMlpGrad && sg.off[1] == kH * kD && sg.off[2] == kH * kD + kH &&
-                     sg.off[3] == kH * kD + 2 * kH;
+                     sg.off[3] == kH * kD + 2 * kH && sg.p[0] == mlp.W1 && sg.p[1] == mlp.b1 && sg.p[2] == mlp.W2 &&
+                     sg.p[3] == mlp.b2;
     for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a, lds ? s_dec : nullptr);
     if (out) {
         if (lds) {
@@ -1490,13 +1547,15 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
 }
 
 int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-                        float* grad_replicas, int32_t replicas, float* const* params, const int64_t* sizes,
-                        int nseg, float* seg_grad, float* seg_exp_avg, float* seg_exp_avg_sq, const PinMlp* mlp,
-                        void* packed, const PinAdamStep* a, void* stream) {
+                        float* grad_replicas, int32_t replicas, int64_t* grad_fixed, int32_t fixed_shift,
+                        float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
+                        float* seg_exp_avg_sq, const PinMlp* mlp, void* packed, const PinAdamStep* a, void* stream) {
     if (!a || n < 0 || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq))) return PIN_ERR_ARG;
     if (a->grad_stride != 8) return PIN_ERR_UNSUPPORTED;
     const bool rep = grad_replicas && replicas > 1;
     if (rep && (n % 4 || ((uintptr_t)grad_replicas & 15))) return PIN_ERR_ARG;
+    if (grad_fixed && (grad_replicas || n % 4 || ((uintptr_t)grad_fixed & 15) || fixed_shift < 0 || fixed_shift > 62))
+        return PIN_ERR_ARG;
     AdamSegs sg{};
     sg.n = 0;
     if (nseg > 0) {
@@ -1514,8 +1573,18 @@ int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_av
     const int64_t nb = nb_dense + (nseg > 0 ? 1 : 0);
     if (nb == 0) return PIN_OK;
     hipLaunchKernelGGL(k_adam_train, dim3((unsigned)nb), dim3(kTBlock), 0, as_stream(stream), param, grad, exp_avg,
-                       exp_avg_sq, n, nb_dense, rep ? grad_replicas : nullptr, rep ? (int)replicas : 0, sg, seg_grad,
+                       exp_avg_sq, n, nb_dense, rep ? grad_replicas : nullptr, rep ? (int)replicas : 0,
+                       (long long*)grad_fixed, replicas > 1 ? (int)replicas : 1, (int)fixed_shift, sg, seg_grad,
                        seg_exp_avg, seg_exp_avg_sq, m, pack ? (unsigned char*)packed : nullptr, *a);
+    return launch_status();
+}
+
+int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, float* out, void* stream) {
+    if (n < 0 || (n > 0 && (!acc || !out)) || shift < 0 || shift > 62) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    const int64_t nb = (n + kTBlock - 1) / kTBlock;
+    hipLaunchKernelGGL(k_fixed_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, as_stream(stream),
+                       (long long*)acc, nrep > 1 ? (int)nrep : 1, n, (int)shift, out);
     return launch_status();
 }
 
@@ -1679,6 +1748,9 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     if (rows == 0) return PIN_OK;
     if ((loss_out || mlp_grad) && !workspace) return PIN_ERR_ARG;
+    if ((st->grad_fixed && (st->fixed_shift < 0 || st->fixed_shift > 62 || ((uintptr_t)st->grad_fixed & 15))) ||
+        (st->cert_fixed && (st->cert_shift < 0 || st->cert_shift > 62)))
+        return PIN_ERR_ARG;
     auto s = as_stream(stream);
     const dim3 g = grid_for(rows);
     const int64_t nblk = g.x;
@@ -1719,7 +1791,13 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     }
 #undef PIN_LAUNCH_BWD
 #undef PIN_LAUNCH_BWD_EIK
-    if (grad_features && st->grad_replicas && st->replicas > 1 && st->replica_mode == 0) {
+    if (grad_features && st->grad_fixed && st->replica_mode == 0) {   // deterministic mode
+        const int64_t n = pts->rows * kF;
+        const int64_t nb = (n + kTBlock - 1) / kTBlock;
+        hipLaunchKernelGGL(k_fixed_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, s,
+                           (long long*)st->grad_fixed, st->replicas > 1 ? st->replicas : 1, n, st->fixed_shift,
+                           grad_features);
+    } else if (grad_features && st->grad_replicas && st->replicas > 1 && st->replica_mode == 0) {
         const int64_t n4 = pts->rows * kF / 4;
         const int64_t nb = (n4 + kTBlock - 1) / kTBlock;
         hipLaunchKernelGGL(k_replica_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, s,

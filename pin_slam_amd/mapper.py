@@ -47,6 +47,16 @@ _REPLICAS = int(os.environ.get("PIN_TRAIN_REPLICAS", "8"))
 _PAIR_ROWS = int(os.environ.get("PIN_TRAIN_PAIR_ROWS", str(1 << 17)))
 # the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
 _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
+# deterministic mode (Mapper(deterministic=True) / config.deterministic): the feature-gradient
+# terms and the certainty side effect are summed as 64-bit fixed-point integers
+# (PinTrainState.grad_fixed / cert_fixed), the rows tile-sorted stably -- a mapping() call is then
+# a function of its inputs and draws, bitwise.  Shifts: 2^-50 resolution (8.9e-16) with a range of
+# +-8192 per gradient element; 2^-32 (2.3e-10) and +-2^30 for a call's certainty sums
+FIXED_SHIFT = 50
+CERT_SHIFT = 32
+# data-parallel dense loop: the feature gradient's all-reduce in this many row buckets, each
+# stepped by Adam as soon as it is reduced (_allreduce_adam)
+_AR_BUCKETS = int(os.environ.get("PIN_AR_BUCKETS", "4"))
 
 
 def _viewed_elsewhere(t: torch.Tensor) -> bool:
@@ -84,10 +94,26 @@ class _TrainBuffers:
 
     def replicas(self, n_floats, device):
         """Zeroed scratch of n_floats for PinTrainState.grad_replicas (pin_train_backward re-zeroes
-        it after every use; grown, never shrunk)."""
-        buf = getattr(self, "grad_replicas", None)
-        if buf is None or buf.numel() < n_floats or buf.device != torch.device(device):
-            self.grad_replicas = buf = torch.zeros((max(n_floats, 1 << 16),), dtype=torch.float32, device=device)
+        it after every use); re-allocated when too small or more than 4x too large."""
+        return self._zeroed("grad_replicas", n_floats, torch.float32, device)
+
+    def fixed(self, n, device):
+        """Zeroed int64 scratch for PinTrainState.grad_fixed (the deterministic mode's fixed-point
+        replicas; the consumer re-zeroes it)."""
+        return self._zeroed("grad_fixed", n, torch.int64, device)
+
+    def cert_fixed(self, n, device):
+        """Zeroed int64 scratch for PinTrainState.cert_fixed (folded and re-zeroed by
+        pin_fixed_accumulate at the end of the plan)."""
+        return self._zeroed("cert_fix", n, torch.int64, device)
+
+    def _zeroed(self, name, n, dtype, device):
+        buf = getattr(self, name, None)
+        want = max(int(n), 1 << 16)
+        if (buf is None or buf.numel() < n or buf.numel() > 4 * want or buf.dtype != dtype
+                or buf.device != torch.device(device)):
+            buf = torch.zeros((want,), dtype=dtype, device=device)
+            setattr(self, name, buf)
         return buf
 
     def get(self, rows, nn_k, wf, device):
@@ -118,6 +144,10 @@ class _TrainBuffers:
 class _StepPlan:
     """The launches of one training iteration (Mapper._step_plan); run() takes the batch's draw."""
     packed = None
+    det = False
+    fix = None        # deterministic mode, gradient folded by the Adam launch: the fixed-point replicas
+    nfix = 0
+    cert_fix = None
 
     def run(self, index, index_new):
         b = self.b
@@ -136,8 +166,9 @@ class _StepPlan:
             _lib.call("pin_train_gather", _lib.ptr(q), _lib.ptr(sdf_label), _lib.ptr(ts), _lib.ptr(wpool),
                       int(q.shape[0]), _lib.ptr(index), *self.gather_tail)
         if self.tiled:
-            # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates)
-            query_sort(self.gv, b.rows, out=b.rows4)
+            # process the rows tile by tile (pin_query_sort over the batch + stencil coordinates;
+            # the deterministic mode keeps the input order inside a tile)
+            query_sort(self.gv, b.rows, out=b.rows4, stable=self.det)
         self.mapper._order = b.rows4 if self.tiled else None
         _lib.check("pin_train_forward", self.f_fwd(*self.fwd_args))
         _lib.check("pin_train_backward", self.f_bwd(*self.bwd_args))
@@ -146,6 +177,10 @@ class _StepPlan:
         """After the last run: the side effects went through raw pointers -- invalidate the caches
         built on them; the loss / sdf of the last iteration."""
         nm = self.mapper.neural_points
+        if self.cert_fix is not None:   # the deterministic mode's certainty sums, folded in once
+            cert = nm.local_point_certainties
+            _lib.call("pin_fixed_accumulate", _lib.ptr(self.cert_fix), 1, cert.numel(), CERT_SHIFT, _lib.ptr(cert),
+                      self.s)
         nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if self.ts64 is not None else None)
         self.mapper.last_loss = self.b.loss
         self.mapper.last_sdf = self.b.sdf[: self.n]
@@ -155,7 +190,7 @@ class Mapper:
     """utils/mapper.py:Mapper -- constructor signature, pools and training entry points."""
 
     def __init__(self, config, dataset, neural_points, geo_mlp, sem_mlp=None, color_mlp=None, group=None,
-                 shard="dense", slab_layout="auto"):
+                 shard="dense", slab_layout="auto", deterministic=None):
         self.config = config
         self.silence = config.silence
         self.dataset = dataset
@@ -202,6 +237,9 @@ class Mapper:
         self.shard = shard
         self.slab_layout = slab_layout
         self.last_loss = None        # device f64 tensor: loss of the last iteration
+        # deterministic accumulation (FIXED_SHIFT above); default: config.deterministic, else off
+        self.deterministic = bool(getattr(config, "deterministic", False)) if deterministic is None \
+            else bool(deterministic)
         self._buf = _TrainBuffers()
         self._adam_t = 0
 
@@ -648,19 +686,48 @@ class Mapper:
                 mv = plan.mv if (segs is not None and plan.mv.struct.packed) else None
                 # pin_adam_step_train's arguments but the per-step scalars
                 head = (_lib.ptr(fdata), _lib.ptr(f_grad), _lib.ptr(f_m), _lib.ptr(f_v), fdata.numel(),
-                        _lib.ptr(plan.rep), _REPLICAS if plan.rep is not None else 0,
+                        _lib.ptr(plan.rep), _REPLICAS if plan.rep is not None else plan.nfix,
+                        _lib.ptr(plan.fix), FIXED_SHIFT,
                         segs[0] if segs else None, segs[1] if segs else None, len(mlp_params) if segs else 0,
                         _lib.ptr(m_grad), _lib.ptr(m_m), _lib.ptr(m_v), mv.ref() if mv else None,
                         ctypes.c_void_p(mv.struct.packed) if mv else None)
             plan.run(idx, idx_new)
-            if world > 1:
-                allreduce_gradients([f_grad, m_grad], group)
             self._adam_t += 1
             # the first step of the call's fresh optimiser: the moments are taken as zero (mapping()
             # leaves them unfilled for this loop)
             st = adam_scalars(c.lr, self._adam_t, c.adam_eps, zero_grad=3 if self._adam_t == 1 else 1)
-            _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(st), s))
+            if world > 1:
+                self._allreduce_adam(fdata, f_grad, f_m, f_v, m_grad, head, st, group, s)
+            else:
+                _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(st), s))
         return plan
+
+    def _allreduce_adam(self, fdata, f_grad, f_m, f_v, m_grad, head, st, group, s):
+        """The data-parallel step of the dense loop: SUM all-reduce of the
+        per-rank gradients (scaled by 1/W in the backward) and the Adam step, overlapped -- the
+        [L+1, 8] gradient goes out in _AR_BUCKETS row buckets, all enqueued at once on RCCL's
+        stream, and Adam steps bucket b as soon as its all-reduce is done (a stream wait, no host
+        sync) while the later buckets are still on the wire.  The decoder's 833 gradients (a
+        training decoder) are all-reduced first and stepped (and re-packed) by one block of
+        pin_adam_step_train.  Gloo (CPU tests, 1-GPU rehearsals) runs the same buckets in turn."""
+        if m_grad is not None:
+            all_reduce(m_grad, group=group)
+            dec_args = (None, None, None, None, 0, None, 0, None, 0) + head[9:]
+            _lib.check("pin_adam_step_train", _lib.fn("pin_adam_step_train")(*dec_args, ctypes.byref(st), s))
+        n = fdata.numel()
+        flat = [t.view(-1) for t in (fdata, f_grad, f_m, f_v)]
+        nb = max(1, min(_AR_BUCKETS, n // (1 << 16)))
+        edges = [((n * k // nb) // 8) * 8 for k in range(nb)] + [n]
+        nccl = dist.get_backend(group) != "gloo"
+        works = [dist.all_reduce(flat[1][a:b], group=group, async_op=True) if nccl else None
+                 for a, b in zip(edges[:-1], edges[1:])]
+        step = _lib.fn("pin_adam_step")
+        for k, (a, b) in enumerate(zip(edges[:-1], edges[1:])):
+            if nccl:
+                works[k].wait()          # the current stream waits for bucket k's all-reduce
+            else:
+                all_reduce(flat[1][a:b], group=group)
+            _lib.check("pin_adam_step", step(*[_lib.ptr(t[a:b]) for t in flat], b - a, ctypes.byref(st), s))
 
     def _slab_partition(self, world, fused):
         """shard="space" set-up of one mapping() call: (partition, the slab's pool rows, the slab's
@@ -807,18 +874,35 @@ class Mapper:
         cfg = P.cfg = _lib.PinTrainCfg.from_buffer_copy(cfg_rows)
         cfg.flags = _lib.PIN_TRAIN_ROWS
         P.tiled = grid and _TILE_QUERIES and rows >= _TRAIN_TILE_MIN
+        det = P.det = bool(getattr(self, "deterministic", getattr(c, "deterministic", False)))
         st = P.st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                        sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                        ts_update=nm.local_point_ts_update.data_ptr() if P.ts64 is not None else None,
                                        order=None, sorted_rows=b.rows4.data_ptr() if P.tiled else None,
                                        row_weight=_lib.ptr(P.wrow), row_ts=_lib.ptr(P.ts64))
-        if (grad_features is not None and rows < _REPLICA_ROWS and _REPLICAS > 1
-                and grad_features.shape[0] == pv.features.shape[0]):
+        # replicas for small batches on small maps: every replica is read and re-zeroed in full per
+        # iteration (L+1 rows x 32 B each), which pays only while the map is not much larger than
+        # the batch's (row, neighbour) pairs
+        use_rep = (grad_features is not None and rows < _REPLICA_ROWS and _REPLICAS > 1
+                   and grad_features.shape[0] == pv.features.shape[0]
+                   and grad_features.shape[0] <= 2 * rows * nn_k)
+        # the Adam launch sums the replicas -- unless the gradient is all-reduced before it
+        defer = bool(fused_adam) and world == 1
+        if det and grad_features is not None:
+            if grad_features.shape[0] != pv.features.shape[0]:
+                raise ValueError("deterministic mapping needs grad_features of the local map's [L+1, 8] shape")
+            nrep = _REPLICAS if use_rep else 1
+            fix = b.fixed(nrep * grad_features.numel(), q.device)
+            st.grad_fixed, st.fixed_shift = fix.data_ptr(), FIXED_SHIFT
+            st.replicas, st.replica_mode = nrep, int(defer)
+            P.fix, P.nfix = (fix if defer else None), nrep
+        elif use_rep:
             rep = b.replicas(_REPLICAS * grad_features.numel(), q.device)
-            # the Adam launch sums the replicas -- unless the gradient is all-reduced before it
-            defer = bool(fused_adam) and world == 1
             st.grad_replicas, st.replicas, st.replica_mode = rep.data_ptr(), _REPLICAS, int(defer)
             P.rep = rep if defer else None
+        if det:
+            cf = P.cert_fix = b.cert_fixed(nm.local_point_certainties.numel(), q.device)
+            st.cert_fixed, st.cert_shift = cf.data_ptr(), CERT_SHIFT
         # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
         # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
         dx = wf and mlp_grad is None and _MLP_PACK and not analytic

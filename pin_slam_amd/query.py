@@ -262,10 +262,25 @@ def query_order(gv, q):
     return order
 
 
-def query_sort(gv, q, out=None):
-    """pin_query_sort: the queries q [N,3] in tile order as [N,4] f32 rows {x, y, z, bits(index)}."""
+_stable_ws = {}
+
+
+def query_sort(gv, q, out=None, stable=False):
+    """pin_query_sort: the queries q [N,3] in tile order as [N,4] f32 rows {x, y, z, bits(index)}.
+    stable: pin_query_sort_stable (inside a tile the input order is kept: a deterministic order)."""
     n = q.shape[0]
     q4 = out if out is not None else torch.empty((n, 4), dtype=torch.float32, device=q.device)
+    if stable:
+        need = int(_lib.load().pin_query_sort_stable_workspace_bytes(max(n, 1)))
+        if need < 0:
+            raise RuntimeError("pin_query_sort_stable_workspace_bytes failed")
+        key = str(q.device)
+        ws = _stable_ws.get(key)
+        if ws is None or ws.numel() < need:
+            ws = _stable_ws[key] = torch.empty((need,), dtype=torch.uint8, device=q.device)
+        _lib.call("pin_query_sort_stable", gv.ref(), _lib.ptr(q), n, _lib.ptr(q4), None, _lib.ptr(ws),
+                  _lib.stream(q.device))
+        return q4
     ws = order_workspace(n, q.device)
     _lib.call("pin_query_sort", gv.ref(), _lib.ptr(q), n, _lib.ptr(q4), None, _lib.ptr(ws), _lib.stream(q.device))
     return q4

@@ -299,13 +299,14 @@ KITTI_CFG = dict(voxel_size_m=0.4, query_nn_k=6, search_alpha=0.5, weighted_firs
                  source_vox_down_m=0.8, track_on=True)
 
 
-def street_map(frames=12, device="cuda", seed=21, cfg_overrides=None):
+def street_map(frames=12, device="cuda", seed=21, cfg_overrides=None, deterministic=True):
     """A neural-point map of the synthetic street built by PIN-SLAM's mapping steps with the
     ground-truth poses (pin_slam.py:161-257 with tracking replaced by the known pose, i.e. the
     reference's mapping-only mode): per frame voxel down-sample + crop, process_frame (sampling,
     map update, pool), mapping(iters; 40 x on frame 0) with the decoder training.  KITTI settings
     (KITTI_CFG) unless overridden.  Returns (nm, dec, cfg, scene, poses, rng); the map is centred
-    on the last pose's local map."""
+    on the last pose's local map.  deterministic: the mapper's deterministic mode, so the same
+    arguments give the same map bitwise (the draws come from torch's seeded generators)."""
     from .mapper import Mapper
     from .neural_points import voxel_down_sample
     kw = dict(KITTI_CFG)
@@ -317,7 +318,7 @@ def street_map(frames=12, device="cuda", seed=21, cfg_overrides=None):
     nm = NeuralPoints(cfg)
     torch.manual_seed(42)
     dec = Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1).to(device)
-    mapper = Mapper(cfg, None, nm, dec)
+    mapper = Mapper(cfg, None, nm, dec, deterministic=deterministic)
     travel = [0.0]
     for k in range(frames):
         if k > 0:

@@ -315,8 +315,9 @@ def test_train_adam_equals_replica_sum_segments_and_pack(dev):
     views = [mlp_view(d, packed=True) for d in decs]
     packs = [torch.zeros(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=dev) for _ in range(2)]
     ptrs = [(ctypes.c_void_p * 4)(*[p.data.data_ptr() for p in d.parameters()]) for d in decs]
-    _lib.call("pin_adam_step_train", *[_lib.ptr(t) for t in fa], n, _lib.ptr(rep), R, ptrs[0], szs, 4, _lib.ptr(sg),
-              _lib.ptr(sm), _lib.ptr(sv), views[0].ref(), _lib.ptr(packs[0]), ctypes.byref(st), _lib.stream())
+    _lib.call("pin_adam_step_train", *[_lib.ptr(t) for t in fa], n, _lib.ptr(rep), R, None, 0, ptrs[0], szs, 4,
+              _lib.ptr(sg), _lib.ptr(sm), _lib.ptr(sv), views[0].ref(), _lib.ptr(packs[0]), ctypes.byref(st),
+              _lib.stream())
     acc = torch.zeros(n, device=dev)
     for k in range(R):
         acc += repb[k * n:(k + 1) * n]
@@ -335,7 +336,8 @@ def test_train_adam_equals_replica_sum_segments_and_pack(dev):
 
 def test_fresh_moments_flag_equals_zero_moments(dev):
     """PinAdamStep.zero_grad bit 1 (the first step of a fresh optimiser): moments holding garbage
-    are taken as zero -- bitwise the step on zeroed moments; features and decoder segments."""
+    are taken as zero -- bitwise the step on zeroed moments; features and decoder segments.  Bit 0
+    alone zeroes the gradient: zero_grad = 2 (fresh moments, gradient kept) leaves it as it was."""
     import ctypes
     from pin_slam_amd.mapper import adam_scalars
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -343,8 +345,9 @@ def test_fresh_moments_flag_equals_zero_moments(dev):
     p0, gr = torch.randn(n, generator=g).to(dev), torch.randn(n, generator=g).to(dev)
     seg0 = [torch.randn(k, generator=g).to(dev) for k in sizes]
     sgr = torch.randn(sum(sizes), generator=g).to(dev)
-    out = []
-    for fresh in (False, True):
+    out, grads = [], []
+    for zg in (1, 3, 2):
+        fresh = bool(zg & 2)
         p, gg = p0.clone(), gr.clone()
         m = torch.full_like(p, float("nan")) if fresh else torch.zeros_like(p)
         v = torch.full_like(p, float("nan")) if fresh else torch.zeros_like(p)
@@ -354,13 +357,18 @@ def test_fresh_moments_flag_equals_zero_moments(dev):
         sv = torch.full_like(sg, float("nan")) if fresh else torch.zeros_like(sg)
         ptrs = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in seg])
         szs = (ctypes.c_int64 * 4)(*sizes)
-        st = adam_scalars(0.01, 1, 1e-15, zero_grad=3 if fresh else 1)
-        _lib.call("pin_adam_step_train", _lib.ptr(p), _lib.ptr(gg), _lib.ptr(m), _lib.ptr(v), n, None, 0, ptrs, szs, 4,
-                  _lib.ptr(sg), _lib.ptr(sm), _lib.ptr(sv), None, None, ctypes.byref(st), _lib.stream())
+        st = adam_scalars(0.01, 1, 1e-15, zero_grad=zg)
+        _lib.call("pin_adam_step_train", _lib.ptr(p), _lib.ptr(gg), _lib.ptr(m), _lib.ptr(v), n, None, 0, None, 0,
+                  ptrs, szs, 4, _lib.ptr(sg), _lib.ptr(sm), _lib.ptr(sv), None, None, ctypes.byref(st),
+                  _lib.stream())
         torch.cuda.synchronize()
         out.append([p, m, v, sm, sv] + seg)
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+        grads.append((gg, sg))
+    for k in (1, 2):
+        for a, b in zip(out[0], out[k]):
+            assert torch.equal(a, b)
+    assert float(grads[1][0].abs().max()) == 0.0 and float(grads[1][1].abs().max()) == 0.0
+    assert torch.equal(grads[2][0], gr) and torch.equal(grads[2][1], sgr)
 
 
 def test_split_gather_equals_concatenated_index(dev):
