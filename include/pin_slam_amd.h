@@ -458,10 +458,14 @@ typedef struct PinTrainCfg {
                                     all-reduce of per-rank gradients is the gradient of the mean loss */
     int32_t flags;               /* PIN_TRAIN_ROWS: `coord` of pin_train_forward holds every row (batch and
                                     stencil, pin_train_rows / pin_train_gather) instead of the batch;
-                                    PIN_TRAIN_DX (weighted_first, mlp->packed set, no decoder gradient):
+                                    PIN_TRAIN_DX (mlp->packed set, no decoder gradient): weighted_first --
                                     the forward decodes on the matrix cores and saves s dsdf/dx[0:8] as
                                     x [rows, 8] instead of the input, and the backward applies it without
-                                    re-evaluating the decoder;
+                                    re-evaluating the decoder; per-neighbour -- the forward saves each
+                                    neighbour's 64 ReLU masks as x [rows, nn_k] uint64 instead of its
+                                    vector, and the backward's input gradients are the matrix-core
+                                    decoder's second GEMM over them (no feature re-gather, no hidden
+                                    layer);
                                     PIN_TRAIN_EIK: analytic-gradient eikonal (numerical_grad off,
                                     mapper.py:481-482, get_gradient create_graph=True, tools.py:174-184):
                                     n_stencil must be 0; the forward evaluates dsdf/dq of every batch row in
@@ -488,7 +492,8 @@ typedef struct PinTrainState {
     int32_t* ids;                /* [rows, nn_k] local feature rows, -1 invalid */
     float* weights;              /* [rows, nn_k] IDW weights */
     float* x;                    /* weighted_first: [rows, 11] decoder input (PIN_TRAIN_DX: [rows, 8] s dsdf/dx
-                                    over the features); else [rows, nn_k, 3] vectors */
+                                    over the features); else [rows, nn_k, 3] vectors (PIN_TRAIN_DX:
+                                    the buffer read as [rows, nn_k] uint64 ReLU masks) */
     float* sdf;                  /* [rows] predicted sdf */
     float* certainties;          /* [L] += w (training side effect, neural_points.py:640), may be NULL;
                                     applied by pin_train_backward from ids / weights */

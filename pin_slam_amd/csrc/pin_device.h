@@ -795,9 +795,13 @@ __device__ __forceinline__ void load_row(const float* __restrict__ w, int c, flo
 // Decoder forward fused with its input gradient (model/decoder.py:66-88):
 //   sdf = s * (w2 . relu(W1 x + b1) + b2),  gx[i] = s * sum_c w2[c] 1[pre_c > 0] W1[c][OFF+i].
 // One pass over the hidden units, two at a time with packed FMAs (v_pk_fma_f32).
+// mask (may be NULL): the 64 ReLU masks, bit c = [pre_c > 0] (the per-neighbour training forward
+// saves them for the backward's input gradient, mlp_grad8_from_mask).
 template <bool GRAD, int OFF, int NOUT>
-__device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
+__device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT],
+                                                uint64_t* mask = nullptr) {
     f32x2 out2 = {0.f, 0.f};
+    uint64_t mk = 0;
     f32x2 g2[NOUT];
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) g2[i] = (f32x2){0.f, 0.f};
@@ -815,6 +819,7 @@ __device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[
         const f32x2 pre = acc + b;
         const f32x2 a = {pre.x > 0.f ? v2.x : 0.f, pre.y > 0.f ? v2.y : 0.f};
         out2 = __builtin_elementwise_fma(a, pre, out2);
+        if (mask) mk |= (uint64_t)((pre.x > 0.f ? 1u : 0u) | (pre.y > 0.f ? 2u : 0u)) << c;
         if (GRAD) {
 #pragma unroll
             for (int i = 0; i < NOUT; ++i) g2[i] = __builtin_elementwise_fma(a, wv[OFF + i], g2[i]);
@@ -824,6 +829,7 @@ __device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[
 #pragma unroll
         for (int i = 0; i < NOUT; ++i) gx[i] = (g2[i].x + g2[i].y) * m.sdf_scale;
     }
+    if (mask) *mask = mk;
     return ((out2.x + out2.y) + m.w[kWB2]) * m.sdf_scale;
 }
 
@@ -862,9 +868,10 @@ __device__ __forceinline__ float mlp_sdf_rows(const MlpW& m, const float (&x)[kD
 }
 
 template <bool GRAD, int OFF, int NOUT>
-__device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT]) {
-    if constexpr (PIN_MLP_ROWS != 0) return mlp_sdf_rows<GRAD, OFF, NOUT>(m, x, gx);
-    else return mlp_sdf_packed<GRAD, OFF, NOUT>(m, x, gx);
+__device__ __forceinline__ float mlp_sdf(const MlpW& m, const float (&x)[kD], float (&gx)[NOUT],
+                                         uint64_t* mask = nullptr) {
+    if constexpr (PIN_MLP_ROWS != 0) return mlp_sdf_rows<GRAD, OFF, NOUT>(m, x, gx);   // experiment: no masks
+    else return mlp_sdf_packed<GRAD, OFF, NOUT>(m, x, gx, mask);
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1236,6 +1243,63 @@ __device__ __forceinline__ float mlp_sdf_mfma16(const MlpW& m, const float (&x)[
         for (int i = 0; i < NOUT; ++i) gx[i] = g[OFF + i] * m.sdf_scale;
     }
     return out * m.sdf_scale;
+}
+
+// The decoder's input gradient over the features from a given ReLU mask: gx[i] = s * sum_c
+// 1[mask bit c] w2_c W1[c][i], i < 8 -- GEMM2 of mlp_sdf_mfma16 alone (16 MFMAs per wave, no
+// GEMM1, no input staging).  The per-neighbour training backward takes each neighbour's mask from
+// the forward's f32 decode (PIN_TRAIN_DX), so it neither re-gathers the neighbour's features nor
+// re-evaluates its hidden layer.  All 64 lanes of the wave call this (lanes without a row pass 0).
+__device__ __forceinline__ void mlp_grad8_from_mask(const MlpW& m, uint64_t mask, float (&gx)[kF]) {
+    float* xs = m.xs;
+    const unsigned char* pk = m.pk;
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15, grp = lane >> 4;
+    wave_lds_sync();   // xs is the wave's scratch: every lane is past its earlier reads
+    ((uint2*)xs)[lane] = make_uint2((uint32_t)mask, (uint32_t)(mask >> 32));
+    wave_lds_sync();
+    uint64_t qm[4];   // the masks of queries 16 nt + col
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const uint2 v = ((const uint2*)xs)[16 * nt + col];
+        qm[nt] = ((uint64_t)v.y << 32) | v.x;
+    }
+    auto word = [](uint32_t b4, int p) -> uint32_t {   // two f16 halves: 1.0h where the bit is set
+        return ((b4 >> (2 * p)) & 1u ? 0x3C00u : 0u) | ((b4 >> (2 * p + 1)) & 1u ? 0x3C000000u : 0u);
+    };
+    f32x4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+        const f16x8 a2h = ((const f16x8*)(pk + kPkA2))[(2 * ch) * 64 + lane];
+        const f16x8 a2l = ((const f16x8*)(pk + kPkA2))[(2 * ch + 1) * 64 + lane];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            // K-slot s of lane group grp <-> hidden 32 ch + (s < 4 ? 4 grp + s : 16 + 4 grp + s - 4)
+            const uint32_t lo4 = (uint32_t)(qm[nt] >> (32 * ch + 4 * grp)) & 15u;
+            const uint32_t hi4 = (uint32_t)(qm[nt] >> (32 * ch + 16 + 4 * grp)) & 15u;
+            const f16x8 b = __builtin_bit_cast(f16x8, make_uint4(word(lo4, 0), word(lo4, 1), word(hi4, 0), word(hi4, 1)));
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2h, b, acc[nt], 0, 0, 0);
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2l, b, acc[nt], 0, 0, 0);
+        }
+    }
+    // rows 4 grp .. 4 grp + 3 of query 16 nt + col back to the query's lane (rows 0..7 are used)
+    wave_lds_sync();   // every lane has read the masks
+    if (grp < 2) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) *(f32x4*)(xs + (16 * nt + col) * kXsStride + 4 * grp) = acc[nt];
+    }
+    wave_lds_sync();
+    const f32x4* r = (const f32x4*)(xs + lane * kXsStride);
+    const f32x4 g0 = r[0], g1 = r[1];
+    const f32x4* us = (const f32x4*)(pk + kPkScale);
+    const f32x4 u0 = us[0], u1 = us[1];
+    gx[0] = g0[0] * u0[0] * m.sdf_scale; gx[1] = g0[1] * u0[1] * m.sdf_scale;
+    gx[2] = g0[2] * u0[2] * m.sdf_scale; gx[3] = g0[3] * u0[3] * m.sdf_scale;
+    gx[4] = g1[0] * u1[0] * m.sdf_scale; gx[5] = g1[1] * u1[1] * m.sdf_scale;
+    gx[6] = g1[2] * u1[2] * m.sdf_scale; gx[7] = g1[3] * u1[3] * m.sdf_scale;
+    wave_lds_sync();   // the next call reuses xs
 }
 
 // Block setup of the decoder (all threads; ends with a barrier): the f32 weights, or (MF) the

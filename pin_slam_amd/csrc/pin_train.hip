@@ -161,13 +161,20 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
         } else {
             float g3[3];
             float sk = 0.f;
-            if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3);
+            uint64_t mk = 0;
+            if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3, DX ? &mk : nullptr);
             sdf = sdf + sk * w;  // sum_j sdf_j w_j (mapper.py:467-468)
-            if (j < nn_k) {
-                float* xo = st.x + (t * nn_k + j) * 3;  // neighbour vectors for the backward
-                xo[0] = v0;
-                xo[1] = v1;
-                xo[2] = v2;
+            if (j < nn_k && live) {
+                if constexpr (DX) {
+                    // PIN_TRAIN_DX, frozen decoder: the neighbour's 64 ReLU masks -- all the backward
+                    // needs for its input gradient over the features (mlp_grad8_from_mask)
+                    ((uint2*)st.x)[t * nn_k + j] = make_uint2((uint32_t)mk, (uint32_t)(mk >> 32));
+                } else {
+                    float* xo = st.x + (t * nn_k + j) * 3;  // neighbour vectors for the backward
+                    xo[0] = v0;
+                    xo[1] = v1;
+                    xo[2] = v2;
+                }
             }
         }
     }
@@ -969,13 +976,17 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 //     instead of the f32 decoder backward.
 // (A per-block LDS pre-sum of the scatter -- hash table on the feature row, 512 tile-sorted slots,
 // ~2.7 references per row -- measured slower: 683 vs 467 us, the LDS float atomics alone 470 us.)
-template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false>
+// MASK (per-neighbour, PIN_TRAIN_DX): each neighbour's ReLU masks saved by the forward's f32 decode;
+//   its input gradient is GEMM2 of the matrix-core decoder alone (mlp_grad8_from_mask) -- no
+//   feature re-gather, no hidden layer.
+template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false, bool MASK = false>
 __global__ void __launch_bounds__(kTBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
                  double* __restrict__ loss_part) {
     static_assert(!MF || !MLP_GRAD || (WF && !EIK), "matrix-core backward with a training decoder: weighted_first");
     static_assert(!EIK || !(WF && MF), "analytic eikonal, weighted_first: gx from the forward");
+    static_assert(!MASK || (!WF && MF && !MLP_GRAD && !EIK), "mask backward: per-neighbour, frozen decoder");
     constexpr bool kDecode = MF && !WF;               // per-neighbour matrix-core decodes
     constexpr bool kRowDecode = MF && WF && MLP_GRAD; // weighted_first, training decoder: one decode per row
     // weighted_first: one staged gradient row per query row, scattered by the block at the end;
@@ -1104,7 +1115,10 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             const float al = (EIK && ok) ? st.eik_coef[r * nn_k + j] : 0.f;
             const float coef = dsdf * w + al;        // dL/dsdf_j
             float x[kD];
-            if (ok) {
+            if (MASK) {
+#pragma unroll
+                for (int d = 0; d < kD; ++d) x[d] = 0.f;
+            } else if (ok) {
                 const float4* fr = (const float4*)(p.features + (int64_t)id * kF);
                 const float4 f0 = fr[0], f1 = fr[1];
                 const float* v = st.x + (r * nn_k + j) * 3;
@@ -1118,7 +1132,15 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
             float gf[kF];
 #pragma unroll
             for (int d = 0; d < kF; ++d) gf[d] = 0.f;
-            if constexpr (kDecode) {
+            if constexpr (MASK) {
+                if (__any(ok)) {   // wave-uniform
+                    const uint2 mv = ok ? ((const uint2*)st.x)[r * nn_k + j] : make_uint2(0u, 0u);
+                    float g8[kF];
+                    mlp_grad8_from_mask(mlpw, ((uint64_t)mv.y << 32) | mv.x, g8);
+#pragma unroll
+                    for (int d = 0; d < kF; ++d) gf[d] = coef * g8[d];
+                }
+            } else if constexpr (kDecode) {
                 if (__any(ok)) {   // wave-uniform: the whole wave decodes together
                     float g8[kF];
                     mlp_sdf_mfma16<true, 0, kF>(mlpw, x, g8);
@@ -1691,7 +1713,7 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     const bool dx = (cfg->flags & PIN_TRAIN_DX) != 0;
-    if (dx && (!cfg->weighted_first || !mlp->packed)) return PIN_ERR_ARG;
+    if (dx && cfg->weighted_first && !mlp->packed) return PIN_ERR_ARG;
     const bool eik = (cfg->flags & PIN_TRAIN_EIK) != 0;
     if (eik && (dx || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec)) return PIN_ERR_ARG;
     if (rows == 0) return PIN_OK;
@@ -1713,8 +1735,12 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     }
 #define PIN_LAUNCH_FWD(KERNEL, SRC)                                                                             \
     do {                                                                                                        \
-        if (dx) hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp, \
-                                   coord, ts, *cfg, *st);                                                       \
+        if (dx && cfg->weighted_first)                                                                          \
+            hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,      \
+                               coord, ts, *cfg, *st);                                                           \
+        else if (dx) /* per-neighbour: the f32 decode saves each neighbour's ReLU masks */                      \
+            hipLaunchKernelGGL((KERNEL<false, false, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts,    \
+                               *mlp, coord, ts, *cfg, *st);                                                     \
         else if (cfg->weighted_first && mlp->packed && kTrainFwdMf)                                             \
             hipLaunchKernelGGL((KERNEL<true, true, false>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts,     \
                                *mlp, coord, ts, *cfg, *st);                                                     \
@@ -1773,9 +1799,13 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
             else PIN_LAUNCH_BWD_EIK(false, false, false);
         }
     } else if (cfg->flags & PIN_TRAIN_DX) {
-        if (mlp_grad || !cfg->weighted_first) return PIN_ERR_UNSUPPORTED;
-        hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st,
-                           grad_features, mpart, lpart);
+        if (mlp_grad || !mlp->packed) return PIN_ERR_UNSUPPORTED;
+        if (cfg->weighted_first)
+            hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
+                               *st, grad_features, mpart, lpart);
+        else
+            hipLaunchKernelGGL((k_train_backward<false, false, true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp,
+                               label, *cfg, *st, grad_features, mpart, lpart);
     } else if (cfg->weighted_first) {
         if (mlp_grad && mlp->packed)   // a training decoder decoded on the matrix cores
             hipLaunchKernelGGL((k_train_backward<true, true, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,

@@ -45,6 +45,9 @@ _REPLICA_ROWS = int(os.environ.get("PIN_TRAIN_REPLICA_ROWS", str(1 << 18)))
 _REPLICAS = int(os.environ.get("PIN_TRAIN_REPLICAS", "8"))
 # batches below this many rows run the forward with two lanes per row (PIN_TRAIN_PAIR)
 _PAIR_ROWS = int(os.environ.get("PIN_TRAIN_PAIR_ROWS", str(1 << 17)))
+# per-neighbour decoding, frozen decoder: the backward's input gradients from the forward's ReLU
+# masks (PIN_TRAIN_DX); PIN_TRAIN_NWF_MASK=0 re-decodes each neighbour in the backward (A/B runs)
+_NWF_MASK = os.environ.get("PIN_TRAIN_NWF_MASK", "1") != "0"
 # the sample pool also kept as one 32-B record per sample for the batch gather (pin_pool_pack)
 _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 # deterministic mode (Mapper(deterministic=True) / config.deterministic): the feature-gradient
@@ -903,9 +906,11 @@ class Mapper:
         if det:
             cf = P.cert_fix = b.cert_fixed(nm.local_point_certainties.numel(), q.device)
             st.cert_fixed, st.cert_shift = cf.data_ptr(), CERT_SHIFT
-        # frozen decoder, weighted_first: decode on the matrix cores and keep dsdf/dx for the
-        # backward (PIN_TRAIN_DX) instead of re-evaluating the decoder there
-        dx = wf and mlp_grad is None and _MLP_PACK and not analytic
+        # frozen decoder (PIN_TRAIN_DX): weighted_first -- decode on the matrix cores and keep
+        # dsdf/dx for the backward instead of re-evaluating the decoder there; per-neighbour -- keep
+        # each neighbour's ReLU masks from the forward's decode, from which the backward's
+        # matrix-core GEMM2 gives its input gradient (no feature re-gather, no hidden layer)
+        dx = mlp_grad is None and _MLP_PACK and not analytic and (wf or _NWF_MASK)
         # per-neighbour decoding: the backward takes each neighbour's dsdf/dx from the matrix cores;
         # weighted_first with a training decoder: the backward decodes each row there once (input
         # gradient + ReLU masks of the decoder-parameter products)

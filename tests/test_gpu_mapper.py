@@ -218,6 +218,38 @@ def test_matrix_core_train_step_matches_f32(dev, backend, wf, monkeypatch):
     np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_nwf_mask_backward_matches_redecode(dev, backend, monkeypatch):
+    """Per-neighbour decoding, frozen decoder: the forward's f32 decode saves each neighbour's
+    ReLU masks and the backward's input gradients are the matrix-core GEMM2 over them
+    (PIN_TRAIN_DX), against the backward re-decoding every neighbour on the matrix cores: the
+    same sdf / loss / certainties / ts bitwise (the forward is unchanged), feature gradients within
+    the split-f16 rounding (a neighbour at a ReLU kink may take the other branch in one of the two
+    decoders: a few elements in 10^5)."""
+    import pin_slam_amd.mapper as M
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    res = []
+    for mask in (False, True):
+        monkeypatch.setattr(M, "_NWF_MASK", mask)
+        nm, dec, pts = surface_map(300, device=dev, weighted_first=False, buffer_size=1 << 22, query_backend=backend)
+        for p in dec.parameters():
+            p.requires_grad_(False)
+        coord, label, ts = surface_pool(pts, 70001, device=dev)
+        ts = torch.randint(0, 5, ts.shape, device=dev)
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        fg = torch.zeros_like(nm.local_geo_features.data)
+        loss = float(mapper.train_step(coord, label, ts, fg, None))
+        res.append((loss, mapper.last_sdf.clone(), fg, nm.local_point_certainties.clone(),
+                    nm.local_point_ts_update.clone()))
+    (l0, s0, f0, c0, t0), (l1, s1, f1, c1, t1) = res
+    assert torch.equal(s0, s1) and torch.equal(t0, t1)
+    assert l1 == pytest.approx(l0, rel=1e-9)
+    scale = float(f0.abs().max())
+    off = ~np.isclose(_np(f1), _np(f0), rtol=1e-5, atol=1e-5 * scale)
+    assert off.mean() <= 1e-4, (off.sum(), off.size)
+    np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
+
+
 def test_frozen_decoder_trains_features_only(golden, dev):
     """Decoder frozen (freeze_model, utils/tools.py:186-191, after freeze_after_frame): the
     decoder parameters stay bit-identical and the features still move."""

@@ -46,7 +46,7 @@ def main():
         n = bs
         nd = (n + 9) // 10
         rows = n + 6 * nd
-        dx = wf
+        dx = os.environ.get("DX", "1") != "0"   # PIN_TRAIN_DX (frozen decoder), both decoding modes
         cfg = _lib.PinTrainCfg(n_main=n, n_stencil=nd, decimation=10, nn_k=8, weighted_first=int(wf),
                                eps=float(np.float32(0.06)), sigma=float(np.float32(0.055)), weight_e=0.5,
                                grad_scale=1.0, flags=_lib.PIN_TRAIN_ROWS | (_lib.PIN_TRAIN_DX if dx else 0))
