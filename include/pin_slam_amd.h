@@ -596,6 +596,16 @@ int pin_train_gather_packed_split(const float* packed_pool, int64_t pool_rows, c
                                   const PinTrainCfg* cfg, float* rows_out, float* label_out, int64_t* ts_out,
                                   float* weight_out, int32_t* error, void* stream);
 
+/* pin_train_gather_packed_draw -- pin_train_gather_packed_split with the batch drawn on the device:
+ * get_batch's two torch.randint draws (utils/mapper.py:335-340) replaced by a counter-based
+ * generator -- batch row r < n_hist gathers pool row u_r * pool_rows, the rest new_idx[u_r *
+ * new_count], u_r = SplitMix64(mix(seed, counter) + r * golden) / 2^64 (a 64 x 64 high multiply).
+ * The same (seed, counter) gives the same batch; the caller advances counter per iteration. */
+int pin_train_gather_packed_draw(const float* packed_pool, int64_t pool_rows, int64_t n_hist, const int64_t* new_idx,
+                                 int64_t new_count, uint64_t seed, uint64_t counter, const PinTrainCfg* cfg,
+                                 float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                                 void* stream);
+
 /*
  * pin_train_forward -- training-mode query_feature + Decoder.sdf for every row of one mapping
  * iteration (mapper.py:461-468, :683-711; neural_points.py:528-674 with training_mode): fills

@@ -176,6 +176,8 @@ _SIGS = {
                                 c_void_p, c_void_p],
     "pin_train_gather_packed_split": [c_void_p, i64, c_void_p, i64, c_void_p, i64, c_void_p, _P(PinTrainCfg), c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_train_gather_packed_draw": [c_void_p, i64, i64, c_void_p, i64, ctypes.c_uint64, ctypes.c_uint64,
+                                     _P(PinTrainCfg), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_forward": [_P(PinHash), _P(PinGrid), _P(PinPoints), _P(PinMlp), c_void_p, c_void_p, _P(PinTrainCfg),
                           _P(PinTrainState), c_void_p],
     "pin_train_backward": [_P(PinPoints), _P(PinMlp), c_void_p, _P(PinTrainCfg), _P(PinTrainState), c_void_p,

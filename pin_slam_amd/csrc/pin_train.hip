@@ -365,20 +365,38 @@ k_pool_pack(const float* __restrict__ coord, const float* __restrict__ label, co
                                  weight ? weight[i] : 1.f, 0.f);
 }
 
+// The batch draws of pin_train_gather_packed_draw: a counter-based generator (SplitMix64's
+// finaliser over seed, iteration counter and row) in place of get_batch's two torch.randint calls
+// -- row r's pool row (or new-sample slot) is uniform over [0, high) by a 64 x 64 -> high 64-bit
+// multiply (bias < high / 2^64).  No draw launches, no state: the same (seed, counter) gives the
+// same batch.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ int64_t batch_draw(uint64_t key, int64_t r, int64_t high) {
+    return (int64_t)__umul64hi(mix64(key + (uint64_t)r * 0x9E3779B97F4A7C15ull), (uint64_t)high);
+}
+struct BatchDraw {
+    uint64_t key;   // mix64(seed ^ mix64(counter)); 0 = take the index arrays
+    int on;
+};
+
 // k_train_gather over the packed pool: the row's two 16-B halves of one 32-B record
 __global__ void __launch_bounds__(kTBlock)
 k_train_gather_packed(const float4* __restrict__ pool, int64_t pool_rows, const int64_t* __restrict__ index,
                       int64_t n_index, const int64_t* __restrict__ new_idx, int64_t new_count,
                       const int64_t* __restrict__ index_new, PinTrainCfg c, float* __restrict__ rows,
                       float* __restrict__ label, int64_t* __restrict__ ts, float* __restrict__ weight,
-                      int* __restrict__ error) {
+                      int* __restrict__ error, BatchDraw dr = BatchDraw{0, 0}) {
     const int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x;
     if (r >= c.n_main) return;
     int64_t i;
     if (r < n_index) {
-        i = index[r];
+        i = dr.on ? batch_draw(dr.key, r, pool_rows) : index[r];
     } else {   // get_batch's new-sample rows: new_idx[index_new[.]] (utils/mapper.py:335-340)
-        int64_t j = index_new[r - n_index];
+        int64_t j = dr.on ? batch_draw(dr.key, r, new_count) : index_new[r - n_index];
         if (j < 0 || j >= new_count) {
             if (error) atomicOr(error, 1);
             j = 0;
@@ -1685,6 +1703,27 @@ int pin_train_gather_packed_split(const float* packed_pool, int64_t pool_rows, c
     hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kTBlock), 0, as_stream(stream),
                        (const float4*)packed_pool, pool_rows, index, n_index, new_idx, new_count, index_new, *cfg,
                        rows_out, label_out, ts_out, weight_out, (int*)error);
+    return launch_status();
+}
+
+int pin_train_gather_packed_draw(const float* packed_pool, int64_t pool_rows, int64_t n_hist, const int64_t* new_idx,
+                                 int64_t new_count, uint64_t seed, uint64_t counter, const PinTrainCfg* cfg,
+                                 float* rows_out, float* label_out, int64_t* ts_out, float* weight_out, int32_t* error,
+                                 void* stream) {
+    if (!cfg || n_hist < 0 || n_hist > cfg->n_main) return PIN_ERR_ARG;
+    if (n_hist < cfg->n_main && (!new_idx || new_count < 1)) return PIN_ERR_ARG;
+    const int rc = gather_packed_args(packed_pool, pool_rows, cfg, rows_out, label_out);
+    if (rc != PIN_OK || cfg->n_main == 0) return rc;
+    // the key on the host: one 64-bit mix of seed and counter per call
+    auto hmix = [](uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    const BatchDraw dr{hmix(seed ^ hmix(counter)), 1};
+    hipLaunchKernelGGL(k_train_gather_packed, grid_for(cfg->n_main), dim3(kTBlock), 0, as_stream(stream),
+                       (const float4*)packed_pool, pool_rows, (const int64_t*)nullptr, n_hist, new_idx, new_count,
+                       (const int64_t*)nullptr, *cfg, rows_out, label_out, ts_out, weight_out, (int*)error, dr);
     return launch_status();
 }
 

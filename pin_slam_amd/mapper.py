@@ -57,6 +57,10 @@ _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 # +-8192 per gradient element; 2^-32 (2.3e-10) and +-2^30 for a call's certainty sums
 FIXED_SHIFT = 50
 CERT_SHIFT = 32
+# the dense loop draws get_batch's rows on the device (pin_train_gather_packed_draw: no draw
+# launches) unless _randint is replaced on the instance (the tests' replay hook) or
+# Mapper.device_draws is False; PIN_DEVICE_DRAWS=0 turns it off everywhere
+_DEVICE_DRAWS = os.environ.get("PIN_DEVICE_DRAWS", "1") != "0"
 # data-parallel dense loop: the feature gradient's all-reduce in this many row buckets, each
 # stepped by Adam as soon as it is reduced (_allreduce_adam)
 _AR_BUCKETS = int(os.environ.get("PIN_AR_BUCKETS", "4"))
@@ -119,6 +123,16 @@ class _TrainBuffers:
             setattr(self, name, buf)
         return buf
 
+    def draw_shapes(self, n_hist, new_sel, n_new, device):
+        """Placeholder index tensors of a device-drawn batch's sizes (the launch plan is sized from
+        them; the draw kernel never reads them)."""
+        key = (n_hist, n_new, str(device))
+        if getattr(self, "_draw_key", None) != key:
+            self._draw_idx = torch.empty((n_hist,), dtype=torch.int64, device=device)
+            self._draw_new = torch.empty((n_new,), dtype=torch.int64, device=device)
+            self._draw_key = key
+        return self._draw_idx, (None if new_sel is None else (new_sel, self._draw_new))
+
     def get(self, rows, nn_k, wf, device):
         key = (rows, nn_k, wf, str(device))
         if key != self.key:
@@ -152,9 +166,16 @@ class _StepPlan:
     nfix = 0
     cert_fix = None
 
-    def run(self, index, index_new):
+    def run(self, index, index_new, draw=None):
+        """draw (n_hist, new_idx or None, seed, counter): the batch drawn on the device
+        (pin_train_gather_packed_draw) instead of from the index tensors."""
         b = self.b
-        if not self.index_mode:
+        if draw is not None:
+            n_hist, new_sel, seed, ctr = draw
+            _lib.check("pin_train_gather_packed_draw", self.f_draw(
+                self.packed_ptr, self.packed_rows, n_hist, None if new_sel is None else new_sel.data_ptr(),
+                0 if new_sel is None else new_sel.shape[0], seed, ctr, *self.gather_tail))
+        elif not self.index_mode:
             _lib.call("pin_train_rows", _lib.ptr(self.q), self.gather_tail[0], self.gather_tail[1], self.s)
         elif self.packed is not None and index_new is not None:
             new_sel, draw = index_new
@@ -534,6 +555,20 @@ class Mapper:
                 return index_history, new_idx, index_new_batch
         return pick(self._randint(count, bs)), None, None
 
+    def _batch_sizes(self):
+        """_batch_parts' sizes without its draws: (history rows, new_idx or None, new-sample rows)
+        -- the device-drawn batch of the dense loop (pin_train_gather_packed_draw)."""
+        bs = int(self.config.bs)
+        bs_new_sample = int(getattr(self.config, "bs_new_sample", 0))
+        self._n_new_rows = 0
+        if self._new_sample_mode() and self.new_idx is not None:
+            new_idx_count = self.new_idx.shape[0]
+            if new_idx_count > 0:
+                bs_new = min(new_idx_count, bs_new_sample)
+                self._n_new_rows = bs_new
+                return bs - bs_new, self.new_idx.to(torch.int64).contiguous(), bs_new
+        return bs, None, 0
+
     def get_batch(self, global_coord=False):
         """utils/mapper.py:323-361."""
         index = self._batch_index()
@@ -676,10 +711,22 @@ class Mapper:
         segs = None
         adam = _lib.fn("pin_adam_step_train")
         s = _lib.stream()
-        for _ in range(iter_count):
-            index, new_sel, index_new = self._batch_parts()
-            idx, idx_new = self._step_index(self.global_coord_pool, index,
-                                            None if new_sel is None else (new_sel, index_new), packed)
+        # get_batch's draws on the device: one seed per call from torch's (seeded) CPU generator,
+        # the iteration counter per iteration; the tests' replay hook (_randint on the instance)
+        # keeps the host draws
+        dev_draw = (_DEVICE_DRAWS and packed is not None and getattr(self, "device_draws", True)
+                    and "_randint" not in self.__dict__ and getattr(type(self), "_randint", None) is Mapper._randint)
+        seed = int(torch.randint(0, 1 << 62, (1,)).item()) if dev_draw else 0
+        for it in range(iter_count):
+            draw = None
+            if dev_draw:
+                n_hist, new_sel, n_new = self._batch_sizes()
+                idx, idx_new = self._buf.draw_shapes(n_hist, new_sel, n_new, fdata.device)
+                draw = (n_hist, new_sel, seed, it)
+            else:
+                index, new_sel, index_new = self._batch_parts()
+                idx, idx_new = self._step_index(self.global_coord_pool, index,
+                                                None if new_sel is None else (new_sel, index_new), packed)
             n = idx.shape[0] + (0 if idx_new is None else idx_new[1].shape[0])
             if plan is None or plan.n != n:
                 plan = self._step_plan(self.global_coord_pool, self.sdf_label_pool, self.time_pool, f_grad, m_grad,
@@ -694,7 +741,7 @@ class Mapper:
                         segs[0] if segs else None, segs[1] if segs else None, len(mlp_params) if segs else 0,
                         _lib.ptr(m_grad), _lib.ptr(m_m), _lib.ptr(m_v), mv.ref() if mv else None,
                         ctypes.c_void_p(mv.struct.packed) if mv else None)
-            plan.run(idx, idx_new)
+            plan.run(idx, idx_new, draw)
             self._adam_t += 1
             # the first step of the call's fresh optimiser: the moments are taken as zero (mapping()
             # leaves them unfilled for this loop)
@@ -933,6 +980,7 @@ class Mapper:
         P.keep = (hv, pv, gv, mv, grad_features, mlp_grad)
         P.f_fwd, P.f_bwd = _lib.fn("pin_train_forward"), _lib.fn("pin_train_backward")
         P.f_split = _lib.fn("pin_train_gather_packed_split")
+        P.f_draw = _lib.fn("pin_train_gather_packed_draw")
         return P
 
     def _adam(self, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, step=None, partition=None):

@@ -446,6 +446,63 @@ def test_split_gather_equals_concatenated_index(dev):
     assert int(c[4].item()) == 1
 
 
+def _mix64(z):
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_device_batch_draws(dev):
+    """pin_train_gather_packed_draw (get_batch's two torch.randint draws replaced by a counter-based
+    generator in the gather): the gathered rows are exactly the pool rows of the host restatement
+    of the draws (history rows uniform over the pool, new rows new_idx[uniform]); the same
+    (seed, counter) repeats the batch, another counter gives another one; the history draws are
+    uniform (chi-square over 64 bins)."""
+    import ctypes
+    g = torch.Generator(device="cpu").manual_seed(9)
+    N, n_hist, n_new, n_sel = 50000, 7000, 1200, 900
+    coord = torch.randn(N, 3, generator=g).to(dev)
+    label = torch.randn(N, generator=g).to(dev)
+    ts = torch.randint(0, 1 << 40, (N,), generator=g).to(dev)
+    weight = torch.randn(N, generator=g).to(dev)
+    packed = P.Mapper._pack(coord, label, ts, weight)
+    new_sel = torch.randint(0, N, (n_sel,), generator=g).to(dev)
+    n = n_hist + n_new
+    cfg = _lib.PinTrainCfg(n_main=n, n_stencil=(n + 9) // 10, decimation=10, nn_k=8, weighted_first=1, eps=0.06,
+                           sigma=0.1, weight_e=0.1, grad_scale=1.0, flags=0, n_tail=0, grad_scale_tail=0.0)
+    rows = n + 6 * cfg.n_stencil
+
+    def run(seed, ctr):
+        o = (torch.empty(rows * 3, device=dev), torch.empty(n, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
+             torch.empty(n, device=dev), torch.zeros(1, dtype=torch.int32, device=dev))
+        _lib.call("pin_train_gather_packed_draw", _lib.ptr(packed), N, n_hist, _lib.ptr(new_sel), n_sel, seed, ctr,
+                  ctypes.byref(cfg), *[_lib.ptr(t) for t in o], _lib.stream())
+        torch.cuda.synchronize()
+        return o
+    seed, ctr = 0x1234_5678_9ABC_DEF0, 7
+    a, b, c = run(seed, ctr), run(seed, ctr), run(seed, ctr + 1)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert not torch.equal(a[1], c[1])
+    key = _mix64(seed ^ _mix64(ctr))
+    m = (1 << 64) - 1
+    idx = []
+    for r in range(n):
+        u = _mix64((key + r * 0x9E3779B97F4A7C15) & m)
+        idx.append((u * (N if r < n_hist else n_sel)) >> 64)
+    idx = np.array(idx)
+    pool_rows = np.concatenate([idx[:n_hist], _np(new_sel)[idx[n_hist:]]])
+    np.testing.assert_array_equal(_np(a[0])[: 3 * n].reshape(n, 3), _np(coord)[pool_rows])
+    np.testing.assert_array_equal(_np(a[1]), _np(label)[pool_rows])
+    np.testing.assert_array_equal(_np(a[2]), _np(ts)[pool_rows])
+    np.testing.assert_array_equal(_np(a[3]), np.abs(_np(weight)[pool_rows]))
+    assert int(a[4].item()) == 0
+    counts = np.bincount(idx[:n_hist] * 64 // N, minlength=64)
+    chi2 = float(((counts - n_hist / 64) ** 2 / (n_hist / 64)).sum())
+    assert chi2 < 120, chi2    # 63 degrees of freedom: p ~ 1e-5 at 120
+
+
 def test_fat_cache_sees_training_writes(dev):
     """Local inference queries read cached copies of the local features and certainties (fat
     compact records).  mapping() writes those through raw pointers (Adam, certainty / ts side
@@ -508,6 +565,7 @@ def test_fused_gather_path_matches_get_batch(dev):
         ts = torch.randint(0, 4, ts.shape, device=dev)
         mapper = P.Mapper(nm.config, None, nm, dec)
         mapper.set_pool(coord, label, ts)
+        mapper.device_draws = False    # both paths draw with torch.randint (the same draws)
         if not fused:
             mapper.get_batch = lambda global_coord=False, m=mapper: P.Mapper.get_batch(m, global_coord)
         torch.manual_seed(77)
