@@ -615,12 +615,12 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
 
 // The tile sort in ONE launch (small grids): rank as k_tile_rank, then a grid-wide barrier on a
 // counter in the workspace state (every block of a <= kFusedMaxBlocks grid is resident at once:
-// one 1024-thread block per CU at most), then the tile totals' scan and the placement with each
+// one 1024-thread block per CU, at most two with 16,384 tiles' 64 KB of LDS), then the tile totals' scan and the placement with each
 // thread's queries, tiles and ranks still in registers -- no second launch, no re-read of the
 // queries and no (tile, offset) round trip through memory.  The barrier's wait is bounded: a
 // block that waits too long sets *err and goes on (wrong order, no hang).  The last block to
 // leave zeroes the totals and the two counters for the next call.
-constexpr int kFusedMaxBlocks = 128;
+constexpr int kFusedMaxBlocks = 256;
 #ifdef PIN_SORT_STAMPS   // experiment: per-block phase timestamps of k_tile_sort_fused (pin_debug_sort_stamps)
 __device__ unsigned long long g_sort_stamps[kFusedMaxBlocks * 8];
 #define PIN_STAMP(I) do { if (threadIdx.x == 0) g_sort_stamps[blockIdx.x * 8 + (I)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -814,6 +814,10 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
     };
     if (n <= (1 << 19)) launch(std::integral_constant<int, PIN_RANK_PER>(), std::integral_constant<int, kMaxTiles>());
     else if (!large) launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTiles>());
+    else if (fused_ok && (n + 8 * kPartThreads - 1) / (8 * kPartThreads) <= kFusedMaxBlocks)
+        // the mapper's 1.68M rows: one launch of <= 256 blocks of 8 queries per thread (the two-launch
+        // form's 820 placement blocks each scanned all 16,384 tile totals)
+        launch(std::integral_constant<int, 8>(), std::integral_constant<int, kMaxTilesLarge>());
     else launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTilesLarge>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }

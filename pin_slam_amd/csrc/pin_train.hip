@@ -68,6 +68,18 @@ __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const
 #define PIN_TRAIN_FWD_MF 1   // weighted_first, not PIN_TRAIN_DX, mlp->packed: the forward's sdf on the matrix cores
 #endif
 constexpr bool kTrainFwdMf = PIN_TRAIN_FWD_MF != 0;
+#ifndef PIN_TRAIN_NWF_MF
+#define PIN_TRAIN_NWF_MF 0   // 1: per-neighbour, PIN_TRAIN_DX, mlp->packed: the forward's decodes on the matrix
+                             // cores (measured slower: 727 us at 2 waves/SIMD with 84 spilled VGPRs, 925 us at
+                             // 1 wave, vs 644 us for the f32 VALU decodes, 1.68M rows)
+#endif
+constexpr bool kTrainNwfMf = PIN_TRAIN_NWF_MF != 0;
+#ifndef PIN_TRAIN_NWF_WAVES
+#define PIN_TRAIN_NWF_WAVES 2   // its occupancy target (the eight decodes' operands otherwise take ~340 VGPRs)
+#endif
+#ifndef PIN_TRAIN_NWF_NT
+#define PIN_TRAIN_NWF_NT 1   // its decoder with the query tile as the outer GEMM loop (fewer live VGPRs)
+#endif
 
 #ifndef PIN_TRAIN_IDP
 #define PIN_TRAIN_IDP 1   // training forward: top-k payload = feature-row id (GridSource IDP)
@@ -162,7 +174,17 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             float g3[3];
             float sk = 0.f;
             uint64_t mk = 0;
-            if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3, DX ? &mk : nullptr);
+            if constexpr (MF) {   // per-neighbour on the matrix cores: the whole wave decodes together
+                float g8[kF];
+                float xz[kD];
+#pragma unroll
+                for (int d = 0; d < kD; ++d) xz[d] = valid ? xj[d] : 0.f;
+                const float sj = mlp_sdf_mfma16<false, 0, kF, PIN_TRAIN_NWF_NT != 0>(m, xz, g8, DX ? &mk : nullptr);
+                sk = valid ? sj : 0.f;
+                if (!valid) mk = 0;
+            } else {
+                if (valid) sk = mlp_sdf<false, kF, 3>(m, xj, g3, DX ? &mk : nullptr);
+            }
             sdf = sdf + sk * w;  // sum_j sdf_j w_j (mapper.py:467-468)
             if (j < nn_k && live) {
                 if constexpr (DX) {
@@ -282,6 +304,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
 // the scan chain each.
 template <bool WF, bool MF, bool DX = MF, bool PAIR = false>
 __global__ void __launch_bounds__(kTBlock) PIN_FWD_WAVES_ATTR
+__attribute__((amdgpu_waves_per_eu((!WF && MF) ? PIN_TRAIN_NWF_WAVES : 1)))
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
@@ -1777,6 +1800,9 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
         if (dx && cfg->weighted_first)                                                                          \
             hipLaunchKernelGGL((KERNEL<true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts, *mlp,      \
                                coord, ts, *cfg, *st);                                                           \
+        else if (dx && mlp->packed && kTrainNwfMf) /* per-neighbour: matrix-core decodes, masks saved */         \
+            hipLaunchKernelGGL((KERNEL<false, true, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts,     \
+                               *mlp, coord, ts, *cfg, *st);                                                     \
         else if (dx) /* per-neighbour: the f32 decode saves each neighbour's ReLU masks */                      \
             hipLaunchKernelGGL((KERNEL<false, false, true>), grid_for(rows), dim3(kTBlock), 0, s, *SRC, *pts,    \
                                *mlp, coord, ts, *cfg, *st);                                                     \
