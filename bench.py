@@ -489,6 +489,7 @@ def map_leg(args, dev, world, rank):
     res = {"metric": "map update frames/sec", "value": nsteps * world / el, "unit": "frames/s",
            "points_per_sec": MAP_FRAME * nsteps * world / el, "ms_per_frame": el / nsteps * 1e3,
            "median_ms_per_frame": med * 1e3, "timing": _FRAME_TIMING, "steps": nsteps,
+           "frame_ms": [round(t * 1e3, 3) for t in per_frame],
            "map_points_before": M0, "map_points_after": nm.count(), "local_points": nm.local_count(),
            "scaling": "replicas",
            "config": {"workload": "NeuralPoints.update (+ reset_local_map) of 131072-point scans into the 1M-point "
@@ -544,6 +545,7 @@ def process_frame_leg(args, dev, world, rank):
     res = {"metric": "mapper frames/sec (process_frame)", "value": nsteps * world / el, "unit": "frames/s",
            "samples_per_sec": FRAME_RAYS * mapper.ray_sample_count * nsteps * world / el,
            "ms_per_frame": el / nsteps * 1e3, "median_ms_per_frame": med * 1e3, "timing": _FRAME_TIMING,
+           "frame_ms": [round(t * 1e3, 3) for t in per_frame],
            "steps": nsteps, "pool_samples": int(mapper.pool_sample_count),
            "map_points": nm.count(), "new_samples": int(mapper.new_idx.shape[0]), "scaling": "replicas",
            "config": {"workload": "Mapper.process_frame: 65536-ray frames, 7 samples/ray, into the 1M-point surface "
@@ -641,6 +643,7 @@ def slam_frame_leg(args, dev, world, rank):
               for k in range(warm + nsteps))
     return {"metric": "SLAM frames/sec (pin_slam.py frame loop)", "value": nsteps * world / el, "unit": "frames/s",
             "ms_per_frame": el / nsteps * 1e3, "median_ms_per_frame": med * 1e3,
+            "frame_ms": [round(t * 1e3, 3) for t in frame_s],
             "parts_mean_ms": {k: round(statistics.mean(v) * 1e3, 4) for k, v in parts.items()},
             "frames": nsteps, "valid_frames": valid, "max_pose_error_m": err, "map_points": nm.count(),
             "pool_samples": int(mapper.pool_sample_count), "scaling": "replicas", "timing": _FRAME_TIMING,
@@ -761,6 +764,13 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
         idx = torch.randint(0, MAPPER_POOL, (MAPPER_BS,), device=dev)
         res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx])
     return res
+
+
+def _fresh_allocator():
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
 
 def main():
@@ -891,21 +901,31 @@ def main():
     if not args.no_mesher:
         out["mesher"] = mesher_leg(nm, dec, pts, args, dev, world, rank)
     del nm, dec, pts, q
+    # every further leg builds its own workload: start each from an empty caching allocator, so a
+    # leg's timed frames do not pay for releasing an earlier leg's cached blocks (the first timed
+    # map_update frame took ~22 ms when the allocator freed the headline's blocks inside it)
+    _fresh_allocator()
     if not args.no_tracker:
         out["tracker"] = tracker_leg(args, dev, world, rank)
+        _fresh_allocator()
     if not args.no_map_update:
         out["map_update"] = map_leg(args, dev, world, rank)
+        _fresh_allocator()
     if not args.no_process_frame:
         out["process_frame"] = process_frame_leg(args, dev, world, rank)
+        _fresh_allocator()
     if not args.no_slam:
         out["slam_frame"] = slam_frame_leg(args, dev, world, rank)
+        _fresh_allocator()
     if not args.no_mapper:
         out["mapper"] = mapper_leg(args, dev, world, rank)
+        _fresh_allocator()
         if world > 1 and not args.no_mapper_alt:
             # both data-parallel designs in one line: the dense gradient all-reduce (north_star's
             # RCCL step) and the owner-partitioned cells with halo exchange
             alt = "space" if args.mapper_shard == "dense" else "dense"
             out["mapper_" + alt] = mapper_leg(args, dev, world, rank, shard=alt)
+            _fresh_allocator()
     if not args.no_mapper and not args.no_mapper_nwf and not args.nwf:
         # per-neighbour decoding (weighted_first False: run_kitti / mulran / ncd_128 / livox .yaml)
         out["mapper_nwf"] = mapper_leg(args, dev, world, rank, wf=False)

@@ -202,6 +202,8 @@ def save_implicit_map(run_path, neural_points, geo_decoder, color_decoder=None, 
         if not isinstance(x, torch.Tensor):
             return x
         x = x.detach()
+        if x.untyped_storage().nbytes() != x.numel() * x.element_size():
+            x = x.clone()    # a prefix view of a capacity buffer (NeuralPoints._append_rows): save its rows only
         return x.to(tensor_device) if tensor_device is not None else x
 
     state = {}

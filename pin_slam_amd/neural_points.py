@@ -560,21 +560,49 @@ class NeuralPoints(nn.Module):
                   _lib.ptr(n_new), _lib.ptr(map_workspace(n, dev)), _lib.stream())
         torch.autograd.graph.increment_version(self.buffer_pt_index)
         k = int(n_new.item())
-        added = pts[new_rows[:k]]
-        self.neural_points = torch.cat((self.neural_points, added), 0)
+        # the reference's torch.cat of each per-point array (:225-242), appended in place into
+        # buffers with spare capacity (_append_rows): no per-frame copy of the whole map and no
+        # allocator growth as the map grows (a growing torch.cat needed a fresh, larger block from
+        # time to time -- a ~10 ms frame)
+        self.neural_points = self._append_rows("neural_points", self.neural_points, pts[new_rows[:k]])
         if was_trusted:
             self._trust_table()
         quat = torch.zeros((k, 4), dtype=self.dtype, device=dev)
         quat[:, 0] = 1.0
-        self.point_orientations = torch.cat((self.point_orientations, quat), 0)
+        self.point_orientations = self._append_rows("point_orientations", self.point_orientations, quat)
         ts = torch.full((k,), int(cur_ts), device=dev, dtype=torch.long)
-        self.point_ts_create = torch.cat((self.point_ts_create, ts), 0)
-        self.point_ts_update = torch.cat((self.point_ts_update, ts), 0)
+        self.point_ts_create = self._append_rows("point_ts_create", self.point_ts_create, ts)
+        self.point_ts_update = self._append_rows("point_ts_update", self.point_ts_update, ts)
         new_fts = self.geo_feature_std * torch.randn(k + 1, self.geo_feature_dim, device=dev, dtype=self.dtype)
-        self.geo_features = torch.cat((self.geo_features[:-1], new_fts), 0)
-        self.point_certainties = torch.cat(
-            (self.point_certainties, torch.zeros(k, device=dev, dtype=self.dtype)), 0)
+        self.geo_features = self._append_rows("geo_features", self.geo_features, new_fts, replace_last=True)
+        self.point_certainties = self._append_rows("point_certainties", self.point_certainties,
+                                                   torch.zeros(k, device=dev, dtype=self.dtype))
         self.reset_local_map(sensor_position, sensor_orientation, cur_ts)
+
+    def _append_rows(self, name, cur, new, replace_last=False):
+        """torch.cat((cur, new)) -- or torch.cat((cur[:-1], new)) with replace_last (the padding
+        feature row) -- as a prefix view of a buffer with spare rows, written in place when cur is
+        the view this method returned last time (anything else, e.g. an array a caller assigned,
+        is copied once into a new buffer with 1.25x the rows).  The rows of cur are not touched,
+        except the padding row with replace_last, whose old tensor then gets a version bump."""
+        bufs = self.__dict__.setdefault("_row_bufs", {})
+        buf, last = bufs.get(name, (None, None))
+        n = cur.shape[0] - (1 if replace_last else 0)
+        m = new.shape[0]
+        dt = torch.promote_types(cur.dtype, new.dtype)
+        in_place = (buf is not None and last is not None and last() is cur and buf.dtype == dt
+                    and buf.shape[1:] == cur.shape[1:] and buf.shape[0] >= n + m and cur.is_contiguous()
+                    and (cur.shape[0] == 0 or cur.data_ptr() == buf.data_ptr()))
+        if not in_place:
+            rows = max(int((n + m) * 1.25), n + m, 1024)
+            buf = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
+            buf[:n] = cur[:n]
+        elif replace_last:
+            torch.autograd.graph.increment_version(cur)
+        buf[n:n + m] = new
+        out = buf[:n + m]
+        bufs[name] = (buf, weakref.ref(out))
+        return out
 
     def reset_local_map(self, sensor_position: torch.Tensor, sensor_orientation: torch.Tensor, cur_ts: int,
                         use_travel_dist: bool = True, diff_ts_local: int = 50):
