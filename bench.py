@@ -727,7 +727,9 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
     mapper.set_pool(coord, label, ts)
     torch.manual_seed(1234 + rank)
     backend = nm.backend()
+    progress(f"mapper ({shard}, wf {wf}): map and pool built, warm-up")
     mapper.mapping(max(args.mapper_warmup, 1))
+    progress("mapper: timed iterations")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -764,6 +766,15 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
         idx = torch.randint(0, MAPPER_POOL, (MAPPER_BS,), device=dev)
         res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx])
     return res
+
+
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (rank 0): long multi-rank runs print as they go."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 def _fresh_allocator():
@@ -831,6 +842,7 @@ def main():
         if world > 1:
             dist.barrier()
         return time.perf_counter() - t0
+    progress("headline")
     elapsed = window("tile")
     kern_ms, order_ms = time_kernel(nm, dec, q, wf, backend, args.steps, flags=1)
     elapsed_in = kern_in_ms = float("nan")
@@ -895,10 +907,13 @@ def main():
             "kernel_ms": kern_in_ms, "frac_kernel": BYTES_PER_QUERY * N_QUERY / (kern_in_ms * 1e-3) / HBM_PEAK},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
     if wf and not args.no_nwf_leg:
+        progress("per_neighbour")
         out["per_neighbour"] = nwf_leg(nm, dec, q, args, world)
     if not args.no_mesher:
+        progress("mesher")
         out["mesher"] = mesher_leg(nm, dec, pts, args, dev, world, rank)
     del nm, dec, pts, q
     # every further leg builds its own workload: start each from an empty caching allocator, so a
@@ -906,28 +921,35 @@ def main():
     # map_update frame took ~22 ms when the allocator freed the headline's blocks inside it)
     _fresh_allocator()
     if not args.no_tracker:
+        progress("tracker")
         out["tracker"] = tracker_leg(args, dev, world, rank)
         _fresh_allocator()
     if not args.no_map_update:
+        progress("map_update")
         out["map_update"] = map_leg(args, dev, world, rank)
         _fresh_allocator()
     if not args.no_process_frame:
+        progress("process_frame")
         out["process_frame"] = process_frame_leg(args, dev, world, rank)
         _fresh_allocator()
     if not args.no_slam:
+        progress("slam_frame")
         out["slam_frame"] = slam_frame_leg(args, dev, world, rank)
         _fresh_allocator()
     if not args.no_mapper:
+        progress("mapper")
         out["mapper"] = mapper_leg(args, dev, world, rank)
         _fresh_allocator()
         if world > 1 and not args.no_mapper_alt:
             # both data-parallel designs in one line: the dense gradient all-reduce (north_star's
             # RCCL step) and the owner-partitioned cells with halo exchange
             alt = "space" if args.mapper_shard == "dense" else "dense"
+            progress("mapper (other shard mode)")
             out["mapper_" + alt] = mapper_leg(args, dev, world, rank, shard=alt)
             _fresh_allocator()
     if not args.no_mapper and not args.no_mapper_nwf and not args.nwf:
         # per-neighbour decoding (weighted_first False: run_kitti / mulran / ncd_128 / livox .yaml)
+        progress("mapper_nwf")
         out["mapper_nwf"] = mapper_leg(args, dev, world, rank, wf=False)
     # speed-up over the CPU baseline measured in the same run (BASELINE.md's CPU-baseline plan: "speed-up"
     # per config); at N > 1 no CPU baseline runs, and the headline is set against BASELINE.md's own
