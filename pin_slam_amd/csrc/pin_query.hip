@@ -791,11 +791,13 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
 #endif
     constexpr int kPlacePer = PIN_PLACE_PER;
     const int nplace = (int)((n + kPlacePer * kPartThreads - 1) / (kPlacePer * kPartThreads));
-    // one launch (k_tile_sort_fused) where the grid is small enough to be resident at once;
-    // PIN_SORT_FUSED=0 keeps the two launches (A/B runs)
+    // one launch (k_tile_sort_fused) only on request (PIN_SORT_FUSED=1): its grid barrier needs
+    // every block resident at once, which holds for one process per GPU but not when processes
+    // share the GPU -- 8 ranks on one device (bench.py --dist-backend gloo rehearsal) left blocks of
+    // several ranks' sorts spinning for their absent peers.  Measured: headline step 52.6 -> 51.4 us.
     static const bool fused_ok = [] {
         const char* e = getenv("PIN_SORT_FUSED");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     auto launch = [&](auto per_tag, auto maxt_tag) {
         constexpr int PER = decltype(per_tag)::value;
