@@ -745,9 +745,24 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
     elapsed = float(t[0])
     bpi = mapper_bytes_per_iter(MAPPER_BS, L)
     ms = elapsed / args.mapper_steps * 1e3
+    replicas_identical = None
+    if world > 1:
+        # every rank must end with the same map (the data-parallel step applies one update to every
+        # replica): a checksum of the features and certainties, compared across ranks
+        f = nm.geo_features.detach().double()
+        ck = torch.stack([f.sum(), (f * f).sum(), f.abs().max(), nm.point_certainties.double().sum()]).to(dev)
+        allck = [torch.zeros_like(ck) for _ in range(world)]
+        if dist.get_backend() == "gloo":
+            hk = [t.cpu() for t in allck]
+            dist.all_gather(hk, ck.cpu())
+            allck = hk
+        else:
+            dist.all_gather(allck, ck)
+        replicas_identical = all(torch.equal(allck[0].cpu(), t.cpu()) for t in allck)
     res = {"metric": "mapper iters/sec", "value": args.mapper_steps / elapsed, "unit": "iters/s",
            "queries_per_sec": MAPPER_BS * world * args.mapper_steps / elapsed, "ms_per_iter": ms,
            "steps": args.mapper_steps, "warmup": args.mapper_warmup, "scaling": "weak",
+           "replicas_identical": replicas_identical,
            "config": {"workload": "Mapper.mapping, 4M-point map, 1M queries/iter/GPU + numerical-gradient "
                                   "stencil (configs[3])", "map_points": int(pts.shape[0]),
                       "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",

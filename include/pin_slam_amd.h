@@ -190,6 +190,21 @@ int pin_query_feature_bwd(const PinPoints* pts, const float* q, int64_t n, int32
                           const float* grad_weights, float* grad_q, float* grad_features, void* stream);
 
 /*
+ * pin_query_feature_bwd2 -- the double backward of pin_query_feature_bwd (second-order autograd:
+ * get_gradient(..., create_graph=True), utils/tools.py:174-184, through model/neural_points.py:
+ * 577-662): given the first backward's inputs (ids, gids, weights, grad_feat G, grad_weights Gw;
+ * G / Gw may be NULL) and the upstream gradients of its outputs, up_q = dL2/dgrad_q [n,3] and
+ * up_features = dL2/dgrad_features [rows,8] (either may be NULL), it writes dL2/dq [n,3],
+ * dL2/dG (grad_feat's shape), dL2/dGw [n,nn_k] (each may be NULL) and, weighted_first only, adds
+ * dL2/dfeatures into d_features [rows,8] with float atomics (may be NULL).  Closed form per query
+ * (pin_query.hip, k_query_feature_bwd2).
+ */
+int pin_query_feature_bwd2(const PinPoints* pts, const float* q, int64_t n, int32_t nn_k, int32_t weighted_first,
+                           const int32_t* ids, const int32_t* gids, const float* weights, const float* grad_feat,
+                           const float* grad_weights, const float* up_q, const float* up_features, float* d_q,
+                           float* d_grad_feat, float* d_grad_weights, float* d_features, void* stream);
+
+/*
  * pin_train_scatter -- training-mode side effects of query_feature (model/neural_points.py:637-648):
  * certainties[id] += w (scatter_add_), ts_update[id] = max(ts_update[id], query_ts) (scatter_reduce amax,
  * only if query_ts and ts_update are non-NULL).

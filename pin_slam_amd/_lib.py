@@ -128,6 +128,8 @@ _SIGS = {
                               c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_feature_bwd": [_P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_query_feature_bwd2": [_P(PinPoints), c_void_p, i64, i32, i32, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_train_scatter": [c_void_p, c_void_p, i64, i32, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_query_certainty": [_P(PinHash), _P(PinPoints), c_void_p, i64, c_void_p, c_void_p],
     "pin_reg_normal_eq": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, i64,

@@ -1062,6 +1062,197 @@ k_query_feature_bwd(const PinPoints p, const float* __restrict__ q, int64_t n, i
     gq_out[3 * i + 2] = gq[2];
 }
 
+// Double backward of k_query_feature_bwd (second order: get_gradient(..., create_graph=True),
+// utils/tools.py:174-184, then a loss on the gradient).  With r_j = q - p_j (record position), u_j =
+// 1/(|r_j|^2 + eps), S = sum u, w_j = u_j / S, x_j = [f_j, P_j (q - p~_j)] (P_j the passive PGO
+// rotation), the first-order backward is
+//   grad_q = sum_j P_j^T dx_j[8:11] + sum_j k_j (a_j - abar),  k_j = -2 u_j^2 r_j / S,
+//   grad_f[id_j] += dx_j[0:8],
+// with dx_j = w_j G, a_j = G . x_j + Gw_j (weighted_first; G = dL/dout [11]) or dx_j = G_j, a_j =
+// Gw_j (per neighbour), abar = sum_j w_j a_j.  Given the upstream H_q = dL2/dgrad_q and H_f =
+// dL2/dgrad_f, this returns dL2/dq, dL2/dG, dL2/dGw and (weighted_first) dL2/dfeatures in closed form:
+//   h_j = H_q . k_j, H = sum h, e_j = h_j - H w_j = dL2/da_j = dL2/dGw_j
+//   weighted_first: dL2/dG = sum_j (w_j [H_f[id_j], P_j H_q] + e_j x_j), dL2/df_j = e_j G[0:8]
+//   per neighbour:  dL2/dG_j = [H_f[id_j], P_j H_q]
+//   dL2/dq = sum_i du_i (s_i - sbar)/S + sum_i (a_i - abar) dh_i + sum_i e_i b_i - H sum_i du_i (a_i - abar)/S
+//     du_i = -2 u_i^2 r_i, s_i = (P_i H_q) . G[8:11] + H_f[id_i] . G[0:8] (weighted_first, else 0),
+//     b_i = P_i^T G[8:11] (weighted_first, else 0), sigma = sum du,
+//     dh_i = -2/S (u_i^2 H_q - 4 u_i^3 (r_i . H_q) r_i) + 2 u_i^2 (r_i . H_q) sigma / S^2.
+template <bool WF, bool PGO>
+__global__ void __launch_bounds__(kBlock)
+k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k, const int* __restrict__ ids,
+                     const int* __restrict__ gids, const float* __restrict__ weights,
+                     const float* __restrict__ gfeat, const float* __restrict__ gw, const float* __restrict__ hq,
+                     const float* __restrict__ hf, float* __restrict__ dq_out, float* __restrict__ dg_out,
+                     float* __restrict__ dgw_out, float* __restrict__ dF) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
+    const float4* __restrict__ rec = (const float4*)p.records;
+    const float H3[3] = {hq ? hq[3 * i] : 0.f, hq ? hq[3 * i + 1] : 0.f, hq ? hq[3 * i + 2] : 0.f};
+    float G[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) G[d] = (WF && gfeat) ? gfeat[i * kD + d] : 0.f;
+    float u[kK], w[kK], a[kK], sj[kK], r[kK][3], ph[kK][3], b[kK][3];
+    int id[kK];
+    float S = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        id[j] = -1;
+        u[j] = w[j] = a[j] = sj[j] = 0.f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) r[j][d] = ph[j][d] = b[j][d] = 0.f;
+        if (j >= nn_k) continue;
+        const int g = gids[i * nn_k + j];
+        if (g < 0) continue;
+        id[j] = ids[i * nn_k + j];
+        const float4 rc = rec[g];
+        u[j] = 1.0f / (dist2(rc.x, rc.y, rc.z, qx, qy, qz) + kIdwEps);
+        S = S + u[j];
+        w[j] = weights[i * nn_k + j];
+        r[j][0] = qx - rc.x;
+        r[j][1] = qy - rc.y;
+        r[j][2] = qz - rc.z;
+        float px = rc.x, py = rc.y, pz = rc.z;
+        if (__float_as_int(rc.w) & PIN_RECORD_UNFAITHFUL) {
+            px = p.positions[3 * (int64_t)id[j]];
+            py = p.positions[3 * (int64_t)id[j] + 1];
+            pz = p.positions[3 * (int64_t)id[j] + 2];
+        }
+        float v[3] = {qx - px, qy - py, qz - pz};
+        float4 qt = make_float4(1.f, 0.f, 0.f, 0.f);
+        ph[j][0] = H3[0]; ph[j][1] = H3[1]; ph[j][2] = H3[2];
+        if (PGO) {
+            qt = ((const float4*)p.orientations)[id[j]];
+            quat_rotate_passive(qt, v[0], v[1], v[2]);
+            quat_rotate_passive(qt, ph[j][0], ph[j][1], ph[j][2]);   // P_j H_q
+        }
+        float hfj[kF];
+#pragma unroll
+        for (int d = 0; d < kF; ++d) hfj[d] = hf ? hf[(int64_t)id[j] * kF + d] : 0.f;
+        if (WF) {
+            const float4* fr = (const float4*)(p.features + (int64_t)id[j] * kF);
+            const float4 f0 = fr[0], f1 = fr[1];
+            const float f[kF] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            float s = 0.f, t = 0.f;
+#pragma unroll
+            for (int d = 0; d < kF; ++d) {
+                s = fmaf(G[d], f[d], s);
+                t = fmaf(hfj[d], G[d], t);
+            }
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                s = fmaf(G[kF + d], v[d], s);
+                t = fmaf(ph[j][d], G[kF + d], t);
+            }
+            a[j] = s;
+            sj[j] = t;
+            float b0 = G[kF], b1 = G[kF + 1], b2 = G[kF + 2];
+            if (PGO) quat_rotate_active(qt, G[kF], G[kF + 1], G[kF + 2], b0, b1, b2);   // P_j^T G[8:11]
+            b[j][0] = b0; b[j][1] = b1; b[j][2] = b2;
+            // x_j is needed again for dL2/dG once e_j is known: re-read in the second pass (not kept live)
+        } else {
+            if (dg_out) {   // dL2/dG_j = [H_f[id_j], P_j H_q]
+                float* o = dg_out + (i * nn_k + j) * kD;
+#pragma unroll
+                for (int d = 0; d < kF; ++d) o[d] = hfj[d];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) o[kF + d] = ph[j][d];
+            }
+        }
+        if (gw) a[j] += gw[i * nn_k + j];
+    }
+    if (!WF && dg_out) {   // invalid / padded neighbour slots get zeros
+#pragma unroll
+        for (int j = 0; j < kK; ++j) {
+            if (j >= nn_k || id[j] >= 0) continue;
+            float* o = dg_out + (i * nn_k + j) * kD;
+#pragma unroll
+            for (int d = 0; d < kD; ++d) o[d] = 0.f;
+        }
+    }
+    const float invS = S > 0.f ? 1.f / S : 0.f;
+    float h[kK], H = 0.f, abar = 0.f, sbar = 0.f, sig[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        const float c = -2.f * u[j] * u[j];                 // du_j = c r_j
+        h[j] = c * invS * (H3[0] * r[j][0] + H3[1] * r[j][1] + H3[2] * r[j][2]);
+        H += h[j];
+        abar = fmaf(w[j], a[j], abar);
+        sbar = fmaf(w[j], sj[j], sbar);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) sig[d] = fmaf(c, r[j][d], sig[d]);
+    }
+    float dq[3] = {0.f, 0.f, 0.f};
+    float dG[kD];
+#pragma unroll
+    for (int d = 0; d < kD; ++d) dG[d] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        if (id[j] < 0) continue;
+        const float e = h[j] - H * w[j];
+        if (dgw_out) dgw_out[i * nn_k + j] = e;
+        const float c = -2.f * u[j] * u[j];
+        const float rh = r[j][0] * H3[0] + r[j][1] * H3[1] + r[j][2] * H3[2];
+        const float da = a[j] - abar;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float du = c * r[j][d];
+            // dPhi: du (s - sbar) / S;  -H du (a - abar) / S
+            float t = du * ((sj[j] - sbar) - H * da) * invS;
+            // (a - abar) dh_j
+            const float dh = -2.f * invS * (u[j] * u[j] * H3[d] - 4.f * u[j] * u[j] * u[j] * rh * r[j][d]) +
+                             2.f * u[j] * u[j] * rh * sig[d] * invS * invS;
+            t = fmaf(da, dh, t);
+            t = fmaf(e, b[j][d], t);
+            dq[d] += t;
+        }
+        if (WF) {
+            // x_j again (features and the rotated vector) for dL2/dG and dL2/df_j
+            const int64_t ij = id[j];
+            const float4* fr = (const float4*)(p.features + ij * kF);
+            const float4 f0 = fr[0], f1 = fr[1];
+            const float f[kF] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            const int g = gids[i * nn_k + j];
+            const float4 rc = rec[g];
+            float px = rc.x, py = rc.y, pz = rc.z;
+            if (__float_as_int(rc.w) & PIN_RECORD_UNFAITHFUL) {
+                px = p.positions[3 * ij];
+                py = p.positions[3 * ij + 1];
+                pz = p.positions[3 * ij + 2];
+            }
+            float v[3] = {qx - px, qy - py, qz - pz};
+            if (PGO) quat_rotate_passive(((const float4*)p.orientations)[ij], v[0], v[1], v[2]);
+#pragma unroll
+            for (int d = 0; d < kF; ++d) {
+                const float hfd = hf ? hf[ij * kF + d] : 0.f;
+                dG[d] = fmaf(w[j], hfd, fmaf(e, f[d], dG[d]));
+            }
+#pragma unroll
+            for (int d = 0; d < 3; ++d) dG[kF + d] = fmaf(w[j], ph[j][d], fmaf(e, v[d], dG[kF + d]));
+            if (dF) {
+                float* dst = dF + ij * kF;
+#pragma unroll
+                for (int d = 0; d < kF; ++d) atomicAdd(dst + d, e * G[d]);
+            }
+        }
+    }
+    if (WF && dg_out) {
+#pragma unroll
+        for (int d = 0; d < kD; ++d) dg_out[i * kD + d] = dG[d];
+    }
+    if (dgw_out) {   // invalid / padded neighbour slots
+#pragma unroll
+        for (int j = 0; j < kK; ++j)
+            if (j < nn_k && id[j] < 0) dgw_out[i * nn_k + j] = 0.f;
+    }
+    if (dq_out) {
+        dq_out[3 * i] = dq[0];
+        dq_out[3 * i + 1] = dq[1];
+        dq_out[3 * i + 2] = dq[2];
+    }
+}
+
 // ------------------------------------------------------------------ training side effects
 __global__ void __launch_bounds__(kBlock)
 k_train_scatter(const int* __restrict__ ids, const float* __restrict__ w, int64_t total, int nn_k,
@@ -1188,6 +1379,27 @@ int pin_query_feature_fwd(const PinHash* hash, const PinPoints* pts, const float
     if (weighted_first) { if (pgo) PIN_LAUNCH_FWD(true, true); else PIN_LAUNCH_FWD(true, false); }
     else { if (pgo) PIN_LAUNCH_FWD(false, true); else PIN_LAUNCH_FWD(false, false); }
 #undef PIN_LAUNCH_FWD
+    return launch_status();
+}
+
+int pin_query_feature_bwd2(const PinPoints* pts, const float* q, int64_t n, int32_t nn_k, int32_t weighted_first,
+                           const int32_t* ids, const int32_t* gids, const float* weights, const float* grad_feat,
+                           const float* grad_weights, const float* up_q, const float* up_features, float* d_q,
+                           float* d_grad_feat, float* d_grad_weights, float* d_features, void* stream) {
+    if (!points_ok(pts) || !pts->features || n < 0) return PIN_ERR_ARG;
+    if (pts->after_pgo && !pts->orientations) return PIN_ERR_ARG;
+    if (nn_k < 1 || nn_k > kK) return PIN_ERR_UNSUPPORTED;
+    if (n == 0) return PIN_OK;
+    if (!q || !ids || !gids || !weights) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    const bool pgo = pts->after_pgo != 0;
+#define PIN_LAUNCH_BWD2(WF, PGO)                                                                                 \
+    hipLaunchKernelGGL((k_query_feature_bwd2<WF, PGO>), grid_for(n), dim3(kBlock), 0, s, *pts, q, n, nn_k, ids, \
+                       gids, weights, grad_feat, grad_weights, up_q, up_features, d_q, d_grad_feat,            \
+                       d_grad_weights, weighted_first ? d_features : nullptr)
+    if (weighted_first) { if (pgo) PIN_LAUNCH_BWD2(true, true); else PIN_LAUNCH_BWD2(true, false); }
+    else { if (pgo) PIN_LAUNCH_BWD2(false, true); else PIN_LAUNCH_BWD2(false, false); }
+#undef PIN_LAUNCH_BWD2
     return launch_status();
 }
 

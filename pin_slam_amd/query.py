@@ -158,15 +158,75 @@ def _query_feature_restated(q, feats, ids, gids, records, positions, orientation
     return out, w
 
 
+# second order through the autograd of _query_feature_restated instead of the native double
+# backward (tests compare the two)
+_QF_RESTATED = os.environ.get("PIN_QF_RESTATED", "0") == "1"
+
+
+class _Saved:
+    """The first backward's inputs kept by QueryFeatureFn (plain holder)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class QueryFeatureBwdFn(torch.autograd.Function):
+    """The first-order backward of QueryFeatureFn as a differentiable op (create_graph=True):
+    forward = pin_query_feature_bwd (grad_q and the grad_features scatter), backward =
+    pin_query_feature_bwd2, the double backward in closed form (no ATen gathers)."""
+
+    @staticmethod
+    def forward(ctx, q, feats, g_feat, g_w, sv):
+        n = sv.qd.shape[0]
+        grad_q = torch.empty_like(sv.qd) if sv.need_q else torch.zeros((0, 3), dtype=torch.float32, device=q.device)
+        grad_f = torch.zeros_like(sv.pv.features) if sv.need_f else torch.zeros((0, 8), dtype=torch.float32,
+                                                                                  device=q.device)
+        gf = g_feat.contiguous() if g_feat is not None else None
+        gw = g_w.contiguous() if g_w is not None else None
+        _lib.call("pin_query_feature_bwd", sv.pv.ref(), _lib.ptr(sv.qd), n, sv.nn_k, int(sv.wf), _lib.ptr(sv.ids),
+                  _lib.ptr(sv.gids), _lib.ptr(sv.weights), _lib.ptr(gf), _lib.ptr(gw),
+                  _lib.ptr(grad_q) if sv.need_q else None, _lib.ptr(grad_f) if sv.need_f else None, _lib.stream())
+        ctx.save_for_backward(gf, gw)
+        ctx.sv = sv
+        ctx.has = (g_feat is not None, g_w is not None)
+        if sv.need_q and sv.q_dtype != torch.float32:
+            grad_q = grad_q.to(sv.q_dtype)
+        return grad_q, grad_f
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, h_q, h_f):
+        gf, gw = ctx.saved_tensors
+        sv = ctx.sv
+        n = sv.qd.shape[0]
+        need_q, need_f, need_g, need_w = (ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                          ctx.needs_input_grad[2] and ctx.has[0], ctx.needs_input_grad[3] and ctx.has[1])
+        up_q = h_q.to(torch.float32).contiguous() if (h_q is not None and sv.need_q) else None
+        up_f = h_f.to(torch.float32).contiguous() if (h_f is not None and sv.need_f) else None
+        dq = torch.empty_like(sv.qd) if need_q else None
+        dg = torch.empty_like(gf) if need_g else None
+        dw = torch.empty_like(gw) if need_w else None
+        dF = torch.zeros_like(sv.pv.features) if need_f else None
+        if up_q is None and up_f is None:
+            return (torch.zeros_like(sv.q) if need_q else None, dF, torch.zeros_like(gf) if need_g else None,
+                    torch.zeros_like(gw) if need_w else None, None)
+        _lib.call("pin_query_feature_bwd2", sv.pv.ref(), _lib.ptr(sv.qd), n, sv.nn_k, int(sv.wf), _lib.ptr(sv.ids),
+                  _lib.ptr(sv.gids), _lib.ptr(sv.weights), _lib.ptr(gf), _lib.ptr(gw), _lib.ptr(up_q), _lib.ptr(up_f),
+                  _lib.ptr(dq), _lib.ptr(dg), _lib.ptr(dw), _lib.ptr(dF), _lib.stream())
+        if dq is not None and sv.q_dtype != torch.float32:
+            dq = dq.to(sv.q_dtype)
+        return dq, dF, dg, dw, None
+
+
 class QueryFeatureFn(torch.autograd.Function):
     """neural_points.py:528-674 forward on the GPU; backward = dL/dq and a float-atomic
     scatter of dL/dfeatures (the reference's autograd through index_put / gather).
 
     Second order (a caller differentiating the gradient, e.g. get_gradient with create_graph=True,
-    utils/tools.py:174-184): the backward is then itself differentiable -- it is taken by autograd
-    over _query_feature_restated on the kernel's own neighbour sets, so the double backward has the
-    reference's autograd semantics (the fused mapping() evaluates that case in closed form instead,
-    PIN_TRAIN_EIK); the first-order backward stays the native kernel."""
+    utils/tools.py:174-184): the backward is then itself a differentiable op, QueryFeatureBwdFn,
+    whose own backward is the closed-form double backward pin_query_feature_bwd2 (the fused
+    mapping() evaluates the eikonal case in closed form too, PIN_TRAIN_EIK).  PIN_QF_RESTATED=1
+    takes it by autograd over _query_feature_restated on the kernel's neighbour sets instead."""
 
     @staticmethod
     def forward(ctx, q, feats, hv, pv, nn_k, weighted_first, gv=None):
@@ -203,6 +263,12 @@ class QueryFeatureFn(torch.autograd.Function):
         need_q, need_f = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if not (need_q or need_f):
             return None, None, None, None, None, None, None
+        if torch.is_grad_enabled() and not _QF_RESTATED:
+            # create_graph=True: the backward as a differentiable op with a native double backward
+            sv = _Saved(pv=ctx.pv, qd=qd, ids=ids, gids=gids, weights=weights, nn_k=ctx.nn_k, wf=ctx.wf,
+                        need_q=need_q, need_f=need_f, q_dtype=ctx.q_dtype, q=q)
+            gq, gf = QueryFeatureBwdFn.apply(q, feats, g_feat, g_w, sv)
+            return (gq if need_q else None), (gf if need_f else None), None, None, None, None, None
         if torch.is_grad_enabled():   # create_graph=True: the backward must itself be differentiable
             pv = ctx.pv
             records, _, positions, orientations = pv.keep[0], pv.keep[1], pv.keep[2], pv.keep[3]

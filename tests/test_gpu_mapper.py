@@ -792,3 +792,45 @@ def test_query_feature_backward_first_order_unchanged(golden, dev):
     # evaluate the same terms in another order (measured: 1 of 49,152 elements off by 3e-6)
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=2e-5)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("wf", [True, False])
+@pytest.mark.parametrize("pgo", [False, True])
+def test_native_double_backward_matches_restated(dev, wf, pgo, monkeypatch):
+    """The closed-form double backward of query_feature (pin_query_feature_bwd2, behind
+    QueryFeatureBwdFn) against autograd over the ATen restatement on the same neighbour sets: a
+    second-order loss on both first-order gradients (dL/dq and dL/dfeatures) differentiated w.r.t.
+    the features, the decoder and the query points; weighted_first and per-neighbour, with and
+    without the after-PGO rotation of the neighbour vectors."""
+    import pin_slam_amd.query as Q
+    from pin_slam_amd.synthetic import surface_map, surface_queries
+    res = []
+    for restated in (True, False):
+        monkeypatch.setattr(Q, "_QF_RESTATED", restated)
+        nm, dec, pts = surface_map(120, device=dev, weighted_first=wf, buffer_size=1 << 20, query_backend="grid")
+        if pgo:
+            g = torch.Generator(device="cpu").manual_seed(13)
+            quat = torch.randn(nm.neural_points.shape[0], 4, generator=g).to(dev)
+            nm.point_orientations = quat / quat.norm(dim=1, keepdim=True)
+            assert nm.local_count() == nm.count()    # the whole map is local, in the same order
+            nm.local_point_orientations = nm.point_orientations.clone()
+            nm.after_pgo = True
+        q = surface_queries(pts, 3000, seed=5, device=dev).requires_grad_(True)
+        feats = nm.local_geo_features
+        geo, _, wk, _, _ = nm.query_feature(q, None, training_mode=False)
+        sdf = dec.sdf(geo)
+        if not wf:
+            sdf = torch.sum(sdf * wk, dim=1).squeeze(1)
+        gq, gfe = torch.autograd.grad(sdf.sum(), (q, feats), create_graph=True)
+        c1 = torch.linspace(-1.0, 1.0, gq.numel(), device=dev).view_as(gq)
+        c2 = torch.linspace(0.5, -0.5, gfe.numel(), device=dev).view_as(gfe)
+        loss = ((gq.norm(dim=-1) - 1.0) ** 2).mean() + (gq * c1).sum() * 1e-3 + (gfe * c2).sum()
+        leaves = [feats, q] + list(dec.parameters())
+        outs = torch.autograd.grad(loss, leaves, allow_unused=True)
+        res.append([torch.zeros_like(t) if o is None else o for o, t in zip(outs, leaves)])
+    names = ["features", "q", "W1", "b1", "W2", "b2"]
+    for name, a, b in zip(names, *res):
+        print(f"{name}: max |restated| {float(a.abs().max()):.3e}, max |native - restated| {float((a - b).abs().max()):.3e}")
+    for name, a, b in zip(names, *res):
+        # float32 sums in another order: within 1e-4 of each output's largest element (1e-7 floor)
+        assert float((a - b).abs().max()) <= 1e-4 * float(a.abs().max()) + 1e-7, name
