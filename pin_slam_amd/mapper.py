@@ -261,9 +261,13 @@ class Mapper:
         self.shard = shard
         self.slab_layout = slab_layout
         self.last_loss = None        # device f64 tensor: loss of the last iteration
-        # deterministic accumulation (FIXED_SHIFT above); default: config.deterministic, else off
-        self.deterministic = bool(getattr(config, "deterministic", False)) if deterministic is None \
-            else bool(deterministic)
+        # deterministic accumulation (FIXED_SHIFT above); default: config.deterministic, else the
+        # PIN_DETERMINISTIC environment switch, else off
+        if deterministic is None:
+            deterministic = getattr(config, "deterministic", None)
+        if deterministic is None:
+            deterministic = os.environ.get("PIN_DETERMINISTIC", "0") == "1"
+        self.deterministic = bool(deterministic)
         self._buf = _TrainBuffers()
         self._adam_t = 0
 
