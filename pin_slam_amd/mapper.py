@@ -66,6 +66,13 @@ _DEVICE_DRAWS = os.environ.get("PIN_DEVICE_DRAWS", "1") != "0"
 _AR_BUCKETS = int(os.environ.get("PIN_AR_BUCKETS", "4"))
 
 
+def _deterministic_default(config):
+    """The mode of a Mapper built without deterministic=: config.deterministic, else the
+    PIN_DETERMINISTIC environment switch (also for the reference's Mapper after install())."""
+    d = getattr(config, "deterministic", None)
+    return os.environ.get("PIN_DETERMINISTIC", "0") == "1" if d is None else bool(d)
+
+
 def _viewed_elsewhere(t: torch.Tensor) -> bool:
     """True if any tensor other than ``t`` shares t's storage (a view kept by a caller).  A view
     holds its base's storage through its TensorImpl, not through a Python reference to ``t``, so
@@ -263,11 +270,7 @@ class Mapper:
         self.last_loss = None        # device f64 tensor: loss of the last iteration
         # deterministic accumulation (FIXED_SHIFT above); default: config.deterministic, else the
         # PIN_DETERMINISTIC environment switch, else off
-        if deterministic is None:
-            deterministic = getattr(config, "deterministic", None)
-        if deterministic is None:
-            deterministic = os.environ.get("PIN_DETERMINISTIC", "0") == "1"
-        self.deterministic = bool(deterministic)
+        self.deterministic = _deterministic_default(config) if deterministic is None else bool(deterministic)
         self._buf = _TrainBuffers()
         self._adam_t = 0
 
@@ -928,7 +931,8 @@ class Mapper:
         cfg = P.cfg = _lib.PinTrainCfg.from_buffer_copy(cfg_rows)
         cfg.flags = _lib.PIN_TRAIN_ROWS
         P.tiled = grid and _TILE_QUERIES and rows >= _TRAIN_TILE_MIN
-        det = P.det = bool(getattr(self, "deterministic", getattr(c, "deterministic", False)))
+        det = P.det = bool(getattr(self, "deterministic", None) if hasattr(self, "deterministic")
+                           else _deterministic_default(c))
         st = P.st = _lib.PinTrainState(ids=b.ids.data_ptr(), weights=b.weights.data_ptr(), x=b.x.data_ptr(),
                                        sdf=b.sdf.data_ptr(), certainties=nm.local_point_certainties.data_ptr(),
                                        ts_update=nm.local_point_ts_update.data_ptr() if P.ts64 is not None else None,

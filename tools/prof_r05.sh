@@ -33,4 +33,8 @@ if [[ $S == *dbwd* ]]; then
     run dbwd 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dbwd -o run -- \
         python3 -m pytest -q tests/test_gpu_mapper.py -k "double_backward_matches_reference and grid"
 fi
+if [[ $S == *dbloop* ]]; then
+    run dbloop 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dbloop -o run -- \
+        python3 tools/dbwd_loop.py
+fi
 echo "end $(date)" >> $OUT/summary.txt
