@@ -571,6 +571,31 @@ typedef struct PinAdamStep {
 /* decoder-parameter gradient layout of pin_train_backward's mlp_grad */
 #define PIN_MLP_GRAD_SIZE (PIN_HIDDEN_DIM * (PIN_FEATURE_DIM + 3) + 2 * PIN_HIDDEN_DIM + 1) /* W1,b1,W2,b2 */
 
+/*
+ * The drop-in Decoder.sdf (model/decoder.py:66-88, the 11 -> 64 -> 1 ReLU decoder with bias)
+ * on rows and its autograd, for callers that go through NeuralPoints.query_feature + Decoder.sdf
+ * (utils/mapper.py:448-573 with autograd, utils/tools.py:174-184 get_gradient):
+ *
+ * pin_mlp_forward -- out[r] = s (w2 . relu(W1 x_r + b1) + b2), x [n, 11], s = mlp->sdf_scale.
+ *
+ * pin_mlp_backward -- with m_c(r) = [W1[c] . x_r + b1_c > 0] (recomputed from x):
+ *   gx   [n, 11] (may be NULL) = go_r s W1^T (w2 o m(r))                 first order, input
+ *   d_go [n]     (may be NULL) = s sum_c w2_c m_c(r) (W1[c] . e_r)       second order: the
+ *        gradient of (gx . e) w.r.t. go, for the double backward of get_gradient
+ *   mlp_grad [PIN_MLP_GRAD_SIZE] += (W1, b1, W2, b2 layout):
+ *     flags & PIN_MLP_GRAD_FIRST:  the first-order parameter gradients of sum_r go_r out_r;
+ *     flags & PIN_MLP_GRAD_SECOND: the second-order ones, d(sum_r gx_r . e_r)/d params with the
+ *       masks held constant: dW1 = s w2 o sum_r m go e^T, dW2 = s W1 . sum_r m go e (b1, b2: 0).
+ *   Sums over rows in a fixed order (per-block products on the f32 matrix cores, then one final
+ *   reduction).  workspace: pin_mlp_backward_workspace_bytes(n) when flags != 0.
+ */
+#define PIN_MLP_GRAD_FIRST 1
+#define PIN_MLP_GRAD_SECOND 2
+int pin_mlp_forward(const PinMlp* mlp, const float* x, int64_t n, float* out, void* stream);
+int64_t pin_mlp_backward_workspace_bytes(int64_t n);
+int pin_mlp_backward(const PinMlp* mlp, const float* x, int64_t n, const float* go, const float* e, int32_t flags,
+                     float* gx, float* d_go, float* mlp_grad, void* workspace, void* stream);
+
 /* pin_train_rows -- coordinates [rows,3] of every row of one iteration (batch + stencil). */
 int pin_train_rows(const float* coord, const PinTrainCfg* cfg, float* rows_out, void* stream);
 
@@ -793,6 +818,36 @@ int pin_prune_rows(const PinMapArrays* map, const float* travel_dist, int64_t cu
  */
 int pin_map_gather(const PinMapArrays* src, const int64_t* rows, int64_t n_rows, int32_t pad_row,
                    const PinMapArrays* dst, void* stream);
+
+/*
+ * pin_pool_window -- the training pool's window filter (utils/mapper.py:226-262):
+ * keep[0..k) = the rows i < n (ascending) with sum((coord[i] - center)^2) < radius2, counts[0] = k,
+ * counts[1] = the kept rows with i >= tail_start (the current frame's samples, :256-259).
+ * center: 3 values on the device, double when center_f64 (then the arithmetic is f64, as torch
+ * promotes an f32 pool minus an f64 pose), else float (f32 arithmetic, radius2 rounded to f32);
+ * the sum in the reference's order.  One host read of counts sizes what follows.
+ * workspace: pin_map_workspace_bytes(n).
+ */
+int pin_pool_window(const float* coord, int64_t n, const void* center, int32_t center_f64, double radius2,
+                    int64_t tail_start, int64_t* keep, int64_t* counts, void* workspace, void* stream);
+
+/* One array of a multi-array row gather: row i of dst = row rows[i] of src, row_bytes each. */
+typedef struct PinRowArray {
+    const void* src;
+    void* dst;
+    int64_t row_bytes;
+} PinRowArray;
+#define PIN_ROW_ARRAYS_MAX 8
+
+/*
+ * pin_gather_rows -- for every array a < n_arrays (<= PIN_ROW_ARRAYS_MAX):
+ * a.dst[i] = a.src[rows[i]] (row_bytes bytes), i < n_rows, all arrays in one launch; each row
+ * moves with the widest of 16/8/4/1-byte accesses its size and both pointers allow.  The training
+ * pool's window filter (utils/mapper.py:226-262: the index selection of coord, global coord,
+ * label, weight, ts and the packed records by one kept-row list) -- torch.index_select per pool
+ * in the reference.  rows must be in [0, source rows); dst must not overlap src.
+ */
+int pin_gather_rows(const PinRowArray* arrays, int32_t n_arrays, const int64_t* rows, int64_t n_rows, void* stream);
 
 /*
  * pin_map_scatter -- dst.x[rows[i]] = src.x[i] for every array non-NULL in src (assign_local_to_

@@ -111,6 +111,13 @@ class PinMapArrays(ctypes.Structure):
                 ("reserved", i32)]
 
 
+class PinRowArray(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("row_bytes", i64)]
+
+
+ROW_ARRAYS_MAX = 8   # PIN_ROW_ARRAYS_MAX
+MLP_GRAD_FIRST, MLP_GRAD_SECOND = 1, 2   # pin_mlp_backward flags
+
 MLP_GRAD_SIZE = HIDDEN_DIM * (FEATURE_DIM + 3) + 2 * HIDDEN_DIM + 1
 MLP_PART_FLOATS = 2 * HIDDEN_DIM * 16 + 16   # PIN_MLP_PART_FLOATS: per-block decoder-gradient partial
 
@@ -200,13 +207,19 @@ _SIGS = {
     "pin_local_map": [_P(PinMapArrays), c_void_p, c_void_p, i32, i64, ctypes.c_double, f32, i32, i32, i64, i64,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_prune_rows": [_P(PinMapArrays), c_void_p, i64, f32, f32, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_mlp_forward": [_P(PinMlp), c_void_p, i64, c_void_p, c_void_p],
+    "pin_mlp_backward_workspace_bytes": [i64],
+    "pin_mlp_backward": [_P(PinMlp), c_void_p, i64, c_void_p, c_void_p, i32, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p],
+    "pin_pool_window": [c_void_p, i64, c_void_p, i32, ctypes.c_double, i64, c_void_p, c_void_p, c_void_p, c_void_p],
+    "pin_gather_rows": [_P(PinRowArray), i32, c_void_p, i64, c_void_p],
     "pin_map_gather": [_P(PinMapArrays), c_void_p, i64, i32, _P(PinMapArrays), c_void_p],
     "pin_map_scatter": [_P(PinMapArrays), c_void_p, i64, i32, _P(PinMapArrays), c_void_p],
     "pin_map_adjust": [_P(PinMapArrays), c_void_p, i64, i32, c_void_p],
 }
 # functions whose return value is not a status code
 _RESTYPES = {"pin_map_workspace_bytes": i64, "pin_mc_workspace_bytes": i64,
-             "pin_query_sort_stable_workspace_bytes": i64}
+             "pin_query_sort_stable_workspace_bytes": i64, "pin_mlp_backward_workspace_bytes": i64}
 
 _lib = None
 

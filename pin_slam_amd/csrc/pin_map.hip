@@ -343,6 +343,37 @@ k_keep_flags(const int64_t* __restrict__ tu, const float* __restrict__ cert, int
     flags[i] = (inactive && cert[i] < cert_thre) ? 0 : 1;
 }
 
+// ----------------------------------------------------------------------------- pool window filter
+// utils/mapper.py:226-233: torch.sum((coord - origin) ** 2, dim=-1) < window_radius ** 2 with
+// torch's type promotion: an f64 pose makes the difference, squares, sum and bound f64; an f32
+// pose keeps them f32 (the bound rounded to f32); the three-term sum in the reference's order
+template <typename T>
+__global__ void __launch_bounds__(kBlock)
+k_window_flags(const float* __restrict__ coord, int64_t n, const T* __restrict__ center, T r2,
+               int32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const T dx = (T)coord[3 * i] - center[0], dy = (T)coord[3 * i + 1] - center[1], dz = (T)coord[3 * i + 2] - center[2];
+    const T d2 = (dx * dx + dy * dy) + dz * dz;
+    flags[i] = d2 < r2 ? 1 : 0;
+}
+
+// kept rows in order, and counts = {kept rows, kept rows at index >= tail_start}
+__global__ void __launch_bounds__(kBlock)
+k_window_write(const int32_t* __restrict__ flags, const int64_t* __restrict__ incl, int64_t n, int64_t tail_start,
+               int64_t* __restrict__ keep, int64_t* __restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        const int64_t total = n > 0 ? incl[n - 1] : 0;
+        const int64_t t = tail_start < 0 ? 0 : tail_start > n ? n : tail_start;
+        counts[0] = total;
+        counts[1] = total - (t > 0 ? incl[t - 1] : 0);
+        return;
+    }
+    if (flags[i]) keep[incl[i] - 1] = i;
+}
+
 // ----------------------------------------------------------------------------- gather / scatter
 // One thread per row: every array of the row moves with 16/8/4-byte loads and stores.  The
 // local / kept row lists are ascending, so neighbouring lanes touch neighbouring rows.
@@ -421,6 +452,44 @@ int move_rows(const PinMapArrays* src, const PinMapArrays* dst, const int64_t* r
                            (uint32_t*)(dst->features + drow * F), F);
     }
     return status(hipSuccess);
+}
+
+// ----------------------------------------------------------------------------- multi-array gather
+struct RowArrays {
+    const unsigned char* src[PIN_ROW_ARRAYS_MAX];
+    unsigned char* dst[PIN_ROW_ARRAYS_MAX];
+    int64_t units[PIN_ROW_ARRAYS_MAX];   // accesses per row
+    int32_t shift[PIN_ROW_ARRAYS_MAX];   // log2 of the access width: 4 (16 B), 3, 2 or 0
+    int32_t n;
+};
+
+template <typename T>
+__device__ __forceinline__ void copy_units(const unsigned char* s, unsigned char* d, int64_t units) {
+    const T* a = (const T*)s;
+    T* b = (T*)d;
+    for (int64_t u = 0; u < units; ++u) b[u] = a[u];
+}
+
+// one thread per output row, every array: the kept-row list is ascending, so neighbouring lanes
+// read neighbouring source rows
+__global__ void __launch_bounds__(kBlock)
+k_gather_rows(RowArrays A, const int64_t* __restrict__ rows, int64_t n_rows) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n_rows) return;
+    const int64_t r = rows[i];
+    for (int a = 0; a < A.n; ++a) {
+        const int64_t units = A.units[a];
+        const int sh = A.shift[a];
+        const int64_t bytes = units << sh;
+        const unsigned char* s = A.src[a] + r * bytes;
+        unsigned char* d = A.dst[a] + i * bytes;
+        switch (sh) {
+            case 4: copy_units<uint4>(s, d, units); break;
+            case 3: copy_units<uint2>(s, d, units); break;
+            case 2: copy_units<uint32_t>(s, d, units); break;
+            default: copy_units<unsigned char>(s, d, units); break;
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------- pose adjustment
@@ -613,6 +682,57 @@ int pin_prune_rows(const PinMapArrays* map, const float* travel_dist, int64_t cu
     }
     hipLaunchKernelGGL(k_local_write, dim3(blocks_for(M + 1)), dim3(kBlock), 0, s, flags, incl, M, (int64_t)0,
                        (uint8_t*)nullptr, (int64_t*)nullptr, keep_rows, keep_count);
+    return status(hipSuccess);
+}
+
+int pin_pool_window(const float* coord, int64_t n, const void* center, int32_t center_f64, double radius2,
+                    int64_t tail_start, int64_t* keep, int64_t* counts, void* workspace, void* stream) {
+    if (n < 0 || !center || !counts || !workspace || (n > 0 && (!coord || !keep))) return PIN_ERR_ARG;
+    auto s = as_stream(stream);
+    Carve c{(char*)workspace};
+    c.take<uint64_t>(n);
+    c.take<uint64_t>(n);
+    c.take<int64_t>(n);
+    c.take<int64_t>(n);
+    int32_t* flags = c.take<int32_t>(n);
+    c.take<int32_t>(n);
+    c.take<int32_t>(n);
+    int64_t* incl = c.take<int64_t>(n + 1);
+    c.take<VdsStats>(1);
+    const size_t temp_bytes = std::max(sort_temp_bytes(n), scan_temp_bytes(n + 1));
+    void* temp = c.take<char>((int64_t)temp_bytes);
+    if (n > 0) {
+        if (center_f64)
+            hipLaunchKernelGGL(k_window_flags<double>, dim3(blocks_for(n)), dim3(kBlock), 0, s, coord, n,
+                               (const double*)center, radius2, flags);
+        else
+            hipLaunchKernelGGL(k_window_flags<float>, dim3(blocks_for(n)), dim3(kBlock), 0, s, coord, n,
+                               (const float*)center, (float)radius2, flags);
+        size_t tb = temp_bytes;
+        if (incl_scan(temp, tb, flags, incl, n, s) != hipSuccess) return PIN_ERR_HIP;
+    }
+    hipLaunchKernelGGL(k_window_write, dim3(blocks_for(n + 1)), dim3(kBlock), 0, s, flags, incl, n, tail_start, keep,
+                       counts);
+    return status(hipSuccess);
+}
+
+int pin_gather_rows(const PinRowArray* arrays, int32_t n_arrays, const int64_t* rows, int64_t n_rows, void* stream) {
+    if (n_arrays < 0 || n_arrays > PIN_ROW_ARRAYS_MAX || n_rows < 0 || (n_arrays > 0 && !arrays)) return PIN_ERR_ARG;
+    if (n_rows > 0 && !rows) return PIN_ERR_ARG;
+    RowArrays A{};
+    for (int a = 0; a < n_arrays; ++a) {
+        const PinRowArray& x = arrays[a];
+        if (x.row_bytes < 0 || (x.row_bytes > 0 && (!x.src || !x.dst))) return PIN_ERR_ARG;
+        const uintptr_t align = (uintptr_t)x.src | (uintptr_t)x.dst | (uintptr_t)x.row_bytes;
+        const int sh = (align & 15) == 0 ? 4 : (align & 7) == 0 ? 3 : (align & 3) == 0 ? 2 : 0;
+        A.src[A.n] = (const unsigned char*)x.src;
+        A.dst[A.n] = (unsigned char*)x.dst;
+        A.units[A.n] = x.row_bytes >> sh;
+        A.shift[A.n] = sh;
+        A.n += x.row_bytes > 0 ? 1 : 0;
+    }
+    if (A.n == 0 || n_rows == 0) return PIN_OK;
+    hipLaunchKernelGGL(k_gather_rows, dim3(blocks_for(n_rows)), dim3(kBlock), 0, as_stream(stream), A, rows, n_rows);
     return status(hipSuccess);
 }
 

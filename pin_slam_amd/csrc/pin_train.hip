@@ -1396,6 +1396,105 @@ __global__ void __launch_bounds__(kTBlock) k_mlp_grad_final(const float* __restr
     }
 }
 
+// ----------------------------------------------------------------------------- Decoder.sdf rows
+// The drop-in Decoder.sdf (model/decoder.py:66-88) on rows x [n, 11] and its autograd: the
+// forward, the first-order backward (input gradient, parameter products) and the double backward
+// of the input gradient (the analytic eikonal through get_gradient(create_graph=True),
+// utils/tools.py:174-184).  The ReLU masks are piecewise constant, so the second-order terms are
+// bilinear in (go, e): with u_c = W1[c] . e,
+//   d(gx . e)/d go = s sum_c w2_c m_c u_c,  d/dW1[c][i] = s w2_c sum_r m_c go e_i,
+//   d/dw2_c = s W1[c] . sum_r m_c go e     -- k_mlp_grad_final's T' terms with e' = go e.
+constexpr int kMlpRowBlocks = 1024;   // persistent grid of the row backward: bounded partials
+
+__global__ void __launch_bounds__(kTBlock)
+k_mlp_forward(PinMlp m, const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+    __shared__ float s_w[kWSize];
+    const MlpW mw = stage_mlp(m, s_w);
+    for (int64_t r = (int64_t)blockIdx.x * kTBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kTBlock) {
+        float xv[kD];
+#pragma unroll
+        for (int i = 0; i < kD; ++i) xv[i] = x[r * kD + i];
+        float g1[1];
+        out[r] = mlp_sdf<false, 0, 1>(mw, xv, g1);
+    }
+}
+
+// GX: gx[r] = go_r s W1^T (w2 o m);  DGO: d_go[r] = s sum_c w2_c m_c (W1[c] . e_r);
+// FIRST / SECOND: the block's parameter products (T from so = go s, T' from go e) into part
+template <bool GX, bool DGO, bool FIRST, bool SECOND>
+__global__ void __launch_bounds__(kTBlock)
+k_mlp_backward(PinMlp m, const float* __restrict__ x, int64_t n, const float* __restrict__ go,
+               const float* __restrict__ e, float* __restrict__ gx, float* __restrict__ d_go,
+               float* __restrict__ part) {
+    constexpr bool PARAMS = FIRST || SECOND;
+    __shared__ float s_w[kWSize];
+    __shared__ float s_mg[PARAMS ? kWaves : 1][PARAMS ? kMgWave : 1];
+    __shared__ float s_so[kWaves];
+    const MlpW mw = stage_mlp(m, s_w);
+    const float s = m.sdf_scale;
+    f32x4 accT[4], accE[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) accT[k] = accE[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float so_sum = 0.f;
+    const int64_t stride = (int64_t)gridDim.x * kTBlock;
+    const int64_t iters = (n + stride - 1) / stride;   // uniform over the block: every lane joins the MFMAs
+    for (int64_t it = 0; it < iters; ++it) {
+        const int64_t r = it * stride + (int64_t)blockIdx.x * kTBlock + threadIdx.x;
+        const bool live = r < n;
+        float xv[kD], ev[kD];
+        float g = 0.f;
+#pragma unroll
+        for (int i = 0; i < kD; ++i) {
+            xv[i] = live ? x[r * kD + i] : 0.f;
+            ev[i] = (live && (DGO || SECOND)) ? e[r * kD + i] : 0.f;
+        }
+        if (live && (GX || PARAMS)) g = go[r];
+        float ga[kD];
+#pragma unroll
+        for (int i = 0; i < kD; ++i) ga[i] = 0.f;
+        float dg = 0.f;
+        uint32_t lo = 0u, hi = 0u;
+#pragma unroll 2
+        for (int c = 0; c < kH; ++c) {
+            float wr[kWRow];
+            load_row(mw.w, c, wr);
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < kD; ++i) acc = fmaf(wr[i], xv[i], acc);
+            const bool on = acc + mw.w[kWB1 + c] > 0.f;
+            const float a = on ? mw.w[kWW2 + c] : 0.f;
+            if (GX) {
+#pragma unroll
+                for (int i = 0; i < kD; ++i) ga[i] = fmaf(a, wr[i], ga[i]);
+            }
+            if (DGO) {
+                float u = 0.f;
+#pragma unroll
+                for (int i = 0; i < kD; ++i) u = fmaf(wr[i], ev[i], u);
+                dg = fmaf(a, u, dg);
+            }
+            const uint32_t bit = on ? 1u << (c & 31) : 0u;
+            if (c < 32) lo |= bit; else hi |= bit;
+        }
+        if (live && GX) {
+            const float k = s * g;
+#pragma unroll
+            for (int i = 0; i < kD; ++i) gx[r * kD + i] = ga[i] * k;
+        }
+        if (live && DGO) d_go[r] = dg * s;
+        if constexpr (PARAMS) {
+            const uint64_t mask = live ? (((uint64_t)hi << 32) | lo) : 0ull;
+            const float so = (FIRST && live) ? g * s : 0.f;
+            float e2[kD];
+#pragma unroll
+            for (int i = 0; i < kD; ++i) e2[i] = SECOND ? g * ev[i] : 0.f;
+            mlp_grad_mfma<SECOND>(s_mg[threadIdx.x >> 6], mask, so, xv, e2, accT, accE);
+            so_sum += so;
+        }
+    }
+    if constexpr (PARAMS) mlp_grad_flush<SECOND>(s_mg, s_so, accT, accE, so_sum, part + (int64_t)blockIdx.x * kMlpPart);
+}
+
 // torch.optim.Adam (single-tensor form, weight_decay 0), four elements per thread:
 //   m = m + (1-b1)(g - m);  v = v b2 + ((1-b1') g) g;  p += (-lr/bc1 * m) / (sqrt(v)/sqrt(bc2) + eps)
 // Element i's gradient sits at (i/8)*grad_stride + i%8 (64-B accumulator rows: lanes 0..7).
@@ -1577,6 +1676,51 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
 }  // namespace
 
 extern "C" {
+
+int pin_mlp_forward(const PinMlp* mlp, const float* x, int64_t n, float* out, void* stream) {
+    if (!mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0 || (n > 0 && (!x || !out))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    const int64_t nb = std::min<int64_t>((n + kTBlock - 1) / kTBlock, 8192);
+    hipLaunchKernelGGL(k_mlp_forward, dim3((unsigned)nb), dim3(kTBlock), 0, as_stream(stream), *mlp, x, n, out);
+    return launch_status();
+}
+
+int64_t pin_mlp_backward_workspace_bytes(int64_t n) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + kTBlock - 1) / kTBlock, kMlpRowBlocks));
+    return nb * kMlpPart * (int64_t)sizeof(float);
+}
+
+int pin_mlp_backward(const PinMlp* mlp, const float* x, int64_t n, const float* go, const float* e, int32_t flags,
+                     float* gx, float* d_go, float* mlp_grad, void* workspace, void* stream) {
+    const bool first = (flags & PIN_MLP_GRAD_FIRST) != 0, second = (flags & PIN_MLP_GRAD_SECOND) != 0;
+    const bool params = first || second;
+    if (!mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || n < 0) return PIN_ERR_ARG;
+    if ((flags & ~(PIN_MLP_GRAD_FIRST | PIN_MLP_GRAD_SECOND)) != 0) return PIN_ERR_ARG;
+    if (params && (!mlp_grad || !workspace)) return PIN_ERR_ARG;
+    if (n > 0 && (!x || ((gx || params) && !go) || ((d_go || second) && !e))) return PIN_ERR_ARG;
+    if (n == 0) return PIN_OK;
+    auto st = as_stream(stream);
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((n + kTBlock - 1) / kTBlock, kMlpRowBlocks));
+    float* part = (float*)workspace;
+    const int key = (gx ? 1 : 0) | (d_go ? 2 : 0) | (first ? 4 : 0) | (second ? 8 : 0);
+#define PIN_MLP_BWD(K)                                                                                           \
+    case K:                                                                                                      \
+        hipLaunchKernelGGL((k_mlp_backward<(K & 1) != 0, (K & 2) != 0, (K & 4) != 0, (K & 8) != 0>), dim3((unsigned)nb), \
+                           dim3(kTBlock), 0, st, *mlp, x, n, go, e, gx, d_go, part);                             \
+        break;
+    switch (key) {
+        case 0: return PIN_OK;
+        PIN_MLP_BWD(1) PIN_MLP_BWD(2) PIN_MLP_BWD(3) PIN_MLP_BWD(4) PIN_MLP_BWD(5) PIN_MLP_BWD(6) PIN_MLP_BWD(7)
+        PIN_MLP_BWD(8) PIN_MLP_BWD(9) PIN_MLP_BWD(10) PIN_MLP_BWD(11) PIN_MLP_BWD(12) PIN_MLP_BWD(13)
+        PIN_MLP_BWD(14) PIN_MLP_BWD(15)
+    }
+#undef PIN_MLP_BWD
+    if (params)
+        hipLaunchKernelGGL(k_mlp_grad_final, dim3(kH / 4), dim3(kTBlock), 0, st, part, nb, second ? 1 : 0, *mlp,
+                           mlp_grad, (const double*)nullptr, (int64_t)0, (double*)nullptr);
+    return launch_status();
+}
+
 
 static int adam_segs(float* const* params, const int64_t* sizes, int nseg, AdamSegs& sg) {
     if (!params || !sizes || nseg < 1 || nseg > kMaxSeg) return PIN_ERR_ARG;

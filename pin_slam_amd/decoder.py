@@ -4,12 +4,104 @@ Same module structure (``layers`` ModuleList + ``lout``) so state_dict keys
 ``layers.{i}.weight/bias`` and ``lout.weight/bias`` load unchanged, and the same
 ``sdf`` / ``occupancy`` / ``sem_label_prob`` / ``regress_color`` heads.  The
 fused tracker/mesher/mapper kernels read the geo decoder's weights directly
-(pin_slam_amd.query.mlp_view); ``sdf`` itself is the plain module forward used
-by callers that go through ``NeuralPoints.query_feature``.
+(pin_slam_amd.query.mlp_view).  ``sdf`` -- used by callers that go through
+``NeuralPoints.query_feature`` (the reference's Mapper.sdf, get_numerical_gradient,
+get_gradient with create_graph) -- runs the HIP row kernels for the geo decoder shape
+(11 -> 64 -> 1, ReLU, bias; pin_mlp_forward / pin_mlp_backward) as an autograd Function
+whose backward is itself differentiable (the double backward of get_gradient); other
+decoder shapes (semantic / colour heads, time-conditioned input) are the module's layers.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from . import _lib
+
+# PIN_DECODER_ATEN=1: Decoder.sdf through the nn.Linear layers (A/B and restatement checks)
+_ATEN_SDF = os.environ.get("PIN_DECODER_ATEN", "0") == "1"
+
+
+def _mlp_grad_split(g, W1, b1, W2, b2):
+    """pin_mlp_backward's mlp_grad layout (W1 [64,11], b1, W2, b2) as the parameters' shapes."""
+    h, d = W1.shape
+    return (g[:h * d].view_as(W1), g[h * d:h * d + h].view_as(b1), g[h * d + h:2 * h + h * d].view_as(W2),
+            g[2 * h + h * d:].view_as(b2))
+
+
+def _rows_backward(dec, rows, go, e, flags, want_gx, want_dgo):
+    """One pin_mlp_backward call: (gx [n,11] or None, d_go [n] or None, mlp_grad or None)."""
+    from .query import mlp_view
+    n = rows.shape[0]
+    dev = rows.device
+    gx = torch.empty((n, rows.shape[1]), dtype=torch.float32, device=dev) if want_gx else None
+    d_go = torch.empty((n,), dtype=torch.float32, device=dev) if want_dgo else None
+    mg = torch.zeros((_lib.MLP_GRAD_SIZE,), dtype=torch.float32, device=dev) if flags else None
+    ws = torch.empty((int(_lib.fn("pin_mlp_backward_workspace_bytes")(n)),), dtype=torch.uint8, device=dev) \
+        if flags else None
+    _lib.call("pin_mlp_backward", mlp_view(dec).ref(), _lib.ptr(rows), n, _lib.ptr(go), _lib.ptr(e), flags,
+              _lib.ptr(gx), _lib.ptr(d_go), _lib.ptr(mg), _lib.ptr(ws), _lib.stream())
+    return gx, d_go, mg
+
+
+class _SdfRowsFn(torch.autograd.Function):
+    """out = Decoder.sdf(x) for x [..., 11] (pin_mlp_forward); backward: pin_mlp_backward, or
+    under create_graph the differentiable _SdfRowsBwdFn."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, dec):
+        from .query import mlp_view
+        rows = x.detach().reshape(-1, x.shape[-1]).contiguous()
+        n = rows.shape[0]
+        out = torch.empty((n,), dtype=torch.float32, device=x.device)
+        _lib.call("pin_mlp_forward", mlp_view(dec).ref(), _lib.ptr(rows), n, _lib.ptr(out), _lib.stream())
+        ctx.save_for_backward(rows, W1, b1, W2, b2)
+        ctx.dec, ctx.xshape = dec, x.shape
+        return out.view(tuple(x.shape[:-1]) + (1,))
+
+    @staticmethod
+    def backward(ctx, g):
+        rows, W1, b1, W2, b2 = ctx.saved_tensors
+        need_x, need_p = ctx.needs_input_grad[0], any(ctx.needs_input_grad[1:5])
+        if torch.is_grad_enabled():   # create_graph: a differentiable backward
+            gx, dW1, db1, dW2, db2 = _SdfRowsBwdFn.apply(g, rows, W1, b1, W2, b2, ctx.dec, need_x, need_p)
+        else:
+            go = g.detach().reshape(-1).to(torch.float32).contiguous()
+            gx, _, mg = _rows_backward(ctx.dec, rows, go, None, _lib.MLP_GRAD_FIRST if need_p else 0, need_x, False)
+            dW1, db1, dW2, db2 = _mlp_grad_split(mg, W1, b1, W2, b2) if need_p else (None,) * 4
+        return (gx.view(ctx.xshape) if gx is not None else None), dW1, db1, dW2, db2, None
+
+
+class _SdfRowsBwdFn(torch.autograd.Function):
+    """The first-order backward of _SdfRowsFn as a function of (go, parameters): outputs gx and the
+    parameter gradients; its backward (the double backward) takes dL/d(gx) = e and returns
+    dL/d(go) and the second-order parameter gradients (pin_mlp_backward with e; the ReLU masks
+    are piecewise constant, so dL/dx is zero).  Gradients flowing into the parameter-gradient
+    outputs (a third order) are not implemented."""
+
+    @staticmethod
+    def forward(ctx, g, rows, W1, b1, W2, b2, dec, need_x, need_p):
+        ctx.set_materialize_grads(False)
+        go = g.detach().reshape(-1).to(torch.float32).contiguous()
+        gx, _, mg = _rows_backward(dec, rows, go, None, _lib.MLP_GRAD_FIRST if need_p else 0, need_x, False)
+        ctx.save_for_backward(go, rows, W1, b1, W2, b2)
+        ctx.dec, ctx.gshape = dec, g.shape
+        dW1, db1, dW2, db2 = _mlp_grad_split(mg, W1, b1, W2, b2) if need_p else (None,) * 4
+        return gx, dW1, db1, dW2, db2
+
+    @staticmethod
+    def backward(ctx, d_gx, d_dW1, d_db1, d_dW2, d_db2):
+        if any(t is not None for t in (d_dW1, d_db1, d_dW2, d_db2)):
+            raise NotImplementedError("Decoder.sdf: differentiating the parameter gradients (third order)")
+        go, rows, W1, b1, W2, b2 = ctx.saved_tensors
+        if d_gx is None:
+            return (None,) * 9
+        need_go, need_p = ctx.needs_input_grad[0], any(ctx.needs_input_grad[2:6])
+        e = d_gx.detach().reshape(rows.shape).to(torch.float32).contiguous()
+        _, d_go, mg = _rows_backward(ctx.dec, rows, go, e, _lib.MLP_GRAD_SECOND if need_p else 0, False, need_go)
+        dW1, db1, dW2, db2 = _mlp_grad_split(mg, W1, b1, W2, b2) if need_p else (None,) * 4
+        return (d_go.view(ctx.gshape) if d_go is not None else None), None, dW1, db1, dW2, db2, None, None, None
 
 
 class Decoder(nn.Module):
@@ -43,8 +135,23 @@ class Decoder(nn.Module):
             x = act(layer(x))
         return x
 
+    def _rows_ok(self, x):
+        """The HIP row kernels cover the geo decoder: one hidden layer of PIN_HIDDEN_DIM units,
+        ReLU, bias, one output, f32 inputs of width 11 on the GPU."""
+        if _ATEN_SDF or not x.is_cuda or x.dtype != torch.float32 or len(self.layers) != 1 or self.out_dim != 1:
+            return False
+        l0 = self.layers[0]
+        return (not self.use_leaky_relu and l0.bias is not None and self.lout.bias is not None
+                and l0.in_features == x.shape[-1] == _lib.FEATURE_DIM + 3 and l0.out_features == _lib.HIDDEN_DIM
+                and all(p.dtype == torch.float32 and p.is_cuda for p in (l0.weight, l0.bias, self.lout.weight,
+                                                                          self.lout.bias)))
+
     def sdf(self, features):
-        """model/decoder.py:66-88 (prediction is the scaled sdf)."""
+        """model/decoder.py:66-88 (prediction is the scaled sdf): HIP row kernels for the geo
+        decoder (differentiable to second order), the module's layers otherwise."""
+        if self._rows_ok(features):
+            l0 = self.layers[0]
+            return _SdfRowsFn.apply(features, l0.weight, l0.bias, self.lout.weight, self.lout.bias, self).squeeze(1)
         out = self.lout(self._trunk(features)).squeeze(1)
         return out * self.sdf_scale
 

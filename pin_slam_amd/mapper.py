@@ -370,29 +370,45 @@ class Mapper:
             self._pool_packed = self._pool_append("packed", self._pool_packed,
                                                   self._pack(global_coord, sdf_label, time_repeat, weight))
         if (frame_id + 1) % int(c.pool_filter_freq) == 0:                                # :226-262
-            rel = self.global_coord_pool - frame_origin.to(self.global_coord_pool)
-            filter_mask = torch.sum(rel ** 2, dim=-1) < c.window_radius ** 2
-            true_indices = torch.nonzero(filter_mask).squeeze()
-            pool_sample_count = true_indices.shape[0]
+            # the sphere test, the kept-row list and both counts in one pass (pin_pool_window),
+            # one host read for the counts; the origin keeps the pose's dtype (torch promotes the
+            # f32 pool against an f64 pose)
+            pool = self.global_coord_pool
+            n_pool = pool.shape[0]
+            origin = frame_origin.detach()
+            f64 = origin.dtype == torch.float64
+            origin = origin.to(device=pool.device, dtype=torch.float64 if f64 else torch.float32).contiguous()
+            keep_all = torch.empty((max(n_pool, 1),), dtype=torch.int64, device=pool.device)
+            counts = torch.empty((2,), dtype=torch.int64, device=pool.device)
+            tail_start = n_pool - self.cur_sample_count if self.cur_sample_count > 0 else 0   # [-0:] is all
+            from .neural_points import map_workspace
+            _lib.call("pin_pool_window", _lib.ptr(pool.contiguous()), n_pool, _lib.ptr(origin), int(f64),
+                      float(c.window_radius) ** 2, tail_start, _lib.ptr(keep_all), _lib.ptr(counts),
+                      _lib.ptr(map_workspace(n_pool, pool.device)), _lib.stream())
+            pool_sample_count, cur_kept = (int(v) for v in counts.cpu().tolist())
+            keep = keep_all[:pool_sample_count]
             if pool_sample_count > c.pool_capacity:
+                # the reference's random discards over the kept rows (:241-245), then the mask's rows
                 discard_count = pool_sample_count - int(c.pool_capacity)
                 discarded_index = self._randint(pool_sample_count, discard_count)
-                filter_mask[true_indices[discarded_index]] = False
-            keep = torch.nonzero(filter_mask).squeeze(1)   # one compaction index for every pool
-            self.coord_pool = self._pool_compact("coord", self.coord_pool, keep)
-            self.global_coord_pool = self._pool_compact("global_coord", self.global_coord_pool, keep)
-            self.sdf_label_pool = self._pool_compact("sdf_label", self.sdf_label_pool, keep)
-            self.weight_pool = self._pool_compact("weight", self.weight_pool, keep)
-            self.time_pool = self._pool_compact("time", self.time_pool, keep)
-            if track:
-                self._pool_packed = self._pool_compact("packed", self._pool_packed, keep)
-            if sem_label is not None:
-                self.sem_label_pool = self._pool_compact("sem", self.sem_label_pool, keep)
-            if color_label is not None:
-                self.color_pool = self._pool_compact("color", self.color_pool, keep)
-            cur_sample_filter_mask = filter_mask[-self.cur_sample_count:]
-            self.cur_sample_count = int(cur_sample_filter_mask.sum().item())
-            self.pool_sample_count = int(filter_mask.sum().item())
+                filter_mask = torch.zeros((n_pool,), dtype=torch.bool, device=pool.device)
+                filter_mask[keep] = True
+                filter_mask[keep[discarded_index]] = False
+                keep = torch.nonzero(filter_mask).squeeze(1)
+                cur_kept = int(filter_mask[-self.cur_sample_count:].sum().item())
+            # every pool compacted by the kept-row list in one launch (pin_gather_rows)
+            names = ["coord", "global_coord", "sdf_label", "weight", "time"] + (["packed"] if track else []) + \
+                (["sem"] if sem_label is not None else []) + (["color"] if color_label is not None else [])
+            attrs = {"coord": "coord_pool", "global_coord": "global_coord_pool", "sdf_label": "sdf_label_pool",
+                     "weight": "weight_pool", "time": "time_pool", "packed": "_pool_packed",
+                     "sem": "sem_label_pool", "color": "color_pool"}
+            outs = self._pool_compact_many([(nm_, getattr(self, attrs[nm_])) for nm_ in names], keep)
+            for nm_, out in zip(names, outs):
+                setattr(self, attrs[nm_], out)
+            # :256-259 -- the kept rows of this frame's samples (filter_mask[-cur:]: all rows when
+            # cur is 0) and of the whole pool
+            self.cur_sample_count = cur_kept
+            self.pool_sample_count = int(keep.shape[0])
         else:
             self.cur_sample_count = coord.shape[0]
             self.pool_sample_count = self.coord_pool.shape[0]
@@ -449,7 +465,31 @@ class Mapper:
         bufs[name] = (buf, n + m)
         return buf[:n + m]
 
+    def _pool_compact_many(self, pools, keep):
+        """_pool_compact of several pools by one kept-row list: the targets taken as
+        _pool_compact takes them, then every row copy in one pin_gather_rows launch.  pools:
+        [(name, tensor)]; returns the compacted views in that order."""
+        k = keep.shape[0]
+        keep = keep.contiguous()
+        outs, arrays = [], []
+        for name, cur in pools:
+            out = self._pool_compact_target(name, cur, k)
+            outs.append(out)
+            if k > 0 and cur.numel() > 0:
+                cur = cur.contiguous()
+                arrays.append(_lib.PinRowArray(cur.data_ptr(), out.data_ptr(),
+                                               cur.numel() // cur.shape[0] * cur.element_size()))
+        for i in range(0, len(arrays), _lib.ROW_ARRAYS_MAX):
+            chunk = arrays[i:i + _lib.ROW_ARRAYS_MAX]
+            arr = (_lib.PinRowArray * len(chunk))(*chunk)
+            _lib.call("pin_gather_rows", arr, len(chunk), _lib.ptr(keep), k, _lib.stream())
+        return outs
+
     def _pool_compact(self, name, cur, keep):
+        """One pool compacted by the kept-row list (_pool_compact_many of one pool)."""
+        return self._pool_compact_many([(name, cur)], keep)[0]
+
+    def _pool_compact_target(self, name, cur, k):
         """cur.index_select(0, keep) written into the pool's spare buffer (kept per pool and
         swapped with the live one), so the window filter allocates nothing in steady state; the
         result is the pool's new live prefix view, which _pool_append then extends in place.
@@ -458,7 +498,6 @@ class Mapper:
         spare itself is left alone (a fresh buffer is taken) and the kept tensor stays valid."""
         bufs = self.__dict__.setdefault("_pool_bufs", {})
         spares = self.__dict__.setdefault("_pool_spare", {})
-        k = keep.shape[0]
         spare = spares.pop(name, None)
         if (spare is None or _viewed_elsewhere(spare) or spare.dtype != cur.dtype
                 or spare.shape[1:] != cur.shape[1:] or spare.shape[0] < k or spare.device != cur.device):
@@ -466,7 +505,6 @@ class Mapper:
             rows = max(k, live.shape[0] if live is not None else 0)
             spare = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=cur.dtype, device=cur.device)
         out = spare[:k]
-        torch.index_select(cur, 0, keep, out=out)
         old = bufs.get(name, (None, -1))[0]
         if old is not None and old.data_ptr() != spare.data_ptr():
             spares[name] = old          # the previous live buffer becomes the spare

@@ -139,6 +139,56 @@ def street_scene(rng):
     return np.asarray(boxes), np.asarray(cyls), g
 
 
+def long_street_scene(rng, length=200.0):
+    """street_scene along a longer street (buildings from x = -40 to `length`, cars and poles
+    spread over it, the wall at length + 5) for sequences of ~100 frames (long_slam_poses)."""
+    g = -SLAM_SENSOR_H
+    boxes = []
+    x = -40.0
+    while x < length:
+        w = rng.uniform(6.0, 14.0)
+        for side in (-1.0, 1.0):
+            y0 = side * rng.uniform(9.0, 12.0)
+            d = rng.uniform(6.0, 12.0)
+            ylo, yhi = (y0, y0 + d) if side > 0 else (y0 - d, y0)
+            boxes.append((x, x + w, ylo, yhi, g, g + rng.uniform(5.0, 16.0)))
+        x += w + rng.uniform(2.0, 6.0)
+    n_cars = int(length / 9)
+    for _ in range(n_cars):
+        cx = rng.uniform(-30.0, length - 10.0)
+        cy = rng.choice([-1.0, 1.0]) * rng.uniform(4.5, 6.5)
+        boxes.append((cx, cx + 4.2, cy - 0.9, cy + 0.9, g, g + 1.5))
+    boxes.append((length + 5.0, length + 6.0, -30.0, 30.0, g, g + 4.0))
+    cyls = [(rng.uniform(-30.0, length - 10.0), rng.choice([-1.0, 1.0]) * rng.uniform(3.2, 7.5),
+             rng.uniform(0.15, 0.45), g, g + rng.uniform(3.0, 8.0)) for _ in range(int(length / 4))]
+    return np.asarray(boxes), np.asarray(cyls), g
+
+
+def long_slam_poses(frames, speed=1.2, ramp=10):
+    """Sensor poses for long sequences: the speed ramps up over `ramp` frames to `speed` m/frame
+    (KITTI-like at 10 Hz) and stays there, with a +-2.5 deg yaw and 0.15 m sway oscillation."""
+    out = []
+    x = 0.0
+    for k in range(frames):
+        if k > 0:
+            x += speed * min(1.0, (k + 1) / ramp)
+        yaw = np.deg2rad(2.5 * np.sin(0.11 * k) + 0.15 * np.sin(0.9 * k))
+        T = np.eye(4)
+        T[:3, :3] = [[np.cos(yaw), -np.sin(yaw), 0.0], [np.sin(yaw), np.cos(yaw), 0.0], [0.0, 0.0, 1.0]]
+        T[:3, 3] = [x, 0.15 * np.sin(0.23 * k) + 0.08 * np.sin(0.7 * k), 0.005 * k]
+        out.append(T)
+    return out
+
+
+def sequence_scene(kind, rng, frames):
+    """(scene, poses) of a SLAM sequence fixture: "street" (street_scene + slam_poses, the 30-frame
+    fixture) or "long" (long_street_scene + long_slam_poses, ~100 frames)."""
+    if kind == "long":
+        poses = long_slam_poses(frames)
+        return long_street_scene(rng, length=float(poses[-1][0, 3]) + 60.0), poses
+    return street_scene(rng), slam_poses(frames)
+
+
 def lidar_scan(pose, scene, rng, beams=64, cols=1024, noise=0.01):
     """A 64-beam spinning lidar at `pose` (4x4, f64) ray-cast against the scene; returns the hits in
     the sensor frame, ranges in [3, 59.5] m (so the reference's crop_frame is a no-op), quantised

@@ -783,7 +783,7 @@ def gen_process_frame_case(name="process_frame", seed=15, frames=4):
 # ------------------------------------------------------------------ sequence fixtures (configs[0])
 sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
 from tests.replay import ReplayDraws, mapping_pool  # noqa: E402
-from pin_slam_amd.synthetic import Q_SCALE, lidar_scan, slam_poses, street_scene  # noqa: E402
+from pin_slam_amd.synthetic import Q_SCALE, lidar_scan, sequence_scene  # noqa: E402
 
 
 class _ReplayTorch:
@@ -841,12 +841,13 @@ def config_scalars(c):
     return out
 
 
-def gen_slam_sequence(name="slam_seq", frames=30, seed=21, replay_seed=2024):
+def gen_slam_sequence(name="slam_seq", frames=30, seed=21, replay_seed=2024, scene="street"):
     """The sequence with 8 torch threads, saved; then again with 1 thread, whose differences (only
-    the reduction order changes) are kept as the reference's own spread (keys spread_*)."""
+    the reduction order changes) are kept as the reference's own spread (keys spread_*).
+    scene: "street" (30 frames, the round-4 fixture) or "long" (synthetic.sequence_scene)."""
     import math
-    rec = _slam_sequence_run(name, frames, seed, replay_seed, 8)
-    t1 = _slam_sequence_run(name + "[1 thread]", frames, seed, replay_seed, 1)
+    rec = _slam_sequence_run(name, frames, seed, replay_seed, 8, scene)
+    t1 = _slam_sequence_run(name + "[1 thread]", frames, seed, replay_seed, 1, scene)
     dts, drs = [], []
     for A, B in zip(rec["hist_pose"], t1["hist_pose"]):
         dts.append(float(np.linalg.norm(A[:3, 3] - B[:3, 3])))
@@ -867,7 +868,7 @@ def gen_slam_sequence(name="slam_seq", frames=30, seed=21, replay_seed=2024):
           "mean |sdf| 8t", float(np.abs(rec["end_surface_sdf"]).mean()), "1t", float(rec["t1_mean_abs_end_surface_sdf"]))
 
 
-def _slam_sequence_run(name, frames, seed, replay_seed, threads):
+def _slam_sequence_run(name, frames, seed, replay_seed, threads, scene_kind="street"):
     """BASELINE configs[0] (the plumbing run): the reference's pin_slam.py frame loop
     (pin_slam.py:96-257 -- read/preprocess, tracking, travel distance, process_frame, freeze,
     mapping(iters)) on a synthetic 64-beam street sequence, with every random draw of the mapper
@@ -880,8 +881,7 @@ def _slam_sequence_run(name, frames, seed, replay_seed, threads):
     import utils.data_sampler as rds
     torch.set_num_threads(threads)
     rng = np.random.default_rng(seed)
-    scene = street_scene(rng)
-    poses = slam_poses(frames)
+    scene, poses = sequence_scene(scene_kind, rng, frames)
     scans = [lidar_scan(T, scene, rng) for T in poses]
     # surface probes: scan points put in the world by the TRUE poses (2,000 per frame), and 5,000
     # points of frame 0 (its sensor frame is the world frame)
@@ -985,6 +985,7 @@ def _slam_sequence_run(name, frames, seed, replay_seed, threads):
     import hashlib
     rec["scan_sha256"] = np.asarray([hashlib.sha256(np.ascontiguousarray(s_).tobytes()).hexdigest() for s_ in scans])
     rec["scan_seed"] = np.int64(seed)
+    rec["scene"] = np.asarray(scene_kind)
     rec["truth_poses"] = np.stack(poses)
     rec.update(surface_probes=surf, f0_surface_probes=surf0)
     rec["config_json"] = np.asarray(json.dumps(config_scalars(cfg)))
@@ -1126,6 +1127,7 @@ def main(only=None):
                                                       dist_weight_on=False, surface_sample_range_m=0.3)),
                  "process_frame": lambda: gen_process_frame_case(),
                  "slam_seq": lambda: gen_slam_sequence(),
+                 "slam_seq100": lambda: gen_slam_sequence("slam_seq100", frames=100, scene="long"),
                  "mapping_calls": lambda: gen_mapping_calls()}
         for name in only:
             cases[name]()

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 STRUCTS = ["PinHash", "PinPoints", "PinGridDims", "PinGrid", "PinMlp", "PinRegParams", "PinTrainCfg",
-           "PinTrainState", "PinAdamStep", "PinMapArrays", "PinSampleCfg", "PinRegIter"]
+           "PinTrainState", "PinAdamStep", "PinMapArrays", "PinSampleCfg", "PinRegIter", "PinRowArray"]
 
 
 def test_struct_layouts_match_header(tmp_path):

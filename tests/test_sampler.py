@@ -187,27 +187,83 @@ def test_pool_append_prefix_view_copies():
     assert d.dtype == torch.float64
 
 
-def test_pool_compact_ping_pong_keeps_held_views():
-    """The window filter's compaction (_pool_compact) writes into the pool's spare buffer and
-    swaps; appends then continue in place; a pool tensor the caller still holds is never
-    overwritten (its buffer is not reused as a spare while viewed)."""
+@pytest.mark.gpu
+def test_pool_compact_ping_pong_keeps_held_views(dev):
+    """The window filter's compaction (_pool_compact: pin_gather_rows) writes into the pool's
+    spare buffer and swaps; appends then continue in place; a pool tensor the caller still holds
+    is never overwritten (its buffer is not reused as a spare while viewed)."""
     import torch
     from pin_slam_amd.mapper import Mapper
     m = Mapper.__new__(Mapper)
-    ref = torch.empty((0, 2))
-    pool = m._pool_append("p", torch.empty((0, 2)), torch.arange(40.).view(20, 2))
-    ref = torch.cat((ref, torch.arange(40.).view(20, 2)))
+    ref = torch.empty((0, 2), device=dev)
+    pool = m._pool_append("p", torch.empty((0, 2), device=dev), torch.arange(40., device=dev).view(20, 2))
+    ref = torch.cat((ref, torch.arange(40., device=dev).view(20, 2)))
     held = None
     for it in range(6):
-        keep = torch.arange(0, pool.shape[0], 2 if it % 2 else 3)
+        keep = torch.arange(0, pool.shape[0], 2 if it % 2 else 3, device=dev)
         if it == 2:
             held, held_copy = pool, pool.clone()
         pool = m._pool_compact("p", pool, keep)
         ref = ref.index_select(0, keep)
         assert torch.equal(pool, ref)
-        new = torch.full((7, 2), float(it))
+        new = torch.full((7, 2), float(it), device=dev)
         before = pool.data_ptr()
         pool = m._pool_append("p", pool, new)
         ref = torch.cat((ref, new))
         assert torch.equal(pool, ref) and pool.data_ptr() == before     # appended in place
     assert torch.equal(held, held_copy)
+
+
+@pytest.mark.gpu
+def test_gather_rows_many_pools(dev):
+    """pin_gather_rows (the window filter's one-launch compaction) against index_select for pools
+    of every row width the mapper keeps (12-B coords, 4-B labels / weights, 8-B ts, 32-B packed
+    records) plus an odd 6-B row, and a keep list with gaps, repeats at the ends and one row."""
+    import torch
+    from pin_slam_amd.mapper import Mapper
+    g = torch.Generator(device="cpu").manual_seed(3)
+    n = 100_003
+    pools = [("coord", torch.randn(n, 3, generator=g)), ("label", torch.randn(n, generator=g)),
+             ("time", torch.randint(0, 1 << 40, (n,), generator=g)), ("packed", torch.randn(n, 8, generator=g)),
+             ("odd", torch.randint(0, 255, (n, 6), generator=g).to(torch.uint8))]
+    pools = [(a, t.to(dev)) for a, t in pools]
+    for keep in (torch.nonzero(torch.rand(n, generator=g) < 0.37).squeeze(1), torch.tensor([n - 1]),
+                 torch.arange(n), torch.zeros(0, dtype=torch.long)):
+        keep = keep.to(dev)
+        m = Mapper.__new__(Mapper)
+        outs = m._pool_compact_many(pools, keep)
+        for (name, t), o in zip(pools, outs):
+            assert torch.equal(o, t.index_select(0, keep)), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f64", [True, False])
+def test_pool_window_filter_dtypes(dev, f64):
+    """pin_pool_window against the reference's own expression on the CPU
+    (torch.sum((pool - origin) ** 2, dim=-1) < window_radius ** 2, utils/mapper.py:229-233) with an
+    f64 pose (torch promotes: f64 arithmetic) and an f32 one, on samples placed within a few ulps
+    of the sphere so that the two precisions disagree; kept rows, total and tail counts exact."""
+    import torch
+    from pin_slam_amd import _lib
+    from pin_slam_amd.neural_points import map_workspace
+    g = torch.Generator(device="cpu").manual_seed(11)
+    R = 40.0
+    n = 200_000
+    d = torch.randn(n, 3, generator=g, dtype=torch.float64)
+    d = d / d.norm(dim=1, keepdim=True) * (R * (1.0 + (torch.rand(n, 1, generator=g, dtype=torch.float64) - 0.5) * 4e-7))
+    origin = torch.tensor([3.123456789, -0.5, 0.1], dtype=torch.float64 if f64 else torch.float32)
+    pool = (d + origin.double()).float()
+    want_mask = torch.sum((pool - origin) ** 2, dim=-1) < R ** 2
+    want = torch.nonzero(want_mask).squeeze(1)
+    assert 0 < want.numel() < n
+    tail = 77_777
+    keep = torch.empty(n, dtype=torch.int64, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)
+    _lib.call("pin_pool_window", _lib.ptr(pool.to(dev)), n, _lib.ptr(origin.to(dev)), int(f64), R ** 2, n - tail,
+              _lib.ptr(keep), _lib.ptr(counts), _lib.ptr(map_workspace(n, dev)), _lib.stream())
+    total, in_tail = counts.cpu().tolist()
+    assert total == want.numel() and in_tail == int(want_mask[-tail:].sum())
+    assert torch.equal(keep[:total].cpu(), want)
+    # the other precision decides some of these samples differently (the test is not vacuous)
+    other = torch.sum((pool - (origin.float() if f64 else origin.double())) ** 2, dim=-1) < R ** 2
+    assert bool((other != want_mask).any())
