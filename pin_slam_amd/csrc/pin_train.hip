@@ -14,6 +14,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
 
 #include "pin_device.h"
 
@@ -1010,6 +1012,122 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 }
 
 
+#ifndef PIN_SCAT_SORT
+#define PIN_SCAT_SORT 1
+#endif
+
+// The same scatter with the block's (row, neighbour) pairs pre-summed per feature row: the pairs
+// are radix-sorted by id in LDS (rocprim block sort, ceil(log2 rows) bits, stable), each run of
+// equal ids becomes one 32-B row of float atomics (8 lanes x 32 contiguous bytes per run, the
+// shape above) -- the memory-side atomics fall by the block's references per row (~2-3 on
+// tile-sorted rows), at the cost of the sort.  Runs are summed in sorted (= input) order.
+// side: the training side effects ride on the same runs (train_side_effects' semantics): per run
+// one certainty add of its weights' sum (fixed-point: the sum of the pairs' fixed-point values)
+// and one ts max over its batch rows' ts.  row: the calling thread's row (its ts).
+__device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
+                                                       int nrow_blk, const float* gst,
+                                                       float* __restrict__ grad_features,
+                                                       unsigned long long* __restrict__ fdst, double fscale,
+                                                       int* buf, int64_t frows, bool side, int64_t row) {
+    constexpr int kP = kTBlock * kK;
+    using Sort = rocprim::block_radix_sort<unsigned, kTBlock, kK, unsigned short>;
+    using Scan = rocprim::block_scan<int, kTBlock>;
+    __shared__ union {
+        typename Sort::storage_type sort;
+        typename Scan::storage_type scan;
+    } s_tmp;
+    __shared__ unsigned short s_val[kP];        // sorted position -> pair index
+    __shared__ int s_run_id[kP];
+    __shared__ unsigned short s_run_start[kP];
+    __shared__ unsigned s_last[kTBlock];
+    __shared__ int64_t s_rts[kTBlock];           // the block's rows' ts (side effects)
+    __shared__ int s_end;                        // sorted position of the first invalid pair
+    int* const s_ids = buf;
+    float* const s_wt = (float*)(buf + kTBlock * kK);
+    const int nn_k = c.nn_k;
+    const int npair = nrow_blk * nn_k;
+    for (int e = threadIdx.x; e < npair; e += kTBlock) {
+        s_ids[e] = st.ids[row0 * nn_k + e];
+        s_wt[e] = st.weights[row0 * nn_k + e];
+    }
+    if (threadIdx.x == 0) s_end = kP;
+    int64_t* const ts_update = (side && st.row_ts) ? st.ts_update : nullptr;
+    if (side)
+        s_rts[threadIdx.x] = (ts_update && (int)threadIdx.x < nrow_blk && row < c.n_main) ? st.row_ts[row] : -1;
+    __syncthreads();
+    const unsigned bits = 32u - (unsigned)__clz((unsigned)frows);   // 2^bits > frows > any id
+    const unsigned inval = (1u << bits) - 1u;
+    unsigned keys[kK];
+    unsigned short vals[kK];
+#pragma unroll
+    for (int i = 0; i < kK; ++i) {
+        const int pidx = threadIdx.x * kK + i;
+        const int id = pidx < npair ? s_ids[pidx] : -1;
+        keys[i] = id < 0 ? inval : (unsigned)id;
+        vals[i] = (unsigned short)pidx;
+    }
+    Sort().sort(keys, vals, s_tmp.sort, 0, bits);
+    s_last[threadIdx.x] = keys[kK - 1];
+    __syncthreads();   // the sort's storage is free, s_last written
+    unsigned prev = threadIdx.x == 0 ? ~0u : s_last[threadIdx.x - 1];
+    int nrun = 0;
+#pragma unroll
+    for (int i = 0; i < kK; ++i) {
+        const unsigned pk = i == 0 ? prev : keys[i - 1];
+        nrun += (keys[i] != inval && keys[i] != pk) ? 1 : 0;
+        if (keys[i] == inval && pk != inval) s_end = threadIdx.x * kK + i;   // one thread: the transition
+    }
+    int off, total;
+    Scan().exclusive_scan(nrun, off, 0, total, s_tmp.scan);
+#pragma unroll
+    for (int i = 0; i < kK; ++i) {
+        const int pos = threadIdx.x * kK + i;
+        s_val[pos] = vals[i];
+        const unsigned pk = i == 0 ? prev : keys[i - 1];
+        if (keys[i] != inval && keys[i] != pk) {
+            s_run_id[off] = (int)keys[i];
+            s_run_start[off] = (unsigned short)pos;
+            ++off;
+        }
+    }
+    __syncthreads();
+    const int end = s_end;
+    for (int e = threadIdx.x; e < total * kF; e += kTBlock) {
+        const int run = e >> 3, d = e & (kF - 1);
+        const int a = s_run_start[run], b = run + 1 < total ? s_run_start[run + 1] : end;
+        float g = 0.f;
+        for (int q = a; q < b; ++q) {
+            const int pidx = s_val[q];
+            g = fmaf(s_wt[pidx], gst[(pidx / nn_k) * kF + d], g);
+        }
+        const int id = s_run_id[run];
+        if (fdst) atomicAdd(fdst + (int64_t)id * kF + d, to_fixed(g, fscale));
+        else atomicAdd(grad_features + (int64_t)id * kF + d, g);
+    }
+    if (!side) return;
+    float* const cert = st.cert_fixed ? nullptr : st.certainties;
+    unsigned long long* const cfix = (unsigned long long*)st.cert_fixed;
+    const double cscale = fixed_scale(st.cert_shift);
+    for (int run = threadIdx.x; run < total; run += kTBlock) {
+        const int a = s_run_start[run], b = run + 1 < total ? s_run_start[run + 1] : end;
+        float wsum = 0.f;
+        unsigned long long fsum = 0ull;
+        int64_t tmax = -1;
+        for (int q = a; q < b; ++q) {
+            const int pidx = s_val[q];
+            const float w = s_wt[pidx];
+            wsum += w;
+            if (cfix) fsum += to_fixed(w, cscale);
+            const int64_t t = s_rts[pidx / nn_k];
+            tmax = t > tmax ? t : tmax;
+        }
+        const int id = s_run_id[run];
+        if (cert) atomicAdd(cert + id, wsum);
+        if (cfix) atomicAdd(cfix + id, fsum);
+        if (ts_update && tmax >= 0) ts_amax(ts_update, id, tmax);
+    }
+}
+
 // MF, frozen decoder (no MLP_GRAD), mlp->packed:
 //   weighted_first (PIN_TRAIN_DX): x holds s dsdf/dx[0:8] per slot from the forward; the feature
 //     terms are dL/dsdf times it, no decoder evaluation here;
@@ -1261,17 +1379,29 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
 #if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 2   // profiling variant: no feature scatter, no side effects
     return;
 #endif
+    const bool side = st.certainties || st.cert_fixed || (st.ts_update && st.row_ts);
+    bool side_done = false;
     if constexpr (WF) {
         if (grad_features) {
-            feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, fdst, fscale, s_pair, p.rows);
+            if (PIN_SCAT_SORT && !EIK) {
+#if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1
+                constexpr bool kSide = false;
+#else
+                constexpr bool kSide = true;
+#endif
+                feature_scatter_sorted(c, st, row0, nrow_blk, gst, gdst, fdst, fscale, s_pair, p.rows, side && kSide,
+                                       row);
+                side_done = true;
+            } else {
+                feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, fdst, fscale, s_pair, p.rows);
+            }
             __syncthreads();   // the staging is read: the table takes the buffer
         }
     }
 #if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1   // profiling variant: no side effects
     return;
 #endif
-    if (st.certainties || st.cert_fixed || (st.ts_update && st.row_ts))
-        train_side_effects(c, st, row0, nrow_blk, row, s_pair);
+    if (side && !side_done) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
 }
 
 // out[i] += float(sum of the nrep fixed-point accumulators at i * 2^-shift); the accumulators are

@@ -254,5 +254,15 @@ def test_slam_sequence_matches_reference(golden, dev, fixture):
             nm.recreate_hash(None, None, False, False)
     else:
         nm.recreate_hash(None, None, False, False)
+        merged = nm.count()
         nm.prune_map(cfg.max_prune_certainty)
-        assert _within(nm.count(), int(z["merged_map_count"]), 0.01)
+        pruned = merged - nm.count()
+        assert pruned == 0 or pruned > 100           # prune_map removes points only above 100 candidates
+        # the map-count bound of the last frame (max(1 %, 3 x the running count spread))
+        rel = max(0.01, 3 * float(np.max(z["spread_rel_map_count"])))
+        if int(z["merged_map_count"]) == int(z["end_map_count"]) and pruned > 0:
+            # the reference pruned nothing (<= 100 candidates: its own cut-off), this run > 100: the
+            # counts before the prune are the comparable ones
+            assert _within(merged, int(z["merged_map_count"]), rel)
+        else:
+            assert _within(nm.count(), int(z["merged_map_count"]), rel)
