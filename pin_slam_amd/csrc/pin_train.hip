@@ -1013,7 +1013,7 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 
 
 #ifndef PIN_SCAT_SORT
-#define PIN_SCAT_SORT 1
+#define PIN_SCAT_SORT 1   // 0: the unsorted scatter for every batch (A/B builds)
 #endif
 
 // The same scatter with the block's (row, neighbour) pairs pre-summed per feature row: the pairs
@@ -1138,7 +1138,7 @@ __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, con
 // MASK (per-neighbour, PIN_TRAIN_DX): each neighbour's ReLU masks saved by the forward's f32 decode;
 //   its input gradient is GEMM2 of the matrix-core decoder alone (mlp_grad8_from_mask) -- no
 //   feature re-gather, no hidden layer.
-template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false, bool MASK = false>
+template <bool WF, bool MLP_GRAD, bool MF = false, bool EIK = false, bool MASK = false, bool SORT = false>
 __global__ void __launch_bounds__(kTBlock)
 k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
                  PinTrainState st, float* __restrict__ grad_features, float* __restrict__ mlp_part,
@@ -1383,7 +1383,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     bool side_done = false;
     if constexpr (WF) {
         if (grad_features) {
-            if (PIN_SCAT_SORT && !EIK) {
+            if constexpr (SORT && !EIK) {
 #if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1
                 constexpr bool kSide = false;
 #else
@@ -2122,9 +2122,19 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
     double* lpart = loss_out ? (double*)workspace : nullptr;
     float* mpart = mlp_grad ? (float*)((char*)workspace + nblk * kWaves * sizeof(double)) : nullptr;
     const int extra = (cfg->flags & PIN_TRAIN_EIK) ? 1 : 0;
-#define PIN_LAUNCH_BWD(WF, MG)                                                                               \
-    hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
-                       grad_features, mpart, lpart)
+    // the sorted-run scatter (feature_scatter_sorted) for large batches, which scatter straight
+    // into the gradient; small ones (gradient replicas) keep the direct scatter: at 26K rows the
+    // sort costs more than the replicas leave to save (backward 36 vs 28 us per SLAM-frame iteration)
+    const bool sorted = PIN_SCAT_SORT && !(st->replicas > 1);
+#define PIN_LAUNCH_BWD(WF, MG)                                                                                  \
+    do {                                                                                                        \
+        if (WF && sorted)                                                                                       \
+            hipLaunchKernelGGL((k_train_backward<WF, MG, false, false, false, true>), g, dim3(kTBlock), 0, s,  \
+                               *pts, *mlp, label, *cfg, *st, grad_features, mpart, lpart);                     \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
+                               grad_features, mpart, lpart);                                                    \
+    } while (0)
 #define PIN_LAUNCH_BWD_EIK(WF, MG, MF)                                                                                 \
     hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                        grad_features, mpart, lpart)
@@ -2139,14 +2149,20 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         }
     } else if (cfg->flags & PIN_TRAIN_DX) {
         if (mlp_grad || !mlp->packed) return PIN_ERR_UNSUPPORTED;
-        if (cfg->weighted_first)
+        if (cfg->weighted_first && sorted)
+            hipLaunchKernelGGL((k_train_backward<true, false, true, false, false, true>), g, dim3(kTBlock), 0, s, *pts,
+                               *mlp, label, *cfg, *st, grad_features, mpart, lpart);
+        else if (cfg->weighted_first)
             hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
                                *st, grad_features, mpart, lpart);
         else
             hipLaunchKernelGGL((k_train_backward<false, false, true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp,
                                label, *cfg, *st, grad_features, mpart, lpart);
     } else if (cfg->weighted_first) {
-        if (mlp_grad && mlp->packed)   // a training decoder decoded on the matrix cores
+        if (mlp_grad && mlp->packed && sorted)   // a training decoder decoded on the matrix cores
+            hipLaunchKernelGGL((k_train_backward<true, true, true, false, false, true>), g, dim3(kTBlock), 0, s, *pts,
+                               *mlp, label, *cfg, *st, grad_features, mpart, lpart);
+        else if (mlp_grad && mlp->packed)
             hipLaunchKernelGGL((k_train_backward<true, true, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
                                *st, grad_features, mpart, lpart);
         else if (mlp_grad) PIN_LAUNCH_BWD(true, true);
