@@ -826,8 +826,9 @@ int pin_map_gather(const PinMapArrays* src, const int64_t* rows, int64_t n_rows,
  * center: 3 values on the device, double when center_f64 (then the arithmetic is f64, as torch
  * promotes an f32 pool minus an f64 pose), else float (f32 arithmetic, radius2 rounded to f32);
  * the sum in the reference's order.  One host read of counts sizes what follows.
- * workspace: pin_map_workspace_bytes(n).
+ * workspace: pin_pool_window_workspace_bytes(n).
  */
+int64_t pin_pool_window_workspace_bytes(int64_t n);
 int pin_pool_window(const float* coord, int64_t n, const void* center, int32_t center_f64, double radius2,
                     int64_t tail_start, int64_t* keep, int64_t* counts, void* workspace, void* stream);
 

@@ -211,6 +211,7 @@ _SIGS = {
     "pin_mlp_backward_workspace_bytes": [i64],
     "pin_mlp_backward": [_P(PinMlp), c_void_p, i64, c_void_p, c_void_p, i32, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p],
+    "pin_pool_window_workspace_bytes": [i64],
     "pin_pool_window": [c_void_p, i64, c_void_p, i32, ctypes.c_double, i64, c_void_p, c_void_p, c_void_p, c_void_p],
     "pin_gather_rows": [_P(PinRowArray), i32, c_void_p, i64, c_void_p],
     "pin_map_gather": [_P(PinMapArrays), c_void_p, i64, i32, _P(PinMapArrays), c_void_p],
@@ -219,7 +220,8 @@ _SIGS = {
 }
 # functions whose return value is not a status code
 _RESTYPES = {"pin_map_workspace_bytes": i64, "pin_mc_workspace_bytes": i64,
-             "pin_query_sort_stable_workspace_bytes": i64, "pin_mlp_backward_workspace_bytes": i64}
+             "pin_query_sort_stable_workspace_bytes": i64, "pin_mlp_backward_workspace_bytes": i64,
+             "pin_pool_window_workspace_bytes": i64}
 
 _lib = None
 

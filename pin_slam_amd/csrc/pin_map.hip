@@ -685,21 +685,19 @@ int pin_prune_rows(const PinMapArrays* map, const float* travel_dist, int64_t cu
     return status(hipSuccess);
 }
 
+int64_t pin_pool_window_workspace_bytes(int64_t n) {
+    n = std::max<int64_t>(n, 1);
+    return align_up(4 * n) + align_up(8 * (n + 1)) + align_up((int64_t)scan_temp_bytes(n + 1));
+}
+
 int pin_pool_window(const float* coord, int64_t n, const void* center, int32_t center_f64, double radius2,
                     int64_t tail_start, int64_t* keep, int64_t* counts, void* workspace, void* stream) {
     if (n < 0 || !center || !counts || !workspace || (n > 0 && (!coord || !keep))) return PIN_ERR_ARG;
     auto s = as_stream(stream);
     Carve c{(char*)workspace};
-    c.take<uint64_t>(n);
-    c.take<uint64_t>(n);
-    c.take<int64_t>(n);
-    c.take<int64_t>(n);
     int32_t* flags = c.take<int32_t>(n);
-    c.take<int32_t>(n);
-    c.take<int32_t>(n);
     int64_t* incl = c.take<int64_t>(n + 1);
-    c.take<VdsStats>(1);
-    const size_t temp_bytes = std::max(sort_temp_bytes(n), scan_temp_bytes(n + 1));
+    const size_t temp_bytes = scan_temp_bytes(n + 1);
     void* temp = c.take<char>((int64_t)temp_bytes);
     if (n > 0) {
         if (center_f64)

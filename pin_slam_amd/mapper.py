@@ -378,20 +378,19 @@ class Mapper:
             origin = frame_origin.detach()
             f64 = origin.dtype == torch.float64
             origin = origin.to(device=pool.device, dtype=torch.float64 if f64 else torch.float32).contiguous()
-            keep_all = torch.empty((max(n_pool, 1),), dtype=torch.int64, device=pool.device)
-            counts = torch.empty((2,), dtype=torch.int64, device=pool.device)
+            keep_all, counts, ws, mask_buf = self._window_buffers(n_pool, pool.device)
             tail_start = n_pool - self.cur_sample_count if self.cur_sample_count > 0 else 0   # [-0:] is all
-            from .neural_points import map_workspace
             _lib.call("pin_pool_window", _lib.ptr(pool.contiguous()), n_pool, _lib.ptr(origin), int(f64),
                       float(c.window_radius) ** 2, tail_start, _lib.ptr(keep_all), _lib.ptr(counts),
-                      _lib.ptr(map_workspace(n_pool, pool.device)), _lib.stream())
+                      _lib.ptr(ws), _lib.stream())
             pool_sample_count, cur_kept = (int(v) for v in counts.cpu().tolist())
             keep = keep_all[:pool_sample_count]
             if pool_sample_count > c.pool_capacity:
                 # the reference's random discards over the kept rows (:241-245), then the mask's rows
                 discard_count = pool_sample_count - int(c.pool_capacity)
                 discarded_index = self._randint(pool_sample_count, discard_count)
-                filter_mask = torch.zeros((n_pool,), dtype=torch.bool, device=pool.device)
+                filter_mask = mask_buf[:n_pool]
+                filter_mask.zero_()
                 filter_mask[keep] = True
                 filter_mask[keep[discarded_index]] = False
                 keep = torch.nonzero(filter_mask).squeeze(1)
@@ -428,6 +427,21 @@ class Mapper:
             self.train_less = bool(getattr(c, "adaptive_mode", False) and
                                    new_sample_count / max(self.cur_sample_count, 1) < c.new_sample_ratio_thre)
 
+    def _window_buffers(self, n, device):
+        """The window filter's kept-row list, counts and workspace for a pool of n rows: sized with
+        the pool buffers (_pool_append) so that the filter allocates nothing in steady state (a
+        first-time workspace allocation inside the filter frame took ~20 ms at 11M rows)."""
+        wb = self.__dict__.get("_window_bufs")
+        if wb is None or wb[0].shape[0] < n or wb[0].device != torch.device(device):
+            rows = max(int(n), 1)
+            wb = (torch.empty((rows,), dtype=torch.int64, device=device),
+                  torch.empty((2,), dtype=torch.int64, device=device),
+                  torch.empty((int(_lib.fn("pin_pool_window_workspace_bytes")(rows)),), dtype=torch.uint8,
+                              device=device),
+                  torch.empty((rows,), dtype=torch.bool, device=device))   # the capacity discards' mask
+            self._window_bufs = wb
+        return wb
+
     def _pool_rows_hint(self, m):
         """Rows a pool buffer is first sized for: the window filter keeps at most pool_capacity
         samples and up to pool_filter_freq frames of m samples arrive between two filters, so
@@ -461,6 +475,8 @@ class Mapper:
             sp = spares.get(name)
             if sp is None or sp.shape[0] < rows or sp.dtype != dt or sp.shape[1:] != nb.shape[1:]:
                 spares[name] = torch.empty_like(nb)
+            if name == "global_coord" and new.is_cuda:   # the window filter's buffers, sized alike
+                self._window_buffers(rows, new.device)
         buf[n:n + m] = new
         bufs[name] = (buf, n + m)
         return buf[:n + m]
@@ -529,9 +545,14 @@ class Mapper:
         """pin_pool_pack of [n] samples -> [n, 8] f32 records (out: written in place)."""
         n = label.shape[0]
         out = torch.empty((n, 8), dtype=torch.float32, device=label.device) if out is None else out
+        # converted copies held in locals until the launch is queued: a temporary freed inside the
+        # argument list could be handed by the caching allocator to the next conversion, whose
+        # queued write would land before the pack kernel reads it
         w = None if weight is None else weight.detach().to(torch.float32).contiguous()
-        _lib.call("pin_pool_pack", _lib.ptr(coord.contiguous()), _lib.ptr(label.contiguous()),
-                  _lib.ptr(None if ts is None else ts.to(torch.int64).contiguous()), _lib.ptr(w), n, _lib.ptr(out),
+        c = coord.contiguous()
+        lb = label.contiguous()
+        t64 = None if ts is None else ts.to(torch.int64).contiguous()
+        _lib.call("pin_pool_pack", _lib.ptr(c), _lib.ptr(lb), _lib.ptr(t64), _lib.ptr(w), n, _lib.ptr(out),
                   _lib.stream())
         return out
 

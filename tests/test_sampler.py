@@ -245,7 +245,6 @@ def test_pool_window_filter_dtypes(dev, f64):
     of the sphere so that the two precisions disagree; kept rows, total and tail counts exact."""
     import torch
     from pin_slam_amd import _lib
-    from pin_slam_amd.neural_points import map_workspace
     g = torch.Generator(device="cpu").manual_seed(11)
     R = 40.0
     n = 200_000
@@ -259,8 +258,10 @@ def test_pool_window_filter_dtypes(dev, f64):
     tail = 77_777
     keep = torch.empty(n, dtype=torch.int64, device=dev)
     counts = torch.empty(2, dtype=torch.int64, device=dev)
-    _lib.call("pin_pool_window", _lib.ptr(pool.to(dev)), n, _lib.ptr(origin.to(dev)), int(f64), R ** 2, n - tail,
-              _lib.ptr(keep), _lib.ptr(counts), _lib.ptr(map_workspace(n, dev)), _lib.stream())
+    pool_d, origin_d = pool.to(dev), origin.to(dev)   # held: the kernel reads them after this line
+    ws = torch.empty(int(_lib.fn("pin_pool_window_workspace_bytes")(n)), dtype=torch.uint8, device=dev)
+    _lib.call("pin_pool_window", _lib.ptr(pool_d), n, _lib.ptr(origin_d), int(f64), R ** 2, n - tail,
+              _lib.ptr(keep), _lib.ptr(counts), _lib.ptr(ws), _lib.stream())
     total, in_tail = counts.cpu().tolist()
     assert total == want.numel() and in_tail == int(want_mask[-tail:].sum())
     assert torch.equal(keep[:total].cpu(), want)
