@@ -1024,8 +1024,9 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 // side: the training side effects ride on the same runs (train_side_effects' semantics): per run
 // one certainty add of its weights' sum (fixed-point: the sum of the pairs' fixed-point values)
 // and one ts max over its batch rows' ts.  row: the calling thread's row (its ts).
+template <bool EIK = false>
 __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, const PinTrainState& st, int64_t row0,
-                                                       int nrow_blk, const float* gst,
+                                                       int nrow_blk, const float* gst, const float* s_dsdf,
                                                        float* __restrict__ grad_features,
                                                        unsigned long long* __restrict__ fdst, double fscale,
                                                        int* buf, int64_t frows, bool side, int64_t row) {
@@ -1044,11 +1045,13 @@ __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, con
     __shared__ int s_end;                        // sorted position of the first invalid pair
     int* const s_ids = buf;
     float* const s_wt = (float*)(buf + kTBlock * kK);
+    float* const s_al = (float*)(buf + 2 * kTBlock * kK);   // EIK: the pairs' eik_coef
     const int nn_k = c.nn_k;
     const int npair = nrow_blk * nn_k;
     for (int e = threadIdx.x; e < npair; e += kTBlock) {
         s_ids[e] = st.ids[row0 * nn_k + e];
         s_wt[e] = st.weights[row0 * nn_k + e];
+        if (EIK) s_al[e] = st.eik_coef[row0 * nn_k + e];
     }
     if (threadIdx.x == 0) s_end = kP;
     int64_t* const ts_update = (side && st.row_ts) ? st.ts_update : nullptr;
@@ -1098,7 +1101,9 @@ __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, con
         float g = 0.f;
         for (int q = a; q < b; ++q) {
             const int pidx = s_val[q];
-            g = fmaf(s_wt[pidx], gst[(pidx / nn_k) * kF + d], g);
+            const int lr = pidx / nn_k;
+            if (EIK) g = fmaf(fmaf(s_wt[pidx], s_dsdf[lr], s_al[pidx]), gst[lr * kF + d], g);
+            else g = fmaf(s_wt[pidx], gst[lr * kF + d], g);
         }
         const int id = s_run_id[run];
         if (fdst) atomicAdd(fdst + (int64_t)id * kF + d, to_fixed(g, fscale));
@@ -1383,14 +1388,14 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
     bool side_done = false;
     if constexpr (WF) {
         if (grad_features) {
-            if constexpr (SORT && !EIK) {
+            if constexpr (SORT) {
 #if defined(PIN_PROF_BWD) && PIN_PROF_BWD >= 1
                 constexpr bool kSide = false;
 #else
                 constexpr bool kSide = true;
 #endif
-                feature_scatter_sorted(c, st, row0, nrow_blk, gst, gdst, fdst, fscale, s_pair, p.rows, side && kSide,
-                                       row);
+                feature_scatter_sorted<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, fdst, fscale, s_pair, p.rows,
+                                            side && kSide, row);
                 side_done = true;
             } else {
                 feature_scatter<EIK>(c, st, row0, nrow_blk, gst, s_dsdf, gdst, fdst, fscale, s_pair, p.rows);
@@ -2135,9 +2140,15 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
             hipLaunchKernelGGL((k_train_backward<WF, MG>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
                                grad_features, mpart, lpart);                                                    \
     } while (0)
-#define PIN_LAUNCH_BWD_EIK(WF, MG, MF)                                                                                 \
-    hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st, \
-                       grad_features, mpart, lpart)
+#define PIN_LAUNCH_BWD_EIK(WF, MG, MF)                                                                          \
+    do {                                                                                                        \
+        if (WF && sorted)                                                                                       \
+            hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true, false, true>), g, dim3(kTBlock), 0, s, *pts, \
+                               *mlp, label, *cfg, *st, grad_features, mpart, lpart);                           \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_train_backward<WF, MG, MF, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, \
+                               *cfg, *st, grad_features, mpart, lpart);                                        \
+    } while (0)
     if (cfg->flags & PIN_TRAIN_EIK) {
         if ((cfg->flags & PIN_TRAIN_DX) || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec) return PIN_ERR_ARG;
         if (cfg->weighted_first) {
