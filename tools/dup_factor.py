@@ -11,7 +11,8 @@ import pin_slam_amd as P  # noqa: E402
 from pin_slam_amd.synthetic import surface_map, surface_pool  # noqa: E402
 
 dev = "cuda"
-nm, dec, pts = surface_map(bench.MAPPER_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=True,
+WF = os.environ.get("WF", "1") != "0"
+nm, dec, pts = surface_map(bench.MAPPER_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=WF,
                            query_backend="grid", bs=bench.MAPPER_BS)
 for p in dec.parameters():
     p.requires_grad_(False)

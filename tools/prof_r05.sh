@@ -4,7 +4,7 @@
 # the drop-in double backward).  Every GPU step has its own time limit; a fault ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r05; mkdir -p $OUT; export TMPDIR=/tmp
-S=${STEPS:-smoke,tests,bench,prof,nwf_pmc,dbwd}
+S=${STEPS:-smoke,tests,bench,prof,nwf_pmc,wf_pmc,dbwd}
 run() {   # name seconds command...
     local name=$1 secs=$2; shift 2
     timeout -k 10 "$secs" "$@" > $OUT/$name.log 2>&1
@@ -28,6 +28,14 @@ if [[ $S == *nwf_pmc* ]]; then
             --no-process-frame --no-slam --no-input-order --mapper-steps 3 --mapper-warmup 1
     done
     python3 tools/traffic.py $OUT/nwf_pmc > $OUT/mapper_nwf_traffic.json 2>&1
+fi
+if [[ $S == *wf_pmc* ]]; then   # HBM traffic of the weighted-first mapper kernels (sorted-run scatter)
+    for c in FETCH_SIZE WRITE_SIZE; do
+        run wf_$c 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/wf_pmc/$c -o run -- \
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-tracker --no-mesher --no-map-update \
+            --no-process-frame --no-slam --no-input-order --no-mapper-nwf --no-nwf-leg --mapper-steps 3 --mapper-warmup 1
+    done
+    python3 tools/traffic.py $OUT/wf_pmc > $OUT/mapper_wf_traffic.json 2>&1
 fi
 if [[ $S == *dbwd* ]]; then
     run dbwd 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dbwd -o run -- \
