@@ -954,14 +954,37 @@ k_query_feature_fwd_grid(const PinGrid g, const PinPoints p, const float* __rest
     query_feature_body<WF, PGO>(src, p, q, i, nn_k, feat, weights, nn_counts, cert_out, ids, gids);
 }
 
+// One 8-float row per lane added into dst[id * 8 ..] (id < 0: nothing), staged through the wave's
+// LDS slice s (64 x 8 floats + 64 ids) and issued as 8 lanes x 32 contiguous bytes per atomic
+// instruction -- the cheapest float-atomic shape measured (the training scatter's); one lane per
+// row with 8 separate 4-B atomics hits 64 lines per instruction.  Every lane of the wave calls this.
+__device__ __forceinline__ void wave_rows_atomic(float* s, int id, const float (&g)[kF], float* __restrict__ dst) {
+    const int lane = threadIdx.x & 63;
+    int* sid = (int*)(s + 64 * kF);
+    wave_lds_sync();   // the previous call's readers are done
+#pragma unroll
+    for (int d = 0; d < kF; ++d) s[lane * kF + d] = g[d];
+    sid[lane] = id;
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < kF; ++u) {
+        const int e = u * 64 + lane;
+        const int rid = sid[e >> 3];
+        if (rid >= 0) atomicAdd(dst + (int64_t)rid * kF + (e & (kF - 1)), s[e]);
+    }
+}
+
 template <bool WF, bool PGO>
 __global__ void __launch_bounds__(kBlock)
 k_query_feature_bwd(const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k, const int* __restrict__ ids,
                     const int* __restrict__ gids, const float* __restrict__ weights,
                     const float* __restrict__ gfeat, const float* __restrict__ gw, float* __restrict__ gq_out,
                     float* __restrict__ gF) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    __shared__ float s_sc[kBlock / 64][64 * kF + 64];
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~(int64_t)63) >= n) return;   // whole waves past the end (the scatter is wave-wide)
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : 0;          // dead lanes compute row 0 and write nothing
     const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
     const float4* __restrict__ rec = (const float4*)p.records;
     float gx[kD];
@@ -981,7 +1004,7 @@ k_query_feature_bwd(const PinPoints p, const float* __restrict__ q, int64_t n, i
         dw[j] = 0.f;
         pg[j][0] = pg[j][1] = pg[j][2] = 0.f;
         if (j >= nn_k) continue;
-        const int g = gids[i * nn_k + j];
+        const int g = live ? gids[i * nn_k + j] : -1;
         if (g < 0) continue;
         id[j] = ids[i * nn_k + j];
         const float4 r = rec[g];
@@ -1032,18 +1055,28 @@ k_query_feature_bwd(const PinPoints p, const float* __restrict__ q, int64_t n, i
             for (int d = 0; d < 3; ++d) gvec[d] = G ? G[kF + d] : 0.f;
         }
         if (gw) dw[j] += gw[i * nn_k + j];
-        if (gF) {
-            float* dst = gF + (int64_t)id[j] * kF;
-#pragma unroll
-            for (int d = 0; d < kF; ++d) atomicAdd(dst + d, gfe[d]);
-        }
         float r0 = gvec[0], r1 = gvec[1], r2 = gvec[2];
         if (PGO) quat_rotate_active(qt, gvec[0], gvec[1], gvec[2], r0, r1, r2);
         gq[0] += r0;
         gq[1] += r1;
         gq[2] += r2;
     }
-    if (!gq_out) return;
+    if (gF) {   // the feature rows: w_j G[0:8] (weighted_first) or G_j[0:8], wave-staged
+        for (int j = 0; j < nn_k; ++j) {
+            float gfe[kF];
+            const bool ok = id[j] >= 0;
+            if (WF) {
+#pragma unroll
+                for (int d = 0; d < kF; ++d) gfe[d] = w[j] * gx[d];
+            } else {
+                const float* G = (gfeat && ok) ? gfeat + (i * nn_k + j) * kD : nullptr;
+#pragma unroll
+                for (int d = 0; d < kF; ++d) gfe[d] = G ? G[d] : 0.f;
+            }
+            wave_rows_atomic(s_sc[threadIdx.x >> 6], ok ? id[j] : -1, gfe, gF);
+        }
+    }
+    if (!gq_out || !live) return;
     if (S > 0.f) {
         float wbar = 0.f;
 #pragma unroll
@@ -1085,8 +1118,11 @@ k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, 
                      const float* __restrict__ gfeat, const float* __restrict__ gw, const float* __restrict__ hq,
                      const float* __restrict__ hf, float* __restrict__ dq_out, float* __restrict__ dg_out,
                      float* __restrict__ dgw_out, float* __restrict__ dF) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    __shared__ float s_sc[kBlock / 64][64 * kF + 64];
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~(int64_t)63) >= n) return;   // whole waves past the end (the scatter is wave-wide)
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : 0;          // dead lanes compute row 0 and write nothing
     const float qx = q[3 * i], qy = q[3 * i + 1], qz = q[3 * i + 2];
     const float4* __restrict__ rec = (const float4*)p.records;
     const float H3[3] = {hq ? hq[3 * i] : 0.f, hq ? hq[3 * i + 1] : 0.f, hq ? hq[3 * i + 2] : 0.f};
@@ -1103,7 +1139,7 @@ k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, 
 #pragma unroll
         for (int d = 0; d < 3; ++d) r[j][d] = ph[j][d] = b[j][d] = 0.f;
         if (j >= nn_k) continue;
-        const int g = gids[i * nn_k + j];
+        const int g = live ? gids[i * nn_k + j] : -1;
         if (g < 0) continue;
         id[j] = ids[i * nn_k + j];
         const float4 rc = rec[g];
@@ -1162,7 +1198,7 @@ k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, 
         }
         if (gw) a[j] += gw[i * nn_k + j];
     }
-    if (!WF && dg_out) {   // invalid / padded neighbour slots get zeros
+    if (!WF && dg_out && live) {   // invalid / padded neighbour slots get zeros
 #pragma unroll
         for (int j = 0; j < kK; ++j) {
             if (j >= nn_k || id[j] >= 0) continue;
@@ -1185,12 +1221,15 @@ k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, 
     }
     float dq[3] = {0.f, 0.f, 0.f};
     float dG[kD];
+    float ej[kK];   // e_j, for the wave-staged dL2/df_j = e_j G[0:8] after the loop
 #pragma unroll
     for (int d = 0; d < kD; ++d) dG[d] = 0.f;
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
+        ej[j] = 0.f;
         if (id[j] < 0) continue;
         const float e = h[j] - H * w[j];
+        ej[j] = e;
         if (dgw_out) dgw_out[i * nn_k + j] = e;
         const float c = -2.f * u[j] * u[j];
         const float rh = r[j][0] * H3[0] + r[j][1] * H3[1] + r[j][2] * H3[2];
@@ -1230,13 +1269,17 @@ k_query_feature_bwd2(const PinPoints p, const float* __restrict__ q, int64_t n, 
             }
 #pragma unroll
             for (int d = 0; d < 3; ++d) dG[kF + d] = fmaf(w[j], ph[j][d], fmaf(e, v[d], dG[kF + d]));
-            if (dF) {
-                float* dst = dF + ij * kF;
-#pragma unroll
-                for (int d = 0; d < kF; ++d) atomicAdd(dst + d, e * G[d]);
-            }
         }
     }
+    if (WF && dF) {
+        for (int j = 0; j < nn_k; ++j) {
+            float gfe[kF];
+#pragma unroll
+            for (int d = 0; d < kF; ++d) gfe[d] = ej[j] * G[d];
+            wave_rows_atomic(s_sc[threadIdx.x >> 6], id[j], gfe, dF);
+        }
+    }
+    if (!live) return;
     if (WF && dg_out) {
 #pragma unroll
         for (int d = 0; d < kD; ++d) dg_out[i * kD + d] = dG[d];

@@ -1539,7 +1539,7 @@ __global__ void __launch_bounds__(kTBlock) k_mlp_grad_final(const float* __restr
 // bilinear in (go, e): with u_c = W1[c] . e,
 //   d(gx . e)/d go = s sum_c w2_c m_c u_c,  d/dW1[c][i] = s w2_c sum_r m_c go e_i,
 //   d/dw2_c = s W1[c] . sum_r m_c go e     -- k_mlp_grad_final's T' terms with e' = go e.
-constexpr int kMlpRowBlocks = 1024;   // persistent grid of the row backward: bounded partials
+constexpr int kMlpRowBlocks = 512;    // persistent grid of the row backward: bounded partials (k_mlp_grad_final reads them all)
 
 __global__ void __launch_bounds__(kTBlock)
 k_mlp_forward(PinMlp m, const float* __restrict__ x, int64_t n, float* __restrict__ out) {
