@@ -454,10 +454,15 @@ class NeuralPoints(nn.Module):
         bricks, dims, n_occ = occ
         pts = self.neural_points.contiguous()
         n = max(n_occ, 1)
-        crec = torch.zeros((n, 4), dtype=torch.float32, device=pts.device)
-        cfeat = torch.zeros((n, 8), dtype=torch.float32, device=pts.device) if feats is not None else None
-        ccert = torch.zeros((n,), dtype=torch.float32, device=pts.device) if feats is not None else None
-        cgid = torch.full((n,), -1, dtype=torch.int32, device=pts.device)
+        # pin_grid_fill writes every one of the n_occ entries exactly once (each marked point its
+        # rank in the brick order; marked == occupied is what made the grid exact), so only an
+        # empty grid's placeholder entry needs values
+        alloc = (lambda shape, dt, v: torch.empty(shape, dtype=dt, device=pts.device)) if n_occ > 0 else \
+            (lambda shape, dt, v: torch.full(shape, v, dtype=dt, device=pts.device))   # noqa: E731
+        crec = alloc((n, 4), torch.float32, 0.0)
+        cfeat = alloc((n, 8), torch.float32, 0.0) if feats is not None else None
+        ccert = alloc((n,), torch.float32, 0.0) if feats is not None else None
+        cgid = alloc((n,), torch.int32, -1)
         f = feats.detach().contiguous() if feats is not None else None
         c = cert.detach().contiguous() if cert is not None else None
         _lib.call("pin_grid_fill", _lib.ptr(pts), pts.shape[0], float(np.float32(self.resolution)),
