@@ -833,6 +833,42 @@ __device__ __forceinline__ float mlp_sdf_packed(const MlpW& m, const float (&x)[
     return ((out2.x + out2.y) + m.w[kWB2]) * m.sdf_scale;
 }
 
+// Two decodes sharing the weight reads (SDF and ReLU masks only, no gradient): the per-neighbour
+// training forward decodes neighbours j and j + 1 of a row together -- one LDS broadcast read of a
+// hidden-unit pair feeds both rows' packed FMAs, and the two chains are independent.  Each result
+// is mlp_sdf_packed<false>'s, bitwise (the same operations in the same order per row).
+__device__ __forceinline__ void mlp_sdf_packed_x2(const MlpW& m, const float (&xa)[kD], const float (&xb)[kD],
+                                                  float& sa, float& sb, uint64_t& mka, uint64_t& mkb) {
+    f32x2 oa = {0.f, 0.f}, ob = {0.f, 0.f};
+    uint64_t ka = 0, kb = 0;
+#pragma unroll PIN_MLP_UNROLL
+    for (int c = 0; c < kH; c += 2) {
+        const f32x2* __restrict__ wp = (const f32x2*)(m.w + (c >> 1) * kWPair);
+        f32x2 wv[kD];
+#pragma unroll
+        for (int i = 0; i < kD; ++i) wv[i] = wp[i];
+        const f32x2 b = *(const f32x2*)(m.w + kWB1 + c);
+        const f32x2 v2 = *(const f32x2*)(m.w + kWW2 + c);
+        f32x2 acca = {0.f, 0.f}, accb = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < kD; ++i) {
+            acca = __builtin_elementwise_fma(wv[i], (f32x2){xa[i], xa[i]}, acca);
+            accb = __builtin_elementwise_fma(wv[i], (f32x2){xb[i], xb[i]}, accb);
+        }
+        const f32x2 pa = acca + b, pb = accb + b;
+        const f32x2 aa = {pa.x > 0.f ? v2.x : 0.f, pa.y > 0.f ? v2.y : 0.f};
+        const f32x2 ab = {pb.x > 0.f ? v2.x : 0.f, pb.y > 0.f ? v2.y : 0.f};
+        oa = __builtin_elementwise_fma(aa, pa, oa);
+        ob = __builtin_elementwise_fma(ab, pb, ob);
+        ka |= (uint64_t)((pa.x > 0.f ? 1u : 0u) | (pa.y > 0.f ? 2u : 0u)) << c;
+        kb |= (uint64_t)((pb.x > 0.f ? 1u : 0u) | (pb.y > 0.f ? 2u : 0u)) << c;
+    }
+    sa = ((oa.x + oa.y) + m.w[kWB2]) * m.sdf_scale;
+    sb = ((ob.x + ob.y) + m.w[kWB2]) * m.sdf_scale;
+    mka = ka;
+    mkb = kb;
+}
+
 // The same decoder one hidden unit at a time with plain FMAs (v_fma_f32 issues in 2 cycles per
 // wave64 on a SIMD-32, so packing buys no FLOP rate on gfx950): the W1 row comes from LDS as
 // three 16-B broadcast reads, and only x, the gradient accumulators and one row are live --

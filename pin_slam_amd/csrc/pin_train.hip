@@ -83,6 +83,9 @@ constexpr bool kTrainNwfMf = PIN_TRAIN_NWF_MF != 0;
 #define PIN_TRAIN_NWF_NT 1   // its decoder with the query tile as the outer GEMM loop (fewer live VGPRs)
 #endif
 
+#ifndef PIN_NWF_X2
+#define PIN_NWF_X2 1      // per-neighbour frozen-decoder forward: two neighbours per decoder pass
+#endif
 #ifndef PIN_TRAIN_IDP
 #define PIN_TRAIN_IDP 1   // training forward: top-k payload = feature-row id (GridSource IDP)
 #endif
@@ -127,6 +130,57 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
 #pragma unroll
     for (int d = 0; d < kD; ++d) x[d] = 0.f;
     float sdf = 0.f;
+#if PIN_NWF_X2
+    if constexpr (!WF && DX && !MF && !PAIR && Src::kIdPayload) {
+        // per-neighbour, frozen decoder, f32 decode: neighbours j and j + 1 decoded together
+        // (mlp_sdf_packed_x2: one weight read feeds both), summed in neighbour order as below
+        auto inputs = [&](int j, bool& valid, float (&xj)[kD], float& w) {
+            valid = u[j] > 0.f;
+            const int id = valid ? tk.g[j] : -1;
+            const int64_t ii = id > 0 ? id : 0;
+            float4 f0, f1;
+            src.features(0, ii, f0, f1);
+            float v0, v1, v2;
+            if (p.positions4) {
+                const float4 pp = ((const float4*)p.positions4)[ii];
+                v0 = qx - pp.x;
+                v1 = qy - pp.y;
+                v2 = qz - pp.z;
+            } else {
+                v0 = qx - p.positions[3 * ii];
+                v1 = qy - p.positions[3 * ii + 1];
+                v2 = qz - p.positions[3 * ii + 2];
+            }
+            if (p.after_pgo && valid) quat_rotate_passive(((const float4*)p.orientations)[id], v0, v1, v2);
+            w = valid && nn > 0 ? u[j] / S : 0.f;
+            cid[j] = valid && live ? id : -1;
+            cw[j] = w;
+            const float xs[kD] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w, v0, v1, v2};
+#pragma unroll
+            for (int d = 0; d < kD; ++d) xj[d] = xs[d];
+        };
+#pragma unroll
+        for (int j = 0; j < kK; j += 2) {
+            bool va, vb;
+            float xa[kD], xb[kD], wa, wb;
+            inputs(j, va, xa, wa);
+            inputs(j + 1, vb, xb, wb);
+            float sa = 0.f, sb = 0.f;
+            uint64_t ka = 0, kb = 0;
+            if (va || vb) mlp_sdf_packed_x2(m, xa, xb, sa, sb, ka, kb);
+            const float ska = va ? sa : 0.f, skb = vb ? sb : 0.f;
+            if (!va) ka = 0;
+            if (!vb) kb = 0;
+            sdf = sdf + ska * wa;
+            sdf = sdf + skb * wb;
+            if (live && j < nn_k) ((uint2*)st.x)[t * nn_k + j] = make_uint2((uint32_t)ka, (uint32_t)(ka >> 32));
+            if (live && j + 1 < nn_k)
+                ((uint2*)st.x)[t * nn_k + j + 1] = make_uint2((uint32_t)kb, (uint32_t)(kb >> 32));
+        }
+        if (writer) st.sdf[r] = sdf;
+        return;
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         if (j == kK / 2) __builtin_amdgcn_sched_barrier(0);
