@@ -1112,8 +1112,9 @@ __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, con
     if (side)
         s_rts[threadIdx.x] = (ts_update && (int)threadIdx.x < nrow_blk && row < c.n_main) ? st.row_ts[row] : -1;
     __syncthreads();
-    const unsigned bits = 32u - (unsigned)__clz((unsigned)frows);   // 2^bits > frows > any id
-    const unsigned inval = (1u << bits) - 1u;
+    // 2^bits > frows > any id (ids are int32 row indices; 32 bits when frows needs them all)
+    const unsigned bits = frows >= (int64_t)0x80000000u ? 32u : 32u - (unsigned)__clz((unsigned)frows);
+    const unsigned inval = bits >= 32u ? ~0u : (1u << bits) - 1u;
     unsigned keys[kK];
     unsigned short vals[kK];
 #pragma unroll
