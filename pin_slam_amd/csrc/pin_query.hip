@@ -504,6 +504,7 @@ template <int PER, int MAXT>
 __global__ void __launch_bounds__(kPartThreads)
 k_tile_rank(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ tot, int2* __restrict__ tk) {
     constexpr int kTpt = MAXT / kPartThreads;   // tiles per thread in the atomic and scan phases
+    static_assert(4 * MAXT <= 160 * 1024 / 2, "k_tile_rank's LDS histogram: gfx950 has 160 KB per CU (two blocks)");
     __shared__ int h[MAXT];
     const int k = threadIdx.x;
 #pragma unroll
@@ -552,6 +553,8 @@ __global__ void __launch_bounds__(kPartThreads)
 k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict__ tot, unsigned* __restrict__ done,
              const int2* __restrict__ tk, float4* __restrict__ q4, int* __restrict__ order) {
     constexpr int kTpt = MAXT / kPartThreads;
+    static_assert(4 * MAXT + 4 * (kPartThreads / 64) + 4 <= 160 * 1024 / 2,
+                  "k_tile_place's LDS tile bases: gfx950 has 160 KB per CU (two blocks); other targets have 64 KB");
     __shared__ int base[MAXT];
     __shared__ int wsum[kPartThreads / 64];
     __shared__ int last;
