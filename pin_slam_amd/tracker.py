@@ -140,6 +140,30 @@ def implicit_reg(points, sdf_grad, sdf_residual, weight, lm_lambda=0.0, require_
 _REG_BUF: dict = {}
 
 
+_LOOP_BUF = {}
+
+
+def _loop_buffers(dev, n):
+    """The tracking loop's per-point buffers (sdf, grad, nn counts, std, posed points, sorted rows)
+    and its two events, one set per (device, stream), grown by 1.25x when a cloud outgrows them:
+    a tracking call then allocates nothing.  Calls on one stream are ordered and each ends with a
+    host read of its last iteration, so the next call's writes never meet the previous one's."""
+    s = _lib.stream(dev)
+    key = (str(dev), s.value)
+    lb = _LOOP_BUF.get(key)
+    if lb is None or lb["cap"] < n:
+        cap = max(int(n * 1.25), 1024)
+        lb = dict(cap=cap, sdf=torch.empty(cap, dtype=torch.float32, device=dev),
+                  grad=torch.empty((cap, 3), dtype=torch.float32, device=dev),
+                  nn=torch.empty(cap, dtype=torch.int32, device=dev),
+                  std=torch.empty(cap, dtype=torch.float32, device=dev),
+                  cur=torch.empty((cap, 3), dtype=torch.float32, device=dev),
+                  q4=torch.empty((cap, 4), dtype=torch.float32, device=dev),
+                  events=(torch.cuda.Event(), torch.cuda.Event()))
+        _LOOP_BUF[key] = lb
+    return lb
+
+
 def _reg_buffers(dev):
     """Buffers reused every step, one set per (device, stream): the reduction workspace (with
     pin_reg_step's last-block ticket), the accumulators + status record (one D2H copy), delta_T
@@ -204,12 +228,13 @@ class _RegLoop:
         self.mv = mlp_view(tracker.geo_decoder, packed=True)
         self.gv = nm.grid_view("local", True) if nm.backend() == "grid" else None
         sorted_ = self.gv is not None and n >= _LOOP_SORT_MIN and _query._TILE_QUERIES
-        self.sdf = torch.empty(n, dtype=torch.float32, device=dev)
-        self.grad = torch.empty((n, 3), dtype=torch.float32, device=dev)
-        self.nn = torch.empty(n, dtype=torch.int32, device=dev)
-        self.std = None if wf else torch.empty(n, dtype=torch.float32, device=dev)
-        self.cur = torch.empty((n, 3), dtype=torch.float32, device=dev)
-        self.q4 = torch.empty((n, 4), dtype=torch.float32, device=dev) if sorted_ else None
+        lb = _loop_buffers(dev, n)   # per-point outputs: reused views, nothing escapes the loop
+        self.sdf = lb["sdf"][:n]
+        self.grad = lb["grad"][:n]
+        self.nn = lb["nn"][:n]
+        self.std = None if wf else lb["std"][:n]
+        self.cur = lb["cur"][:n]
+        self.q4 = lb["q4"][:n] if sorted_ else None
         self.ws = order_workspace(n, dev) if sorted_ else None
         self.src, self.labels = src, labels   # kept alive with the launch record
         prm = _lib.PinRegParams(min_nn_count=nn_k, min_grad_norm=float(min_grad_norm),
@@ -221,7 +246,7 @@ class _RegLoop:
                                 q4_points=int(sorted_))
         b = self.b = _reg_buffers(dev)
         self.pose0 = init_pose.contiguous()
-        self.events = (torch.cuda.Event(), torch.cuda.Event())
+        self.events = lb["events"]
         d = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
         self.rec = [_lib.PinRegIter(src=d(src), n=n, labels=d(labels), cur=d(self.cur), q4=d(self.q4),
                                     order_ws=d(self.ws), sdf=d(self.sdf), grad=d(self.grad), nn_count=d(self.nn),
