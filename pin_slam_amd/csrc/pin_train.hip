@@ -131,9 +131,10 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     for (int d = 0; d < kD; ++d) x[d] = 0.f;
     float sdf = 0.f;
 #if PIN_NWF_X2
-    if constexpr (!WF && DX && !MF && !PAIR && Src::kIdPayload) {
-        // per-neighbour, frozen decoder, f32 decode: neighbours j and j + 1 decoded together
-        // (mlp_sdf_packed_x2: one weight read feeds both), summed in neighbour order as below
+    if constexpr (!WF && !MF && !PAIR && Src::kIdPayload) {
+        // per-neighbour, f32 decode: neighbours j and j + 1 decoded together (mlp_sdf_packed_x2:
+        // one weight read feeds both), summed in neighbour order as below; saved for the backward:
+        // the ReLU masks (DX, frozen decoder) or the neighbour vectors (a training decoder)
         auto inputs = [&](int j, bool& valid, float (&xj)[kD], float& w) {
             valid = u[j] > 0.f;
             const int id = valid ? tk.g[j] : -1;
@@ -173,9 +174,24 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
             if (!vb) kb = 0;
             sdf = sdf + ska * wa;
             sdf = sdf + skb * wb;
-            if (live && j < nn_k) ((uint2*)st.x)[t * nn_k + j] = make_uint2((uint32_t)ka, (uint32_t)(ka >> 32));
-            if (live && j + 1 < nn_k)
-                ((uint2*)st.x)[t * nn_k + j + 1] = make_uint2((uint32_t)kb, (uint32_t)(kb >> 32));
+            if constexpr (DX) {
+                if (live && j < nn_k) ((uint2*)st.x)[t * nn_k + j] = make_uint2((uint32_t)ka, (uint32_t)(ka >> 32));
+                if (live && j + 1 < nn_k)
+                    ((uint2*)st.x)[t * nn_k + j + 1] = make_uint2((uint32_t)kb, (uint32_t)(kb >> 32));
+            } else {
+                if (live && j < nn_k) {
+                    float* xo = st.x + (t * nn_k + j) * 3;
+                    xo[0] = xa[kF];
+                    xo[1] = xa[kF + 1];
+                    xo[2] = xa[kF + 2];
+                }
+                if (live && j + 1 < nn_k) {
+                    float* xo = st.x + (t * nn_k + j + 1) * 3;
+                    xo[0] = xb[kF];
+                    xo[1] = xb[kF + 1];
+                    xo[2] = xb[kF + 2];
+                }
+            }
         }
         if (writer) st.sdf[r] = sdf;
         return;
