@@ -1861,7 +1861,39 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
     const bool lds = out && sg.n == 4 && sg.off[4] == kMlpGrad && sg.off[1] == kH * kD && sg.off[2] == kH * kD + kH &&
                      sg.off[3] == kH * kD + 2 * kH && sg.p[0] == mlp.W1 && sg.p[1] == mlp.b1 && sg.p[2] == mlp.W2 &&
                      sg.p[3] == mlp.b2;
-    for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a, lds ? s_dec : nullptr);
+    if (lds) {
+        // the decoder's kMlpGrad elements in up to four per thread: every load issued before the
+        // first step (one memory latency on the chain to the pack instead of four in turn)
+        static_assert(kMlpGrad <= 4 * kTBlock, "decoder step: four elements per thread");
+        float p[4], g[4], m[4], v[4];
+        float* at[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = threadIdx.x + i * kTBlock;
+            if (t < kMlpGrad) {
+                const int sgi = (t >= sg.off[1] ? 1 : 0) + (t >= sg.off[2] ? 1 : 0) + (t >= sg.off[3] ? 1 : 0);
+                at[i] = sg.p[sgi] + (t - sg.off[sgi]);
+                p[i] = *at[i];
+                g[i] = sgrad[t];
+                m[i] = (a.zero_grad & 2) ? 0.f : sm[t];
+                v[i] = (a.zero_grad & 2) ? 0.f : sv[t];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = threadIdx.x + i * kTBlock;
+            if (t < kMlpGrad) {
+                adam_one(p[i], g[i], m[i], v[i], a);
+                *at[i] = p[i];
+                s_dec[t] = p[i];
+                sm[t] = m[i];
+                sv[t] = v[i];
+                if (a.zero_grad & 1) sgrad[t] = 0.f;
+            }
+        }
+    } else {
+        for (int64_t t = threadIdx.x; t < sg.off[sg.n]; t += kTBlock) adam_segment_body(t, sg, sgrad, sm, sv, a);
+    }
     if (out) {
         if (lds) {
             __syncthreads();
