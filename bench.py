@@ -16,8 +16,8 @@ the barrier + max-over-ranks timing is the only collective.
 Further legs in the same line (informational; `value` stays the headline): "tracker"
 (configs[2], registration steps/s on 200K source points), "mesher" (configs[4], 512^3 grid
 SDF+mask, z-slabs per rank) and "mapper" (configs[3], iterations/s of Mapper.mapping on a
-4M-point map with 1M queries per iteration per GPU, feature gradients SUM all-reduced over
-RCCL when N > 1).
+4M-point map with 1M queries per iteration per GPU; when N > 1 the feature gradients are
+reduce-scattered over RCCL, each rank steps its 1/N of the rows and the rows are all-gathered).
 
 Prints ONE JSON line (rank 0).  Roofline: achieved = 944 B/query (SURVEY.md 8(d):
 12 q + 8*Kc slots + 12*Kc positions + 4*F*k features + 16 out) x queries per launch /
@@ -60,14 +60,14 @@ def mapper_bytes_per_iter(n, L, dec=10):
     return rows * (932 + 512) + 32 * 8 * (L + 1)
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+TRAFFIC_FILE = os.path.join("profiles", "r06", "traffic.json")
 
 
-def measured_traffic(kernel_prefix):
-    """HBM-side bytes per launch of the headline kernel from the committed PMC pass
-    (tools/traffic.sh -> profiles/traffic.json), or None."""
+def measured_traffic(kernel_prefix, path=TRAFFIC_FILE):
+    """HBM-side bytes per launch of a kernel from a committed PMC pass (tools/traffic.sh ->
+    profiles/r06/*.json: FETCH_SIZE x 2 + WRITE_SIZE per launch), or None."""
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(os.path.join(ROOT, path)) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
@@ -206,35 +206,37 @@ def cpu_baseline(nm, dec, q, wf):
                       f"({t:.3f} s each)"}
 
 
-def time_kernel(nm, dec, q, wf, backend, steps, flags=1):
-    """Mean duration (ms) of the headline kernel alone -- HIP events on the launch stream around
+def time_kernel(nm, dec, q, wf, backend, steps, flags=1, mode="global", nn_k=8, want_grad=True, zero_empty=False):
+    """Mean duration (ms) of one query kernel alone -- HIP events on the launch stream around
     each pin_query_sdf(_grid) launch, with the tile order precomputed; flags 1: outputs in tile
     order (PIN_QUERY_OUT_TILE), 0: in input order -- and of the ordering pass (pin_query_sort) that
-    each step also runs."""
+    each step also runs.  mode "local": the map as the tracker queries it (query_locally, the
+    travel-distance filter); want_grad False / zero_empty: the mesher's SDF-only launch."""
     import ctypes  # noqa: F401
     from pin_slam_amd import _lib
     from pin_slam_amd.query import mlp_view, query_sort
     n = q.shape[0]
-    hv, pv = nm._views("global", False)
-    mv = mlp_view(dec, packed=True)
+    hv, pv = nm._views(mode, mode == "local")
+    mv = mlp_view(dec, packed=want_grad)
     sdf = torch.empty(n, device=q.device)
-    grad = torch.empty((n, 3), device=q.device)
+    grad = torch.empty((n, 3), device=q.device) if want_grad else None
     nn = torch.empty(n, dtype=torch.int32, device=q.device)
     std = None if wf else torch.empty(n, device=q.device)
     if backend == "grid":
-        gv = nm.grid_view("global", True)
+        gv = nm.grid_view(mode, True)
         q4 = query_sort(gv, q)
 
         def launch():
-            _lib.call("pin_query_sdf_grid_sorted_ex", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, 8, int(wf), 0,
-                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), int(flags), _lib.stream())
+            _lib.call("pin_query_sdf_grid_sorted_ex", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4), n, nn_k, int(wf),
+                      int(zero_empty), _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), int(flags),
+                      _lib.stream())
 
         def order_pass():
             query_sort(gv, q, out=q4)
     else:
         def launch():
-            _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, 8, int(wf), 0, _lib.ptr(sdf),
-                      _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
+            _lib.call("pin_query_sdf", hv.ref(), pv.ref(), mv.ref(), _lib.ptr(q), n, nn_k, int(wf), int(zero_empty),
+                      _lib.ptr(sdf), _lib.ptr(grad), _lib.ptr(nn), None, _lib.ptr(std), _lib.stream())
         order_pass = None
 
     def mean_ms(fn):
@@ -249,13 +251,42 @@ def time_kernel(nm, dec, q, wf, backend, steps, flags=1):
     return mean_ms(launch), (mean_ms(order_pass) if order_pass else 0.0)
 
 
-def nwf_leg(nm, dec, q, args, world):
+def query_kernel_name(backend, wf, want_grad=True):
+    """rocprof name of the launched query instance: <WF, PGO, GRAD, FAT, MF> (grid), <WF, PGO,
+    GRAD, MF> (hash); the SDF-only instance (mesher) decodes on the VALU."""
+    from pin_slam_amd.query import _MLP_PACK
+    mf = str(bool(_MLP_PACK) and want_grad).lower()
+    g = str(bool(want_grad)).lower()
+    if backend == "grid":
+        return f"k_query_sdf_grid<{str(wf).lower()}, false, {g}, true, {mf}>"
+    return f"k_query_sdf<{str(wf).lower()}, false, {g}, {mf}>"
+
+
+def query_roofline(bytes_per_query, n, kern_ms, kernel, traffic_file=None, note=None):
+    """roofline object of a query leg: algorithmic bytes per launch / the kernel's mean launch
+    time (HIP events), HBM peak; traffic = the PMC bytes per launch of the same kernel from the
+    committed profile (or None)."""
+    achieved = bytes_per_query * n / (kern_ms * 1e-3)
+    traffic = measured_traffic(kernel, traffic_file) if traffic_file else measured_traffic(kernel)
+    out = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": kernel, "kernel_ms": kern_ms,
+           "algorithmic_bytes_per_query": bytes_per_query, "queries_per_launch": n,
+           "traffic_source": traffic_file or TRAFFIC_FILE}
+    if note:
+        out["note"] = note
+    return out
+
+
+def nwf_leg(nm, dec, q, args, world, rank=0, backend="grid"):
     """The same batch and map with per-neighbour decoding (weighted_first False: SDF = IDW mean
     of the 8 neighbours' decoded SDFs, plus its std and gradient) -- what the reference's lidar
-    configs (config/lidar_slam/run_kitti.yaml etc.) run."""
+    configs (config/lidar_slam/run_kitti.yaml:25 etc.) run.  Roofline: the same 944 algorithmic
+    bytes per query as the headline (the decoder's 8 evaluations per query read no more memory),
+    over the per-neighbour kernel's own launch time; CPU baseline: the restatement with
+    per-neighbour decoding on one full batch."""
     def step():
         return P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False, want_std=True,
-                           weighted_first=False)
+                           weighted_first=False, out_order="tile")
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -272,14 +303,22 @@ def nwf_leg(nm, dec, q, args, world):
         torch.cuda.synchronize()
         windows.append(time.perf_counter() - t0)
     el = statistics.median(windows)
-    t = torch.tensor([el], dtype=torch.float64, device=q.device)
+    kern_ms, order_ms = time_kernel(nm, dec, q, False, backend, args.steps, flags=1)
+    t = torch.tensor([el, kern_ms], dtype=torch.float64, device=q.device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t[0])
-    return {"metric": "SDF+grad+std queries/sec, per-neighbour decoding", "value": q.shape[0] * args.steps * world / el,
-            "unit": "queries/s", "ms_per_step": el / args.steps * 1e3, "scaling": "weak",
-            "windows_ms_per_step": [w / args.steps * 1e3 for w in windows],
-            "config": {"workload": "configs[1] batch and map, weighted_first False (8 decoder evaluations per query)"}}
+    el, kern_ms = float(t[0]), float(t[1])
+    res = {"metric": "SDF+grad+std queries/sec, per-neighbour decoding", "value": q.shape[0] * args.steps * world / el,
+           "unit": "queries/s", "ms_per_step": el / args.steps * 1e3, "scaling": "weak",
+           "windows_ms_per_step": [w / args.steps * 1e3 for w in windows],
+           "roofline": query_roofline(BYTES_PER_QUERY, q.shape[0], kern_ms, query_kernel_name(backend, False),
+                                      note="the query kernel alone (tile order precomputed); ms_per_step adds the "
+                                           "sort (outputs in tile order, as the headline)"),
+           "config": {"workload": "configs[1] batch and map, weighted_first False (8 decoder evaluations per query)"}}
+    res["roofline"]["order_pass_ms"] = order_ms
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(nm, dec, q, False)
+    return res
 
 
 TRACKER_SRC = 200_000      # configs[2]: source points per registration step
@@ -361,14 +400,79 @@ def tracker_leg(args, dev, world, rank):
             "residual_bound_cm": cfg.surface_sample_range_m * 0.5 * 100.0,
             "note": "Tracker.tracking from the perturbed pose (0.2 m, 0.5 deg), median of 5 windows; iterations "
                     "counted as run; pose error against the true pose of the scan"}
-    return {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
-            "queries_per_sec": n_src * steps / el, "ms_per_iter": el / steps * 1e3, "steps": steps,
-            "source_points": n_src, "valid_points": int(out[4].shape[0]), "map_points": nm.count(),
-            "scaling": "replicas", "tracking_loop": loop,
+    # the step's dominant kernel alone: the fused SDF + gradient (+ std) query of every source point
+    # in the tracker's local mode, tile order precomputed.  Algorithmic bytes per query (SURVEY.md
+    # 8(d) at run_kitti settings): 12 q + (8 slot + 12 position) x Kc + 4 F k features + 20 out
+    # (sdf, grad, std; 16 with weighted_first)
+    wf = bool(cfg.weighted_first)
+    kc, k, F = int(nm.neighbor_K), int(cfg.query_nn_k), int(cfg.feature_dim)
+    bpq = 12 + 20 * kc + 4 * F * k + (16 if wf else 20)
+    kern_ms, order_ms = time_kernel(nm, dec, src, wf, nm.backend(), steps, flags=1, mode="local", nn_k=k)
+    roof = query_roofline(bpq, n_src, kern_ms, query_kernel_name(nm.backend(), wf),
+                          os.path.join("profiles", "r06", "tracker_traffic.json"),
+                          note=f"12 + 20 x Kc {kc} + 4 x F {F} x k {k} + {16 if wf else 20} B per query; the query "
+                               f"kernel of one registration step alone (tile order precomputed)")
+    roof["order_pass_ms"] = order_ms
+    res = {"metric": "tracker registration iterations/sec", "value": steps / el, "unit": "iters/s",
+           "queries_per_sec": n_src * steps / el, "ms_per_iter": el / steps * 1e3, "steps": steps,
+           "source_points": n_src, "valid_points": int(out[4].shape[0]), "map_points": nm.count(),
+           "scaling": "replicas", "tracking_loop": loop, "roofline": roof,
             "config": {"workload": "Tracker.registration_step, KITTI-style 64 x 3200-ray scan (~200K points) against "
                                    "a 12-frame synthetic street map, run_kitti.yaml settings (configs[2])",
                        "note": "registration_step: one call (query, normal equations, device solve, one host "
                                "read of 39 doubles, valid-point gather) per timed iteration"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = tracker_cpu_baseline(nm, dec, cfg, src)
+    return res
+
+
+def _torch_cpu_local_map(nm, wf):
+    """The drop-in map in the tracker's local mode as oracle/pin_torch_cpu tensors: the hash
+    table over every point, the travel-distance filter (model/neural_points.py:480-488), the
+    global2local table and the local points / features the neighbours are read from."""
+    from oracle import pin_torch_cpu as T
+    c = nm.config
+    td = nm.travel_dist.detach().cpu().numpy()
+    ts_c = nm.point_ts_create.detach().cpu().numpy()
+    dtd = np.abs(td[int(nm.cur_ts)] - td[ts_c])
+    time_ok = torch.from_numpy(dtd < np.float32(nm.diff_travel_dist_local))
+    return T.TorchMap(nm.resolution, nm.buffer_size, nm.buffer_pt_index.cpu(), nm.neural_points.cpu(),
+                      nm.local_geo_features.detach().cpu(), nm.local_point_certainties.cpu(), nm.neighbor_dx.cpu(),
+                      nm.max_valid_dist2, c.query_nn_k, wf, time_ok=time_ok, global2local=nm.global2local.cpu(),
+                      local_points=nm.local_neural_points.cpu())
+
+
+def tracker_cpu_baseline(nm, dec, cfg, src):
+    """One registration step of the same ~200K-point cloud in the PyTorch-CPU restatement
+    (oracle/pin_torch_cpu.registration_step: local-mode query with autograd gradient and IDW std,
+    validity, Geman-McClure weights, normal equations, f64 solve -- utils/tracker.py:277-520) on
+    this process's cores; one warm-up, median of 5."""
+    import torch as _t
+    from oracle import pin_torch_cpu as T
+    threads = cpu_threads()
+    old = _t.get_num_threads()
+    _t.set_num_threads(threads)
+    try:
+        m = _torch_cpu_local_map(nm, bool(cfg.weighted_first))
+        mlp = T.TorchMLP(dec.layers[0].weight.detach().cpu(), dec.layers[0].bias.detach().cpu(),
+                         dec.lout.weight.detach().cpu(), dec.lout.bias.detach().cpu(), dec.sdf_scale)
+        ph = src.detach().cpu()
+        zeros = _t.zeros(ph.shape[0])
+        max_std = float(cfg.surface_sample_range_m * cfg.max_sdf_std_ratio)
+        valid = []
+
+        def one():
+            valid.append(T.registration_step(m, mlp, ph, zeros, cfg.reg_min_grad_norm, cfg.reg_max_grad_norm,
+                                             cfg.reg_GM_dist_m, cfg.reg_GM_grad, cfg.reg_lm_lambda, max_std,
+                                             int(cfg.query_nn_k))[1])
+        t = _timed_median(one)
+    finally:
+        _t.set_num_threads(old)
+    return {"value": 1.0 / t, "unit": "iters/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "queries_per_sec": ph.shape[0] / t, "valid_points": valid[-1],
+            "sample": f"one registration step of the same {ph.shape[0]}-point cloud: oracle/pin_torch_cpu.py "
+                      f"registration_step (torch {_t.__version__} CPU, {threads} threads, autograd gradient), one "
+                      f"warm-up, median of 5 ({t:.3f} s each)"}
 
 
 def mesher_leg(nm, dec, pts, args, dev, world, rank):
@@ -411,6 +515,15 @@ def mesher_leg(nm, dec, pts, args, dev, world, rank):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t[0])
+    # the query kernel alone over the whole slab: every batch's tile order precomputed, HIP events
+    # around each SDF-only launch (zero_empty, mc mask from nn_count, outputs in grid order as the
+    # mesher needs them), summed over the batches.
+    # Algorithmic bytes split by the outcome of each query: a query with
+    # neighbours reads 12 q + 8 Kc slots + 12 Kc positions + 4 F k features and writes 4 = 932 B;
+    # an empty one (nn_count 0: every probed cell empty or out of range) only its 12 + 8 Kc + 4
+    roof = None
+    if nm.backend() == "grid":
+        roof = mesher_kernel_roofline(nm, dec, coord)
     # marching cubes over this rank's slab (the reference runs skimage on the host, mesher.py:327)
     from pin_slam_amd.mesher import marching_cubes
     nzs = z1 - z0
@@ -424,13 +537,92 @@ def mesher_leg(nm, dec, pts, args, dev, world, rank):
         mv, mf = marching_cubes(grid, gmask)
     torch.cuda.synchronize()
     mc_ms = (time.perf_counter() - tm) / reps * 1e3
-    return {"metric": "mesher grid SDF queries/sec", "value": MESH_RES ** 3 / el, "unit": "queries/s",
-            "ms_per_grid": el * 1e3, "map_fit_loss": fit_loss, "scaling": "strong", "masked_fraction": float(mask.float().mean()),
+    res = {"metric": "mesher grid SDF queries/sec", "value": MESH_RES ** 3 / el, "unit": "queries/s",
+           "ms_per_grid": el * 1e3, "map_fit_loss": fit_loss, "scaling": "strong", "masked_fraction": float(mask.float().mean()),
+           "roofline": roof,
             "marching_cubes": {"ms_per_slab": mc_ms, "vertices": int(mv.shape[0]), "faces": int(mf.shape[0]),
                                "note": "device marching cubes over this rank's masked slab, incl. the count "
                                        "read-back and degenerate-face filter"},
             "config": {"workload": "512^3 grid at 0.1 m over the 1M-point map, SDF + mc_mask, batches of 2^20, "
                                    "z-slabs per rank (configs[4])"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        mid = (n // MESH_BATCH // 2) * MESH_BATCH
+        res["cpu_baseline"] = mesher_cpu_baseline(nm, dec, coord[mid:mid + MESH_BATCH])
+    return res
+
+
+def mesher_kernel_roofline(nm, dec, coord):
+    """roofline of the mesher's query kernel: algorithmic bytes of every query by outcome (932 B
+    with neighbours, 12 + 8 Kc + 4 B without) over the summed HIP-event time of the SDF-only
+    launches of every batch (tile order precomputed)."""
+    from pin_slam_amd import _lib
+    from pin_slam_amd.query import mlp_view, query_sort
+    c = nm.config
+    wf, k, F, kc = bool(c.weighted_first), int(c.query_nn_k), int(c.feature_dim), int(nm.neighbor_K)
+    n = coord.shape[0]
+    gv = nm.grid_view("global", True)
+    _, pv = nm._views("global", False)
+    mv = mlp_view(dec, packed=False)
+    spans = [(a, min(n, a + MESH_BATCH)) for a in range(0, n, MESH_BATCH)]
+    q4s = [query_sort(gv, coord[a:b]) for a, b in spans]
+    sdf = torch.empty(n, device=coord.device)
+    nn = torch.empty(n, dtype=torch.int32, device=coord.device)
+    std = None if wf else torch.empty(n, device=coord.device)
+
+    def launch(j):
+        a, b = spans[j]
+        _lib.call("pin_query_sdf_grid_sorted_ex", gv.ref(), pv.ref(), mv.ref(), _lib.ptr(q4s[j]), b - a, k, int(wf), 1,
+                  _lib.ptr(sdf[a:b]), None, _lib.ptr(nn[a:b]), None, _lib.ptr(None if std is None else std[a:b]),
+                  0, _lib.stream())
+    for j in range(len(spans)):
+        launch(j)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in spans]
+    for j, (a, b) in enumerate(ev):
+        a.record()
+        launch(j)
+        b.record()
+    torch.cuda.synchronize()
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev)
+    n_occ = int((nn >= 1).sum())
+    b_occ = 12 + 20 * kc + 4 * F * k + 4
+    b_empty = 12 + 8 * kc + 4
+    algo = n_occ * b_occ + (n - n_occ) * b_empty
+    achieved = algo / (kern_ms * 1e-3)
+    kernel = query_kernel_name("grid", wf, want_grad=False)
+    per_launch = measured_traffic(kernel, os.path.join("profiles", "r06", "mesher_traffic.json"))
+    return {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK,
+            "traffic": per_launch, "traffic_source": "profiles/r06/mesher_traffic.json (per 2^20-query launch)",
+            "kernel": kernel, "kernel_ms_per_grid": kern_ms, "launches": len(spans),
+            "queries_with_neighbours": n_occ, "queries_empty": n - n_occ,
+            "algorithmic_bytes": {"with_neighbours": b_occ, "empty": b_empty, "per_grid": algo,
+                                  "per_launch": algo / len(spans)},
+            "note": "the SDF-only query kernel alone (tile order precomputed), summed over the grid's batches; "
+                    "ms_per_grid adds the sorts, the mask and the output copies"}
+
+
+def mesher_cpu_baseline(nm, dec, coord):
+    """One 2^20-query batch of the same grid (the middle z-range of the slab) in the PyTorch-CPU
+    restatement (oracle/pin_torch_cpu.sdf_only: Mesher.query_points' SDF + mc_mask,
+    utils/mesher.py:41-136) on this process's cores; one warm-up, median of 5."""
+    import torch as _t
+    from oracle import pin_torch_cpu as T
+    threads = cpu_threads()
+    old = _t.get_num_threads()
+    _t.set_num_threads(threads)
+    try:
+        m = _torch_cpu_map(nm, bool(nm.config.weighted_first))
+        mlp = T.TorchMLP(dec.layers[0].weight.detach().cpu(), dec.layers[0].bias.detach().cpu(),
+                         dec.lout.weight.detach().cpu(), dec.lout.bias.detach().cpu(), dec.sdf_scale)
+        qh = coord.cpu()
+        out = []
+        t = _timed_median(lambda: out.append(T.sdf_only(m, mlp, qh, int(nm.config.mesh_min_nn))))
+    finally:
+        _t.set_num_threads(old)
+    return {"value": qh.shape[0] / t, "unit": "queries/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"one {qh.shape[0]}-query batch of the grid (middle of the slab, "
+                      f"{float(out[-1][1].float().mean()):.4f} masked): oracle/pin_torch_cpu.py sdf_only (torch "
+                      f"{_t.__version__} CPU, {threads} threads), one warm-up, median of 5 ({t:.3f} s each)"}
 
 
 _FRAME_TIMING = ("each frame timed on its own (synchronised before and after; the frame's own host syncs "
@@ -658,19 +850,23 @@ def slam_frame_leg(args, dev, world, rank):
                                f"{warm}); the timed frames include the filter of frame {2 * warm - 1}"}}
 
 
-def mapper_cpu_baseline(nm, dec, coord, label):
-    """One full mapper iteration of the same workload in the PyTorch-CPU restatement
-    (oracle/pin_torch_cpu.py: the 1M-row batch + 6 x 100K numerical-gradient stencil rows,
+def mapper_cpu_baseline(nm, dec, coord, label, full_rows=None):
+    """One mapper iteration of the same workload in the PyTorch-CPU restatement
+    (oracle/pin_torch_cpu.py: the batch + its 6 x N/10 numerical-gradient stencil rows,
     training-mode query, BCE + eikonal, backward, Adam on the [L+1, 8] features, decoder frozen),
-    on this process's cores; one warm-up, median of 5."""
+    on this process's cores; one warm-up, median of 5.  full_rows: the batch is a sample of a
+    full_rows batch (the per-neighbour iteration, ~8x the decoder work, is timed on a quarter
+    batch to bound the CPU time); the rate is then scaled to a full iteration by the row ratio
+    (the [L+1, 8] Adam, ~2 % of the CPU iteration, scaled with it: a slightly low baseline)."""
     import torch as _t
     from oracle import pin_torch_cpu as T
     threads = cpu_threads()
     old = _t.get_num_threads()
     _t.set_num_threads(threads)
     c = nm.config
+    wf = bool(c.weighted_first)
     try:
-        m = _torch_cpu_map(nm, True, local=True)
+        m = _torch_cpu_map(nm, wf, local=True)
         mlp = T.TorchMLP(dec.layers[0].weight.detach().cpu(), dec.layers[0].bias.detach().cpu(),
                          dec.lout.weight.detach().cpu(), dec.lout.bias.detach().cpu(), dec.sdf_scale)
         feats = _t.nn.Parameter(m.features.clone())
@@ -685,10 +881,13 @@ def mapper_cpu_baseline(nm, dec, coord, label):
         t = _timed_median(one)
     finally:
         _t.set_num_threads(old)
-    return {"value": 1.0 / t, "unit": "iters/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"one full iteration ({coord.shape[0]} batch rows + stencil, {m.points.shape[0]}-point map): "
-                      f"oracle/pin_torch_cpu.py (torch {_t.__version__} CPU, {threads} threads, autograd backward, "
-                      f"torch.optim.Adam), one warm-up, median of 5 ({t:.2f} s each)"}
+    scale = (full_rows or coord.shape[0]) / coord.shape[0]
+    what = ("one full iteration" if scale == 1 else
+            f"a {coord.shape[0]}-row sample of the {full_rows}-row iteration, rate scaled by {scale:g}")
+    return {"value": 1.0 / (t * scale), "unit": "iters/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{what} ({coord.shape[0]} batch rows + stencil, {m.points.shape[0]}-point map, weighted_first "
+                      f"{wf}): oracle/pin_torch_cpu.py (torch {_t.__version__} CPU, {threads} threads, autograd "
+                      f"backward, torch.optim.Adam), one warm-up, median of 5 ({t:.2f} s each)"}
 
 
 def _shard_info(mapper):
@@ -715,8 +914,9 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
     (decoder frozen, the steady state after freeze_after_frame).  W > 1 (weak scaling, 1M queries
     per rank): --mapper-shard space (default) -- every rank owns a slab of the map, samples its
     batches there and exchanges only halo gradient / feature rows with the neighbouring slabs
-    (pin_slam_amd.sharding); dense -- every rank samples the whole map and the [L+1,8] feature
-    gradient is SUM all-reduced over RCCL every iteration."""
+    (pin_slam_amd.sharding); dense -- every rank samples the whole map, the [L+1,8] feature
+    gradient is reduce-scattered over RCCL, Adam steps each rank's 1/W of the rows and the rows
+    are all-gathered every iteration (sharding.OwnerAdam)."""
     wf = (not args.nwf) if wf is None else wf
     nm, dec, pts = surface_map(MAPPER_SIDE, device=dev, buffer_size=int(5e7), nn_k=8, weighted_first=wf,
                                query_backend=args.backend, bs=MAPPER_BS)
@@ -769,20 +969,49 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
                                   "stencil (configs[3])", "map_points": int(pts.shape[0]),
                       "queries_per_iter_per_gpu": MAPPER_BS, "decoder": "frozen", "optimizer": "Adam on features",
                       "weighted_first": wf, "data_parallel": shard if world > 1 else None,
-                      "grad_allreduce": (f"{dist.get_backend()} all_reduce SUM of the [L+1,8] f32 gradient "
-                                         f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter) in {_ar_buckets()} row buckets, Adam "
-                                         f"on each bucket as soon as it is reduced") if world > 1 and shard == "dense"
+                      "grad_exchange": (f"{dist.get_backend()} reduce_scatter of the [L+1,8] f32 gradient "
+                                        f"({4 * 8 * (L + 1) / 1e6:.0f} MB/iter) in {_ar_buckets()} row buckets, Adam "
+                                        f"on this rank's 1/{world} of each bucket as soon as it lands, all_gather of "
+                                        f"the stepped rows (sharding.OwnerAdam)") if world > 1 and shard == "dense"
                       else None,
                       "shard": (_shard_info(mapper) if world > 1 and shard == "space" else None),
                       "candidate_backend": backend, "timed": "mapping(K): K iterations + Adam state init + "
                                                              "assign_local_to_global"},
            "roofline": {"bound": "hbm", "achieved": bpi / (ms * 1e-3) / 1e9, "peak": HBM_PEAK / 1e9,
-                        "unit": "GB/s", "frac": bpi / (ms * 1e-3) / HBM_PEAK, "traffic": None,
-                        "scope": "whole iteration", "algorithmic_bytes_per_iter": bpi}}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wf == (not args.nwf):
-        idx = torch.randint(0, MAPPER_POOL, (MAPPER_BS,), device=dev)
-        res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx])
+                        "unit": "GB/s", "frac": bpi / (ms * 1e-3) / HBM_PEAK,
+                        "scope": "whole iteration", "algorithmic_bytes_per_iter": bpi,
+                        **mapper_traffic(wf)}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rows = MAPPER_BS if wf else MAPPER_BS // 4
+        idx = torch.randint(0, MAPPER_POOL, (rows,), device=dev)
+        res["cpu_baseline"] = mapper_cpu_baseline(nm, dec, coord[idx], label[idx], full_rows=MAPPER_BS)
     return res
+
+
+def mapper_iter_kernels(wf):
+    """The kernels one mapper iteration launches once each (gather, tile sort of the rows, forward,
+    backward, loss reduction, Adam); their PMC bytes per launch summed are the iteration's
+    traffic.  The forward / backward instances carry weighted_first as their first template
+    argument; the others are shared by both decoding modes (same sizes)."""
+    w = str(bool(wf)).lower()
+    return ("k_train_gather_packed", "k_tile_rank<16, 16384>", "k_tile_place<2, 16384>",
+            f"k_train_forward_grid<{w},", f"k_train_backward<{w},", "k_loss_final", "k_adam_train")
+
+
+def mapper_traffic(wf):
+    """roofline.traffic of a mapper leg: the HBM bytes of one iteration's kernels from the committed
+    PMC pass over the mapper legs (profiles/r06/mapper_traffic.json, tools/traffic.sh), with the
+    per-kernel split."""
+    path = os.path.join("profiles", "r06", "mapper_traffic.json")
+    parts = {}
+    kernels = mapper_iter_kernels(wf)
+    for k in kernels:
+        b = measured_traffic(k, path)
+        if b is not None:
+            parts[k] = b
+    if len(parts) != len(kernels):
+        return {"traffic": None, "traffic_source": path + " (missing)"}
+    return {"traffic": sum(parts.values()), "traffic_source": path, "traffic_per_kernel": parts}
 
 
 _T0 = time.perf_counter()
@@ -874,14 +1103,10 @@ def main():
     value = total_q / elapsed
     achieved = BYTES_PER_QUERY * N_QUERY / (kern_ms * 1e-3)
     # the launched instance: <WF, PGO, GRAD, FAT, MF> (grid) / <WF, PGO, GRAD, MF> (hash)
-    traffic = None
     from pin_slam_amd.query import _MLP_PACK
-    mf = str(bool(_MLP_PACK)).lower()
-    kernel_name = "k_query_sdf_grid" if backend == "grid" else "k_query_sdf"
-    kernel_tpl = (f"{str(wf).lower()}, false, true, true, {mf}>" if backend == "grid"
-                  else f"{str(wf).lower()}, false, true, {mf}>")
-    traffic = (args.traffic_bytes if args.traffic_bytes is not None
-               else measured_traffic(f"{kernel_name}<" + kernel_tpl))
+    kernel_full = query_kernel_name(backend, wf)
+    kernel_name = kernel_full.split("<")[0]
+    traffic = args.traffic_bytes if args.traffic_bytes is not None else measured_traffic(kernel_full)
     out = {
         "metric": "SDF+grad queries/sec over 1M-point map",
         "value": value,
@@ -904,8 +1129,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
-                     "traffic_source": "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
-                                       "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
+                     "traffic_source": TRAFFIC_FILE + " (rocprofv3 --pmc FETCH_SIZE + WRITE_SIZE, "
+                                      "FETCH x2 per MI355X_MICROARCH.md gfx950 note)",
                      "kernel": kernel_name, "kernel_ms": kern_ms,
                      "order_pass_ms": order_ms,
                      "algorithmic_bytes_per_query": BYTES_PER_QUERY,
@@ -916,7 +1141,7 @@ def main():
                      "frac_kernel": achieved / HBM_PEAK,
                      "frac_step": (value / world) * BYTES_PER_QUERY / HBM_PEAK,
                      "frac_pmc_traffic": (traffic / (kern_ms * 1e-3) / HBM_PEAK) if traffic else None},
-        "mfma": mfma_evidence(f"{kernel_name}<" + kernel_tpl, wf, kern_ms) if _MLP_PACK else None,
+        "mfma": mfma_evidence(kernel_full, wf, kern_ms) if _MLP_PACK else None,
         # the same step with the outputs scattered to each query's own index (query_sdf's default
         # for callers that index the outputs by query): same work, uncoalesced stores
         "input_order": None if args.no_input_order else {
@@ -928,7 +1153,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(nm, dec, q, wf)
     if wf and not args.no_nwf_leg:
         progress("per_neighbour")
-        out["per_neighbour"] = nwf_leg(nm, dec, q, args, world)
+        out["per_neighbour"] = nwf_leg(nm, dec, q, args, world, rank, backend)
     if not args.no_mesher:
         progress("mesher")
         out["mesher"] = mesher_leg(nm, dec, pts, args, dev, world, rank)

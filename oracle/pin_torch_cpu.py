@@ -144,3 +144,47 @@ def mapping_iteration(m: TorchMap, mlp: TorchMLP, features: torch.nn.Parameter, 
     loss.backward()
     opt.step()
     return float(loss.detach())
+
+
+def sdf_grad_std(m: TorchMap, mlp: TorchMLP, q: torch.Tensor):
+    """utils/tracker.py:176-275 (query_source_points, one batch): SDF, autograd dsdf/dq, nn_count and,
+    with per-neighbour decoding, the IDW standard deviation of the neighbours' SDFs (:245-249)."""
+    q = q.detach().to(torch.float32).requires_grad_(True)
+    x, w, _, nn = query(m, q)
+    s = mlp(x)[..., 0]
+    if m.wf:
+        mean, std = s, torch.zeros_like(s)
+    else:
+        mean = (s * w).sum(1)
+        std = torch.sqrt((w * (s - mean[:, None]) ** 2).sum(1))
+    (g,) = torch.autograd.grad(mean.sum(), q)
+    return mean.detach(), g, nn, std.detach()
+
+
+def registration_step(m: TorchMap, mlp: TorchMLP, points, labels, min_grad_norm, max_grad_norm, gm_dist, gm_grad,
+                      lm_lambda, max_sdf_std, min_nn):
+    """utils/tracker.py:277-452 + implicit_reg :468-520 without colours / normals: the query, the
+    validity mask (nn_count >= min_nn, gradient norm window, sdf std), Geman-McClure weights
+    normalised by 2 mean(w), J = [p x g, g], N = J^T W J (+ lm_lambda diag N), g = -(J W)^T r and
+    the f64 6x6 solve.  Returns (the 6-vector increment, the valid-point count)."""
+    sdf, grad, nn, std = sdf_grad_std(m, mlp, points)
+    gn = grad.norm(dim=-1)
+    valid = (nn >= min_nn) & (gn < max_grad_norm) & (gn > min_grad_norm) & (std < max_sdf_std)
+    p, g, r, gv = points[valid], grad[valid], sdf[valid] - labels[valid], gn[valid]
+    w = ((gm_grad / (gm_grad ** 2 + (gv - 1.0) ** 2)) ** 2 * (gm_dist / (gm_dist ** 2 + r ** 2)) ** 2)[:, None]
+    w = w / (2.0 * w.mean())
+    J = torch.cat((torch.cross(p, g, dim=-1), g), -1)
+    N = J.T @ (w * J)
+    N = N + lm_lambda * torch.diag(torch.diag(N))
+    rhs = -(J * w).T @ r
+    t = torch.linalg.inv(N.to(torch.float64)) @ rhs.to(torch.float64)
+    return t, int(valid.sum())
+
+
+def sdf_only(m: TorchMap, mlp: TorchMLP, q: torch.Tensor, min_nn):
+    """utils/mesher.py:41-136 (query_points, one batch): SDF of the rows with nn_count >= 1 (0
+    elsewhere) and mc_mask = nn_count >= mesh_min_nn, no gradient."""
+    with torch.no_grad():
+        s, _, _, nn = predict(m, mlp, q.to(torch.float32))
+        s = torch.where(nn >= 1, s, torch.zeros_like(s))
+    return s, nn >= min_nn

@@ -616,134 +616,6 @@ k_tile_place(const float* __restrict__ q, int64_t n, int ntiles, int* __restrict
     }
 }
 
-// The tile sort in ONE launch (small grids): rank as k_tile_rank, then a grid-wide barrier on a
-// counter in the workspace state (every block of a <= kFusedMaxBlocks grid is resident at once:
-// one 1024-thread block per CU, at most two with 16,384 tiles' 64 KB of LDS), then the tile totals' scan and the placement with each
-// thread's queries, tiles and ranks still in registers -- no second launch, no re-read of the
-// queries and no (tile, offset) round trip through memory.  The barrier's wait is bounded: a
-// block that waits too long sets *err and goes on (wrong order, no hang).  The last block to
-// leave zeroes the totals and the two counters for the next call.
-constexpr int kFusedMaxBlocks = 256;
-#ifdef PIN_SORT_STAMPS   // experiment: per-block phase timestamps of k_tile_sort_fused (pin_debug_sort_stamps)
-__device__ unsigned long long g_sort_stamps[kFusedMaxBlocks * 8];
-#define PIN_STAMP(I) do { if (threadIdx.x == 0) g_sort_stamps[blockIdx.x * 8 + (I)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define PIN_STAMP(I) do { } while (0)
-#endif
-
-template <int PER, int MAXT>
-__global__ void __launch_bounds__(kPartThreads)
-k_tile_sort_fused(const float* __restrict__ q, int64_t n, TileMap t, int* __restrict__ tot, unsigned* __restrict__ sync,
-                  float4* __restrict__ q4, int* __restrict__ order) {
-    constexpr int kTpt = MAXT / kPartThreads;
-    static_assert(4 * MAXT + 128 <= 160 * 1024, "LDS of the fused tile sort exceeds gfx950's 160 KB per CU");
-    __shared__ int h[MAXT];
-    __shared__ int wsum[kPartThreads / 64];
-    __shared__ int last;
-    const int k = threadIdx.x;
-    PIN_STAMP(0);
-#pragma unroll
-    for (int j = 0; j < kTpt; ++j) h[k + j * kPartThreads] = 0;
-    const int64_t lo = (int64_t)blockIdx.x * PER * kPartThreads + k;
-    float x[PER], y[PER], z[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int64_t i = lo + (int64_t)u * kPartThreads;
-        const int64_t j = i < n ? i : 0;
-        x[u] = q[3 * j];
-        y[u] = q[3 * j + 1];
-        z[u] = q[3 * j + 2];
-    }
-    int tile[PER], rank[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) tile[u] = lo + (int64_t)u * kPartThreads < n ? tile_of(x[u], y[u], z[u], t) : -1;
-    __syncthreads();
-    PIN_STAMP(1);
-#pragma unroll
-    for (int u = 0; u < PER; ++u) rank[u] = tile[u] >= 0 ? atomicAdd(h + tile[u], 1) : 0;
-    __syncthreads();
-    PIN_STAMP(2);
-    // this block's run inside each tile (independent returning atomics); every block visits the
-    // tiles from its own starting point, so the blocks' same-address atomics on a line of the totals
-    // arrive spread over time instead of all blocks on the first line at once
-    const int rot = (int)((blockIdx.x * 1237u) & (MAXT - 1)) & ~63;
-    int run[kTpt];
-#pragma unroll
-    for (int j = 0; j < kTpt; ++j) {
-        const int tt = (k + j * kPartThreads + rot) & (MAXT - 1);
-        const int c = h[tt];
-        run[j] = c ? atomicAdd(tot + tt, c) : 0;
-    }
-    // grid barrier: every block has reserved its runs (the returning atomics above are complete)
-    __syncthreads();
-    PIN_STAMP(3);
-    if (k == 0) {
-        // (no fence: the returning atomics above have completed at the device's coherence point)
-        atomicAdd(sync, 1u);
-        const unsigned nb = gridDim.x;
-        int spins = 0;
-        while (__hip_atomic_load(sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nb) {
-            if (++spins > (1 << 24)) {   // ~1 s of polls: never in a healthy run; give up rather than hang
-                atomicOr(sync + 2, 1u);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    PIN_STAMP(4);
-    // the tile totals (device-scope loads: they were written by other blocks' atomics) and their
-    // exclusive scan; thread k owns tiles kTpt*k .. kTpt*k + kTpt-1
-    int v[kTpt], sum = 0;
-#pragma unroll
-    for (int j = 0; j < kTpt; ++j) {
-        v[j] = kTpt * k + j < t.ntiles
-                   ? __hip_atomic_load(tot + kTpt * k + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        sum += v[j];
-    }
-    int incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int w = __shfl_up(incl, o);
-        if ((k & 63) >= o) incl += w;
-    }
-    if ((k & 63) == 63) wsum[k >> 6] = incl;
-#pragma unroll
-    for (int j = 0; j < kTpt; ++j) h[(k + j * kPartThreads + rot) & (MAXT - 1)] = run[j];   // the block's run, by tile
-    __syncthreads();
-    int base = incl - sum;
-    for (int w = 0; w < (k >> 6); ++w) base += wsum[w];
-#pragma unroll
-    for (int j = 0; j < kTpt; ++j) {   // h[tile] = the tile's base + this block's run in it
-        h[kTpt * k + j] += base;
-        base += v[j];
-    }
-    __syncthreads();
-    PIN_STAMP(5);
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int64_t i = lo + (int64_t)u * kPartThreads;
-        if (tile[u] < 0) continue;
-        const int64_t pos = (int64_t)h[tile[u]] + rank[u];
-        if (pos < 0 || pos >= n) continue;   // only a workspace whose state was not zeroed
-        if (q4) q4[pos] = make_float4(x[u], y[u], z[u], __int_as_float((int)i));
-        if (order) order[pos] = (int)i;
-    }
-    // leave: the last block out zeroes the totals and the counters (every block has read them)
-#ifdef PIN_SORT_STAMPS
-    __syncthreads();
-#endif
-    PIN_STAMP(6);
-    if (k == 0) last = atomicAdd(sync + 1, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-#pragma unroll
-        for (int j = 0; j < kTpt; ++j) tot[k + j * kPartThreads] = 0;
-        if (k == 0) {
-            sync[0] = 0u;
-            sync[1] = 0u;
-        }
-    }
-}
-
 // host: tile map of a grid box with at most maxt tiles
 TileMap tile_map(const PinGrid& g, int maxt) {
     TileMap t;
@@ -794,35 +666,16 @@ int sort_queries(const PinGrid& g, const float* q, int64_t n, float4* q4, int* o
 #endif
     constexpr int kPlacePer = PIN_PLACE_PER;
     const int nplace = (int)((n + kPlacePer * kPartThreads - 1) / (kPlacePer * kPartThreads));
-    // one launch (k_tile_sort_fused) only on request (PIN_SORT_FUSED=1): its grid barrier needs
-    // every block resident at once, which holds for one process per GPU but not when processes
-    // share the GPU -- 8 ranks on one device (bench.py --dist-backend gloo rehearsal) left blocks of
-    // several ranks' sorts spinning for their absent peers.  Measured: headline step 52.6 -> 51.4 us.
-    static const bool fused_ok = [] {
-        const char* e = getenv("PIN_SORT_FUSED");
-        return e && e[0] == '1';
-    }();
     auto launch = [&](auto per_tag, auto maxt_tag) {
         constexpr int PER = decltype(per_tag)::value;
         constexpr int MAXT = decltype(maxt_tag)::value;
         const int nblk = (int)((n + PER * kPartThreads - 1) / (PER * kPartThreads));
-        if constexpr (PER <= 8) {   // more queries per thread would spill: 1024-thread blocks cap at 128 VGPRs
-            if (fused_ok && nblk <= kFusedMaxBlocks) {
-                hipLaunchKernelGGL((k_tile_sort_fused<PER, MAXT>), dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot,
-                                   done, q4, order);
-                return;
-            }
-        }
         hipLaunchKernelGGL((k_tile_rank<PER, MAXT>), dim3(nblk), dim3(kPartThreads), 0, s, q, n, t, tot, tk);
         hipLaunchKernelGGL((k_tile_place<kPlacePer, MAXT>), dim3(nplace), dim3(kPartThreads), 0, s, q, n, t.ntiles, tot,
                            done, tk, q4, order);
     };
     if (n <= (1 << 19)) launch(std::integral_constant<int, PIN_RANK_PER>(), std::integral_constant<int, kMaxTiles>());
     else if (!large) launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTiles>());
-    else if (fused_ok && (n + 8 * kPartThreads - 1) / (8 * kPartThreads) <= kFusedMaxBlocks)
-        // the mapper's 1.68M rows: one launch of <= 256 blocks of 8 queries per thread (the two-launch
-        // form's 820 placement blocks each scanned all 16,384 tile totals)
-        launch(std::integral_constant<int, 8>(), std::integral_constant<int, kMaxTilesLarge>());
     else launch(std::integral_constant<int, 16>(), std::integral_constant<int, kMaxTilesLarge>());
     return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
 }
@@ -1508,12 +1361,6 @@ int pin_query_sort(const PinGrid* grid, const float* q, int64_t n, float* q4, in
     return sort_queries(*grid, q, n, (float4*)q4, (int*)order, workspace, as_stream(stream));
 }
 
-#ifdef PIN_SORT_STAMPS
-int pin_debug_sort_stamps(unsigned long long* host_out) {   // experiment builds only
-    return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_sort_stamps), sizeof(g_sort_stamps)) == hipSuccess ? PIN_OK
-                                                                                                           : PIN_ERR_HIP;
-}
-#endif
 
 int64_t pin_query_sort_stable_workspace_bytes(int64_t n) {
     if (n < 0) return PIN_ERR_ARG;

@@ -31,7 +31,7 @@ import torch.distributed as dist
 from . import _lib
 from .data_sampler import DataSampler
 from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
-from .sharding import all_reduce
+from .sharding import OwnerAdam, all_reduce
 
 # weighted_first with a training decoder: decode each row in the backward on the matrix cores
 # (PIN_TRAIN_ROW_DECODE=0: the f32 VALU decoder backward, for A/B runs)
@@ -61,8 +61,8 @@ CERT_SHIFT = 32
 # launches) unless _randint is replaced on the instance (the tests' replay hook) or
 # Mapper.device_draws is False; PIN_DEVICE_DRAWS=0 turns it off everywhere
 _DEVICE_DRAWS = os.environ.get("PIN_DEVICE_DRAWS", "1") != "0"
-# data-parallel dense loop: the feature gradient's all-reduce in this many row buckets, each
-# stepped by Adam as soon as it is reduced (_allreduce_adam)
+# data-parallel dense loop: the feature gradient reduce-scattered in this many row buckets, each
+# rank's piece of a bucket stepped by Adam as soon as it lands and all-gathered (_owner_adam)
 _AR_BUCKETS = int(os.environ.get("PIN_AR_BUCKETS", "4"))
 
 
@@ -696,13 +696,21 @@ class Mapper:
         fused = (not self.ba_done_flag and "get_batch" not in self.__dict__ and self._pools_fusable())
         dense_loop = fused and (world <= 1 or getattr(self, "shard", "dense") != "space")
         nf, nmg = fdata.numel(), (_lib.MLP_GRAD_SIZE if train_mlp else 0)
+        owner = None
         if dense_loop:
             grads = torch.zeros((nf + nmg,), dtype=torch.float32, device=dev)
-            moments = torch.empty((2 * nf + 2 * nmg,), dtype=torch.float32, device=dev)
-            f_grad, f_m, f_v = grads[:nf].view_as(fdata), moments[:nf].view_as(fdata), moments[nf:2 * nf].view_as(fdata)
+            # data-parallel: reduce-scatter -> Adam on this rank's rows -> all-gather (OwnerAdam),
+            # so the feature moments cover only this rank's rows
+            if world > 1:
+                owner = OwnerAdam(nf, getattr(self, "group", None), _AR_BUCKETS)
+            nfm = owner.moments_size() if owner is not None else nf
+            moments = torch.empty((2 * nfm + 2 * nmg,), dtype=torch.float32, device=dev)
+            f_grad, f_m, f_v = grads[:nf].view_as(fdata), moments[:nfm], moments[nfm:2 * nfm]
+            if owner is None:
+                f_m, f_v = f_m.view_as(fdata), f_v.view_as(fdata)
             m_grad = m_m = m_v = None
             if train_mlp:
-                m_grad, m_m, m_v = grads[nf:], moments[2 * nf:2 * nf + nmg], moments[2 * nf + nmg:]
+                m_grad, m_m, m_v = grads[nf:], moments[2 * nfm:2 * nfm + nmg], moments[2 * nfm + nmg:]
         else:
             state = torch.zeros((3 * nf + 3 * nmg,), dtype=torch.float32, device=dev)
             f_grad, f_m, f_v = (state[k * nf:(k + 1) * nf].view_as(fdata) for k in range(3))
@@ -723,7 +731,8 @@ class Mapper:
         # it reads them
         plan = None
         if fused and part is None:
-            plan = self._dense_loop(iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed)
+            plan = self._dense_loop(iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed,
+                                    owner, grads)
         for _ in range(iter_count if plan is None else 0):
             if fused:
                 index = self._batch_index(slab_rows, slab_new)
@@ -764,7 +773,8 @@ class Mapper:
             self._buf.gather_error.zero_()
             raise IndexError("mapping(): a batch index fell outside the sample pool")
 
-    def _dense_loop(self, iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed):
+    def _dense_loop(self, iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed,
+                    owner=None, grads=None):
         """The iterations of a dense fused mapping() call (utils/mapper.py:443-575): per iteration
         the batch draw (_batch_parts), the gather, forward and backward of a launch plan built
         once (_step_plan) and one pin_adam_step_train launch (the gradient replicas summed, a
@@ -772,7 +782,6 @@ class Mapper:
         the caller's, after the loop -- nothing inside it reads them.  Returns the plan (None
         for no iterations)."""
         c = self.config
-        group = getattr(self, "group", None)
         plan = None
         segs = None
         adam = _lib.fn("pin_adam_step_train")
@@ -813,37 +822,30 @@ class Mapper:
             # leaves them unfilled for this loop)
             st = adam_scalars(c.lr, self._adam_t, c.adam_eps, zero_grad=3 if self._adam_t == 1 else 1)
             if world > 1:
-                self._allreduce_adam(fdata, f_grad, f_m, f_v, m_grad, head, st, group, s)
+                self._owner_adam(owner, fdata, grads, f_m, f_v, m_grad, head, st, s)
             else:
                 _lib.check("pin_adam_step_train", adam(*head, ctypes.byref(st), s))
         return plan
 
-    def _allreduce_adam(self, fdata, f_grad, f_m, f_v, m_grad, head, st, group, s):
-        """The data-parallel step of the dense loop: SUM all-reduce of the
-        per-rank gradients (scaled by 1/W in the backward) and the Adam step, overlapped -- the
-        [L+1, 8] gradient goes out in _AR_BUCKETS row buckets, all enqueued at once on RCCL's
-        stream, and Adam steps bucket b as soon as its all-reduce is done (a stream wait, no host
-        sync) while the later buckets are still on the wire.  The decoder's 833 gradients (a
-        training decoder) are all-reduced first and stepped (and re-packed) by one block of
-        pin_adam_step_train.  Gloo (CPU tests, 1-GPU rehearsals) runs the same buckets in turn."""
-        if m_grad is not None:
-            all_reduce(m_grad, group=group)
-            dec_args = (None, None, None, None, 0, None, 0, None, 0) + head[9:]
-            _lib.check("pin_adam_step_train", _lib.fn("pin_adam_step_train")(*dec_args, ctypes.byref(st), s))
-        n = fdata.numel()
-        flat = [t.view(-1) for t in (fdata, f_grad, f_m, f_v)]
-        nb = max(1, min(_AR_BUCKETS, n // (1 << 16)))
-        edges = [((n * k // nb) // 8) * 8 for k in range(nb)] + [n]
-        nccl = dist.get_backend(group) != "gloo"
-        works = [dist.all_reduce(flat[1][a:b], group=group, async_op=True) if nccl else None
-                 for a, b in zip(edges[:-1], edges[1:])]
+    def _owner_adam(self, owner, fdata, grads, f_m, f_v, m_grad, head, st, s):
+        """The data-parallel step of the dense loop (the reference's
+        optimizer.step(), utils/mapper.py:570-572): the ranks' gradients (scaled by 1/W in the
+        backward) reduce-scattered in row buckets, pin_adam_step on this rank's piece of each
+        bucket as soon as that bucket lands, the stepped piece all-gathered while the later
+        buckets are still on the wire (sharding.OwnerAdam).  The decoder's 833 gradients travel
+        with the few feature rows that do not fill a bucket in one all-reduce; every rank steps
+        (and re-packs) the decoder with one block of pin_adam_step_train."""
         step = _lib.fn("pin_adam_step")
-        for k, (a, b) in enumerate(zip(edges[:-1], edges[1:])):
-            if nccl:
-                works[k].wait()          # the current stream waits for bucket k's all-reduce
-            else:
-                all_reduce(flat[1][a:b], group=group)
-            _lib.check("pin_adam_step", step(*[_lib.ptr(t[a:b]) for t in flat], b - a, ctypes.byref(st), s))
+
+        def adam(p, g, m, v):
+            _lib.check("pin_adam_step", step(_lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), p.numel(),
+                                             ctypes.byref(st), s))
+
+        def decoder():
+            if m_grad is not None:
+                dec_args = (None, None, None, None, 0, None, 0, None, 0) + head[9:]
+                _lib.check("pin_adam_step_train", _lib.fn("pin_adam_step_train")(*dec_args, ctypes.byref(st), s))
+        owner.step(fdata.view(-1), grads, f_m, f_v, adam, decoder)
 
     def _slab_partition(self, world, fused):
         """shard="space" set-up of one mapping() call: (partition, the slab's pool rows, the slab's

@@ -46,6 +46,82 @@ def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
         dist.all_reduce(t, op=op, group=group)
 
 
+class OwnerAdam:
+    """The dense data-parallel optimiser step of SURVEY.md 8e: reduce-scatter of the per-rank
+    feature gradients -> Adam on the rank's own 1/W of the rows -> all-gather of the stepped rows.
+    It replaces the reference's single-process `optimizer.step()` (utils/mapper.py:570-572, Adam
+    from utils/tools.py:89-116) for W ranks that each backpropagated their own batch (loss scaled
+    by 1/W, so the sum over ranks is the gradient of the mean loss of the union of the batches).
+    The wire bytes equal a ring all-reduce's (reduce-scatter + all-gather), the Adam work and the
+    moments are 1/W of the dense step's.
+
+    Layout of the n = 8 (L+1) feature floats: `buckets` contiguous buckets of W pieces of `piece`
+    floats (a multiple of `align`); rank r owns piece r of every bucket, so each bucket is one
+    reduce_scatter_tensor / all_gather_into_tensor on contiguous memory and the buckets pipeline:
+    bucket k's Adam and all-gather are issued while buckets k+1.. are still being reduced.  The
+    rest -- the last n - n_main floats, fewer than buckets * W * align -- travels with the
+    decoder's gradients (contiguous behind the features in the caller's buffer) in one all-reduce
+    and is stepped by every rank alike.
+
+    adam(p, g, m, v, step_state) steps one contiguous piece in place (the HIP pin_adam_step on the
+    GPU, a restatement in the CPU tests: this class only moves data).  Collectives are issued with
+    async_op on every backend, so gloo runs the same sequence RCCL does."""
+
+    def __init__(self, n, group=None, buckets=4, align=64):
+        self.group = group
+        self.world, self.rank = _ranks(group)
+        W = self.world
+        self.n = int(n)
+        nb = max(1, int(buckets))
+        piece = (self.n // (nb * W)) // align * align
+        if piece == 0:   # a map too small to split: everything travels as the all-reduced rest
+            nb = 0
+        self.buckets, self.piece = nb, piece
+        self.n_main = nb * W * piece
+        self.rest = self.n - self.n_main
+
+    def own_slices(self):
+        """(start, end) of this rank's piece of every bucket in the flat feature array."""
+        W, c = self.world, self.piece
+        return [(k * W * c + self.rank * c, k * W * c + (self.rank + 1) * c) for k in range(self.buckets)]
+
+    def moments_size(self):
+        """Floats of this rank's feature moments (m or v): its pieces, then the rest."""
+        return self.buckets * self.piece + self.rest
+
+    def step(self, params, grads, m, v, adam, tail_step=None):
+        """One optimiser step.  params: the flat features [n]; grads: the flat gradient buffer
+        [n + extra] (features, then any tail gradients such as the decoder's, contiguous), this
+        rank's unreduced contribution -- zero again when the call returns; m, v: [moments_size()]
+        moments of this rank's rows; tail_step(): steps the extra tail (e.g. the decoder) once
+        grads[n:] holds its reduced gradient.  Leaves params identical on every rank."""
+        g, W, c = self.group, self.world, self.piece
+        span = W * c
+        own = getattr(self, "_own", None)   # the reduced pieces, kept for the next steps
+        if self.buckets and (own is None or own.device != grads.device or own.dtype != grads.dtype):
+            own = self._own = grads.new_empty((self.buckets, c))
+        rs = [dist.reduce_scatter_tensor(own[k], grads[k * span:(k + 1) * span], group=g, async_op=True)
+              for k in range(self.buckets)]
+        tail = grads[self.n_main:]
+        ar = dist.all_reduce(tail, group=g, async_op=True) if tail.numel() else None
+        ag = []
+        for k, (a, b) in enumerate(self.own_slices()):
+            rs[k].wait()                                  # bucket k reduced: its piece is in own[k]
+            grads[k * span:(k + 1) * span].zero_()        # this rank's contribution consumed
+            adam(params[a:b], own[k], m[k * c:(k + 1) * c], v[k * c:(k + 1) * c])
+            ag.append(dist.all_gather_into_tensor(params[k * span:(k + 1) * span], params[a:b], group=g,
+                                                  async_op=True))
+        if ar is not None:
+            ar.wait()
+            if self.rest:
+                o = self.buckets * c
+                adam(params[self.n_main:], grads[self.n_main:self.n], m[o:], v[o:])
+            if tail_step is not None:
+                tail_step()
+        for w in ag:
+            w.wait()
+
+
 def _factor_pairs(W):
     return [(a, W // a) for a in range(1, W + 1) if W % a == 0]
 

@@ -305,3 +305,86 @@ def test_data_parallel_only_with_an_explicit_group():
         assert (w_none, w_none2, w_group) == (1, 1, 2)
         assert sh_none == (0, 10, 1)
         assert sh_group == ((0, 5, 2) if rank == 0 else (5, 10, 2))
+
+
+# ------------------------------------------------------------------ dense step: owner Adam
+def _adam_ref(p, g, m, v, t, first, lr=0.01, b1=0.9, b2=0.99, eps=1e-15):
+    """torch.optim.Adam's update (utils/tools.py:89-116) on one contiguous piece, in place; the
+    gradient is consumed (zeroed) as pin_adam_step's zero_grad does."""
+    if first:
+        m.zero_()
+        v.zero_()
+    m.mul_(b1).add_(g, alpha=1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    denom = (v.sqrt() / np.sqrt(1 - b2 ** t)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / (1 - b1 ** t))
+    g.zero_()
+
+
+def _rank_grads(n, extra, world, it):
+    gens = [torch.Generator().manual_seed(1000 * it + r) for r in range(world)]
+    return [torch.randn(n + extra, generator=gg, dtype=torch.float64) / world for gg in gens]
+
+
+def _owner_worker(rank, world, port, n, extra, iters, buckets, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pin_slam_amd.sharding import OwnerAdam
+        oa = OwnerAdam(n, None, buckets)
+        params = torch.linspace(-1, 1, n, dtype=torch.float64)
+        dec = torch.zeros(extra, dtype=torch.float64)
+        grads = torch.zeros(n + extra, dtype=torch.float64)
+        m = torch.empty(oa.moments_size(), dtype=torch.float64)
+        v = torch.empty_like(m)
+        dm, dv = torch.empty(extra, dtype=torch.float64), torch.empty(extra, dtype=torch.float64)
+        for it in range(1, iters + 1):
+            grads += _rank_grads(n, extra, world, it)[rank]     # this rank's backward (scaled 1/W)
+            oa.step(params, grads, m, v, lambda p, g, mm, vv: _adam_ref(p, g, mm, vv, it, it == 1),
+                    lambda: _adam_ref(dec, grads[n:], dm, dv, it, it == 1) if extra else None)
+            assert not grads.any(), "the gradient buffer must be consumed"
+        q.put((rank, params.numpy(), dec.numpy(), oa.buckets, oa.rest))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("n,extra,buckets", [(8 * 40001, 833, 4), (8 * 4096, 0, 3), (8 * 7, 5, 4)])
+def test_owner_adam_equals_single_process_adam(world, n, extra, buckets):
+    """Mapper's data-parallel dense step (mapper._owner_adam, sharding.OwnerAdam): reduce-scatter
+    in buckets, Adam on the owned pieces, all-gather (plus the all-reduced rest and decoder tail),
+    three iterations with fresh-moment first step, equals one process summing the ranks'
+    gradients and stepping every element -- and leaves every replica bit-identical.  Sizes: a map
+    whose rows do not fill the buckets evenly (rest + decoder tail), an exact split without a
+    tail, and a map too small to split (everything in the all-reduced rest)."""
+    iters = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, n, extra, iters, buckets, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict((r, (a, b, nb, rest)) for r, a, b, nb, rest in (q.get(timeout=240) for _ in range(world)))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(1, world):
+        np.testing.assert_array_equal(res[0][0], res[r][0])
+        np.testing.assert_array_equal(res[0][1], res[r][1])
+    params = torch.linspace(-1, 1, n, dtype=torch.float64)
+    dec = torch.zeros(extra, dtype=torch.float64)
+    m, v = torch.empty(n + extra, dtype=torch.float64), torch.empty(n + extra, dtype=torch.float64)
+    for it in range(1, iters + 1):
+        g = torch.stack(_rank_grads(n, extra, world, it)).sum(0)
+        _adam_ref(params, g[:n], m[:n], v[:n], it, it == 1)
+        _adam_ref(dec, g[n:], m[n:], v[n:], it, it == 1)
+    np.testing.assert_allclose(res[0][0], params.numpy(), rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(res[0][1], dec.numpy(), rtol=1e-9, atol=1e-12)
+    nb, rest = res[0][2], res[0][3]
+    if n == 8 * 7:
+        assert nb == 0 and rest == n
+    else:
+        assert nb == buckets and rest < buckets * world * 64

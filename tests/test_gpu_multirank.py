@@ -1,7 +1,8 @@
 """Multi-rank Mapper.mapping on the GPU: two ranks share cuda:0 over gloo (as
 tools/rehearse_multi.sh does; the scaling run uses one rank per GPU over RCCL) and run the
-whole fused mapping() call end to end with shard="dense" (SUM all-reduce of the feature /
-decoder gradients) and shard="space" (slab ownership, halo exchange, shared row, Adam on owned
+whole fused mapping() call end to end with shard="dense" (the feature gradient reduce-scattered,
+Adam on each rank's rows, the rows all-gathered -- sharding.OwnerAdam; the decoder's gradients
+all-reduced) and shard="space" (slab ownership, halo exchange, shared row, Adam on owned
 rows, all-gather of the owned rows).
 
 Oracle: one process on the union of the same batches.  Every train_step of each rank is
@@ -148,7 +149,9 @@ def _norm(a):
     return float(np.linalg.norm(np.asarray(a, dtype=np.float64).ravel()))
 
 
-@pytest.mark.parametrize("case,shard,world,layout", [("mapping_wf", "dense", 2, "auto"), ("mapping_wf", "space", 2, "auto"),
+@pytest.mark.parametrize("case,shard,world,layout", [("mapping_wf", "dense", 2, "auto"), ("mapping_wf", "dense", 4, "auto"),
+                                                     ("mapping_nwf_weighted", "dense", 2, "auto"),
+                                                     ("mapping_wf", "space", 2, "auto"),
                                                      ("mapping_wf_frozen", "space", 2, "auto"),
                                                      ("mapping_nwf_weighted", "space", 2, "auto"),
                                                      ("mapping_wf", "space", 4, (2, 2)),

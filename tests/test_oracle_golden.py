@@ -237,3 +237,47 @@ def test_torch_cpu_mapping_iteration(golden, case):
     np.testing.assert_allclose(feats.grad.numpy(), z["it0_feat_grad"], rtol=1e-4, atol=1e-8)
     for key, p in zip(("W1", "b1", "W2", "b2"), mlp.params):
         np.testing.assert_allclose(p.grad.numpy(), z[f"it0_grad_{key}"].reshape(p.shape), rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("case", ["tracker_wf", "tracker_nwf"])
+def test_torch_cpu_registration_step(golden, case):
+    """bench.py's tracker CPU baseline (pin_torch_cpu.registration_step): the reference's query
+    (SDF 1e-6, gradient, IDW std), its valid-point count and its pose increment
+    (utils/tracker.py:277-520)."""
+    import torch
+    from oracle import pin_torch_cpu as T
+    z = golden(case)
+    m, _ = _torch_map(z, 1)
+    mlp = T.TorchMLP(z["dec_W1"], z["dec_b1"], z["dec_W2"], z["dec_b2"], float(z["dec_sdf_scale"]))
+    src = torch.from_numpy(z["source"])
+    sdf, grad, nn, std = T.sdf_grad_std(m, mlp, src)
+    np.testing.assert_allclose(sdf.numpy(), z["sdf"], atol=1e-6)
+    np.testing.assert_allclose(grad.numpy(), z["grad"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(std.numpy(), z["sdf_std"], rtol=1e-4, atol=1e-6)
+    k = int(z["nn_k"])
+    np.testing.assert_array_equal((nn >= k).numpy(), z["mask"])
+    max_std = float(z["surface_sample_range_m"]) * float(z["max_sdf_std_ratio"])
+    t, cnt = T.registration_step(m, mlp, src, torch.zeros(src.shape[0]), float(z["reg_min_grad_norm"]),
+                                 float(z["reg_max_grad_norm"]), float(z["reg_GM_dist_m"]), float(z["reg_GM_grad"]),
+                                 float(z["reg_lm_lambda"]), max_std, k)
+    assert cnt == int(z["valid_count"])
+    dT = z["delta_T"]
+    np.testing.assert_allclose(t[3:].numpy(), dT[:3, 3], atol=2e-6)
+    w = t[:3].numpy()
+    th = np.linalg.norm(w)
+    K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]]) / max(th, 1e-30)
+    R = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K    # utils/tools.py expmap (Rodrigues)
+    np.testing.assert_allclose(R, dT[:3, :3], atol=2e-6)
+
+
+def test_torch_cpu_mesher_batch(golden):
+    """bench.py's mesher CPU baseline (pin_torch_cpu.sdf_only): the reference's query_points SDF
+    and marching-cubes mask (utils/mesher.py:41-136)."""
+    import torch
+    from oracle import pin_torch_cpu as T
+    z = golden("mesher_wf")
+    m, _ = _torch_map(z, 0)
+    mlp = T.TorchMLP(z["dec_W1"], z["dec_b1"], z["dec_W2"], z["dec_b2"], float(z["dec_sdf_scale"]))
+    sdf, mask = T.sdf_only(m, mlp, torch.from_numpy(z["coord"]), int(z["mesh_min_nn"]))
+    np.testing.assert_array_equal(mask.numpy(), z["mc_mask"])
+    np.testing.assert_allclose(sdf.numpy(), z["sdf"], atol=1e-6)
