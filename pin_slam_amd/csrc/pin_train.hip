@@ -1085,6 +1085,12 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
 #ifndef PIN_SCAT_SORT
 #define PIN_SCAT_SORT 1   // 0: the unsorted scatter for every batch (A/B builds)
 #endif
+#ifndef PIN_NWF_SORT
+#define PIN_NWF_SORT 1    // 0: the per-neighbour mask backward scatters per wave, unsorted (A/B builds)
+#endif
+// the per-neighbour mask path reads the ReLU masks the forward's f32 decode saves: the row-wise
+// experiment decoder (mlp_sdf_rows) does not produce them
+static_assert(PIN_MLP_ROWS == 0, "PIN_MLP_ROWS builds lack the ReLU masks of the PIN_TRAIN_DX per-neighbour path");
 
 // The same scatter with the block's (row, neighbour) pairs pre-summed per feature row: the pairs
 // are radix-sorted by id in LDS (rocprim block sort, ceil(log2 rows) bits, stable), each run of
@@ -1479,6 +1485,183 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
 #endif
     if (side && !side_done) train_side_effects(c, st, row0, nrow_blk, row, s_pair);
 }
+
+// Per-neighbour (weighted_first False) backward of a frozen decoder, large batches: the feature
+// terms pre-summed per feature row over the block's (row, neighbour) pairs before the atomics.
+// Each pair's term is dL/dsdf_row * w_j * s dsdf_j/dx[0:8], where dsdf_j/dx comes from neighbour
+// j's ReLU mask (saved by the forward) through GEMM2 of the matrix-core decoder.  Instead of
+// staging the 2,048 pairs' 32-B terms (64 KB of LDS, one block per CU), the block
+//   1. stages only the pairs' ids and weights (coalesced loads, 16 KB),
+//   2. radix-sorts the pairs by feature row (rocprim block sort, stable: a run keeps input order),
+//   3. evaluates the terms in SORTED order -- 256 pairs per round, each wave's 64 consecutive
+//      sorted pairs through one mlp_grad8_from_mask (mask gathered by the pair's index) -- so the
+//      pairs of a feature row sit in consecutive lanes: a segmented sum over equal ids (six
+//      shuffle steps) leaves each run's total in its last lane, and the runs' totals leave as
+//      8 lanes x 32 contiguous bytes per run (the direct scatter's request shape);
+//   4. applies the training side effects on the same runs (one certainty add of the run's weight
+//      sum, one ts max), as feature_scatter_sorted does.
+// A run cut by a wave or round boundary adds its pieces separately (same sum, one more atomic).
+// LDS: 8.3 KB decoder image + 16 KB pairs + the sort storage shared with the waves' decoder
+// scratch + 4 KB positions -- three blocks per CU.
+__global__ void __launch_bounds__(kTBlock)
+k_train_backward_nwf_sorted(const PinPoints p, const PinMlp m, const float* __restrict__ label, PinTrainCfg c,
+                            PinTrainState st, float* __restrict__ grad_features, double* __restrict__ loss_part) {
+    constexpr int kP = kTBlock * kK;
+    static_assert(kP <= 65536, "sorted positions are 16-bit");
+    using Sort = rocprim::block_radix_sort<unsigned, kTBlock, kK, unsigned short>;
+    __shared__ uint4 s_pk[kPkBytes / 16];
+    __shared__ union {
+        typename Sort::storage_type sort;
+        float xs[kWaves][kXsWave];              // mlp_grad8_from_mask's scratch, then the runs' totals
+    } s_u;
+    __shared__ int s_key[kP];                   // the pairs' ids; after the sort: the id at each position
+    __shared__ float s_wt[kP];
+    __shared__ unsigned short s_val[kP];        // sorted position -> pair index
+    __shared__ float s_dsdf[kTBlock];
+    __shared__ int64_t s_rts[kTBlock];
+    __shared__ unsigned s_last[kTBlock];
+    __shared__ int s_end;
+    for (int e = threadIdx.x; e < kPkBytes / 16; e += kTBlock) s_pk[e] = ((const uint4*)m.packed)[e];
+    const int nn_k = c.nn_k;
+    const int64_t nrows = c.n_main + 6 * c.n_stencil;
+    const int64_t row0 = (int64_t)blockIdx.x * kTBlock;
+    const int nrow_blk = (int)(nrows - row0 < kTBlock ? nrows - row0 : kTBlock);
+    const int npair = nrow_blk * nn_k;
+    const int64_t r = row0 + threadIdx.x;
+    const bool live = r < nrows;
+    const int64_t row = !live ? r : st.sorted_rows ? (int64_t)__float_as_int(((const float4*)st.sorted_rows)[r].w)
+                                  : st.order ? st.order[r] : r;
+    double loss = 0.0;
+    const float rs = live ? row_scale(c, row) : 0.f;
+    const float dsdf = live ? row_dsdf(c, st.sdf, label, st.row_weight, row, loss) * rs : 0.f;
+    loss *= (double)rs;
+    {
+        double t = loss;
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if ((threadIdx.x & 63) == 0 && loss_part) loss_part[(int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)] = t;
+    }
+    int64_t* const ts_update = st.row_ts ? st.ts_update : nullptr;
+    const bool side = st.certainties || st.cert_fixed || ts_update;
+    s_dsdf[threadIdx.x] = dsdf;
+    s_rts[threadIdx.x] = (ts_update && live && row < c.n_main) ? st.row_ts[row] : -1;
+    for (int e = threadIdx.x; e < npair; e += kTBlock) {
+        s_key[e] = st.ids[row0 * nn_k + e];
+        s_wt[e] = st.weights[row0 * nn_k + e];
+    }
+    if (threadIdx.x == 0) s_end = kP;
+    __syncthreads();
+    // ---- sort the pairs by feature row (as feature_scatter_sorted)
+    const int64_t frows = p.rows;
+    const unsigned bits = frows >= (int64_t)0x80000000u ? 32u : 32u - (unsigned)__clz((unsigned)frows);
+    const unsigned inval = bits >= 32u ? ~0u : (1u << bits) - 1u;
+    unsigned keys[kK];
+    unsigned short vals[kK];
+#pragma unroll
+    for (int i = 0; i < kK; ++i) {
+        const int pidx = threadIdx.x * kK + i;
+        const int id = pidx < npair ? s_key[pidx] : -1;
+        keys[i] = id < 0 ? inval : (unsigned)id;
+        vals[i] = (unsigned short)pidx;
+    }
+    Sort().sort(keys, vals, s_u.sort, 0, bits);
+    s_last[threadIdx.x] = keys[kK - 1];
+    __syncthreads();   // the sort's storage is free, s_last written, every s_key read
+    const unsigned prev = threadIdx.x == 0 ? ~0u : s_last[threadIdx.x - 1];
+#pragma unroll
+    for (int i = 0; i < kK; ++i) {
+        const int pos = threadIdx.x * kK + i;
+        const unsigned pk = i == 0 ? prev : keys[i - 1];
+        if (keys[i] == inval && pk != inval) s_end = pos;   // one thread: the transition
+        s_val[pos] = vals[i];
+        s_key[pos] = (int)keys[i];
+    }
+    __syncthreads();   // positions and s_end visible; the sort's storage is free (decoder scratch)
+    const int end = s_end;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long* const fdst = (grad_features && st.grad_fixed) ? (unsigned long long*)st.grad_fixed : nullptr;
+    const double fscale = fixed_scale(st.fixed_shift);
+    if (grad_features) {
+        const MlpW mw{nullptr, m.sdf_scale, s_u.xs[wave], (const unsigned char*)s_pk};
+        const uint2* masks = (const uint2*)st.x + row0 * nn_k;
+        const int rounds = (end + kTBlock - 1) / kTBlock;   // block-uniform
+        for (int u = 0; u < rounds; ++u) {
+            const int pos = u * kTBlock + threadIdx.x;
+            const bool ok = pos < end;
+            int key = -1;
+            float coef = 0.f;
+            uint64_t mk = 0;
+            if (ok) {
+                const int pidx = s_val[pos];
+                key = s_key[pos];
+                coef = s_dsdf[pidx / nn_k] * s_wt[pidx];
+                const uint2 mv = masks[pidx];
+                mk = ((uint64_t)mv.y << 32) | mv.x;
+            }
+            float g[kF];
+            if (__any(ok)) {   // wave-uniform: the wave's 64 positions decode together
+                float g8[kF];
+                mlp_grad8_from_mask(mw, mk, g8);
+#pragma unroll
+                for (int d = 0; d < kF; ++d) g[d] = coef * g8[d];
+                // segmented inclusive sum over lanes of equal id (equal ids are consecutive)
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int ku = __shfl_up(key, o);
+                    const bool add = lane >= o && ku == key;
+#pragma unroll
+                    for (int d = 0; d < kF; ++d) {
+                        const float v = __shfl_up(g[d], o);
+                        g[d] = add ? g[d] + v : g[d];
+                    }
+                }
+                const int kn = __shfl_down(key, 1);
+                const bool tail = ok && (lane == 63 || kn != key);
+                // the runs' totals, compacted into the wave's scratch: 8 lanes x 32 B per run
+                const uint64_t tails = __ballot(tail);
+                const int nt = __popcll(tails);
+                float* const ws = s_u.xs[wave];
+                int* const wid = (int*)(ws + 64 * kF);
+                if (tail) {
+                    const int slot = __popcll(tails & ((1ull << lane) - 1ull));
+#pragma unroll
+                    for (int d = 0; d < kF; ++d) ws[slot * kF + d] = g[d];
+                    wid[slot] = key;
+                }
+                wave_lds_sync();
+                for (int e = lane; e < nt * kF; e += 64) {
+                    const int rid = wid[e >> 3];
+                    if (fdst) atomicAdd(fdst + (int64_t)rid * kF + (e & (kF - 1)), to_fixed(ws[e], fscale));
+                    else atomicAdd(grad_features + (int64_t)rid * kF + (e & (kF - 1)), ws[e]);
+                }
+                wave_lds_sync();   // the next round's decode reuses the scratch
+            }
+        }
+    }
+    if (!side) return;
+    float* const cert = st.cert_fixed ? nullptr : st.certainties;
+    unsigned long long* const cfix = (unsigned long long*)st.cert_fixed;
+    const double cscale = fixed_scale(st.cert_shift);
+    // one thread per run: the run starts where the sorted id changes
+    for (int a = threadIdx.x; a < end; a += kTBlock) {
+        const int id = s_key[a];
+        if (a > 0 && s_key[a - 1] == id) continue;
+        float wsum = 0.f;
+        unsigned long long fsum = 0ull;
+        int64_t tmax = -1;
+        for (int q = a; q < end && s_key[q] == id; ++q) {
+            const int pidx = s_val[q];
+            const float w = s_wt[pidx];
+            wsum += w;
+            if (cfix) fsum += to_fixed(w, cscale);
+            const int64_t t = s_rts[pidx / nn_k];
+            tmax = t > tmax ? t : tmax;
+        }
+        if (cert) atomicAdd(cert + id, wsum);
+        if (cfix) atomicAdd(cfix + id, fsum);
+        if (ts_update && tmax >= 0) ts_amax(ts_update, id, tmax);
+    }
+}
+static_assert(kXsWave >= 64 * (kF + 1), "a wave's run totals (8 floats + id per lane) must fit its decoder scratch");
 
 // out[i] += float(sum of the nrep fixed-point accumulators at i * 2^-shift); the accumulators are
 // zeroed (pin_fixed_accumulate, and the deterministic pin_train_backward with replica_mode 0)
@@ -2157,7 +2340,10 @@ int pin_train_forward(const PinHash* hash, const PinGrid* grid, const PinPoints*
     if (cfg->nn_k < 1 || cfg->nn_k > kK) return PIN_ERR_UNSUPPORTED;
     const int64_t rows = cfg->n_main + 6 * cfg->n_stencil;
     const bool dx = (cfg->flags & PIN_TRAIN_DX) != 0;
-    if (dx && cfg->weighted_first && !mlp->packed) return PIN_ERR_ARG;
+    // PIN_TRAIN_DX needs the matrix-core image in both decoding modes: the backward takes each
+    // row's (weighted_first) or each neighbour's (masks) input gradient from it -- rejected here,
+    // before the forward overwrites st.x, as pin_train_backward would reject it after
+    if (dx && !mlp->packed) return PIN_ERR_ARG;
     const bool eik = (cfg->flags & PIN_TRAIN_EIK) != 0;
     if (eik && (dx || cfg->n_stencil != 0 || !st->eik_coef || !st->eik_vec)) return PIN_ERR_ARG;
     if (rows == 0) return PIN_OK;
@@ -2269,6 +2455,9 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         else if (cfg->weighted_first)
             hipLaunchKernelGGL((k_train_backward<true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg,
                                *st, grad_features, mpart, lpart);
+        else if (sorted && PIN_NWF_SORT)   // per-neighbour masks, runs pre-summed in sorted order
+            hipLaunchKernelGGL(k_train_backward_nwf_sorted, g, dim3(kTBlock), 0, s, *pts, *mlp, label, *cfg, *st,
+                               grad_features, lpart);
         else
             hipLaunchKernelGGL((k_train_backward<false, false, true, false, true>), g, dim3(kTBlock), 0, s, *pts, *mlp,
                                label, *cfg, *st, grad_features, mpart, lpart);

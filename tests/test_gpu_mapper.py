@@ -250,6 +250,40 @@ def test_nwf_mask_backward_matches_redecode(dev, backend, monkeypatch):
     np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("det", [False, True])
+def test_nwf_sorted_backward_matches_wave_scatter(dev, det, monkeypatch):
+    """Per-neighbour decoding, frozen decoder, a batch that scatters straight into the gradient
+    (no replicas): k_train_backward_nwf_sorted -- the block's pairs sorted by feature row, each
+    pair's term evaluated in sorted order and the runs pre-summed before the atomics, side effects
+    on the runs -- against the per-wave unsorted scatter of the same forward (the replica path,
+    summed): the same loss / sdf / ts bitwise, feature gradients and certainties to float-sum
+    reordering.  det: the fixed-point mode -- two sorted calls bitwise equal."""
+    import pin_slam_amd.mapper as M
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    res = []
+    for sorted_ in (False, True, True):
+        # replicas (small-batch path, unsorted scatter) or none (the sorted kernel)
+        monkeypatch.setattr(M, "_REPLICA_ROWS", 0 if sorted_ else 1 << 30)
+        nm, dec, pts = surface_map(300, device=dev, weighted_first=False, buffer_size=1 << 22, query_backend="grid")
+        for p in dec.parameters():
+            p.requires_grad_(False)
+        coord, label, ts = surface_pool(pts, 70001, device=dev)
+        ts = torch.randint(0, 5, ts.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+        mapper = P.Mapper(nm.config, None, nm, dec, deterministic=det)
+        fg = torch.zeros_like(nm.local_geo_features.data)
+        loss = float(mapper.train_step(coord, label, ts, fg, None))
+        res.append((loss, mapper.last_sdf.clone(), fg, nm.local_point_certainties.clone(),
+                    nm.local_point_ts_update.clone()))
+    (l0, s0, f0, c0, t0), (l1, s1, f1, c1, t1), (l2, s2, f2, c2, t2) = res
+    assert torch.equal(s0, s1) and torch.equal(t0, t1)
+    assert l1 == pytest.approx(l0, rel=1e-9)
+    scale = float(f0.abs().max())
+    np.testing.assert_allclose(_np(f1), _np(f0), rtol=1e-5, atol=1e-6 * scale)
+    np.testing.assert_allclose(_np(c1), _np(c0), rtol=1e-5, atol=1e-5)
+    if det:
+        assert torch.equal(f1, f2) and torch.equal(c1, c2) and torch.equal(t1, t2)
+
+
 def test_frozen_decoder_trains_features_only(golden, dev):
     """Decoder frozen (freeze_model, utils/tools.py:186-191, after freeze_after_frame): the
     decoder parameters stay bit-identical and the features still move."""
