@@ -589,10 +589,10 @@ def mesher_kernel_roofline(nm, dec, coord):
     algo = n_occ * b_occ + (n - n_occ) * b_empty
     achieved = algo / (kern_ms * 1e-3)
     kernel = query_kernel_name("grid", wf, want_grad=False)
-    per_launch = measured_traffic(kernel, os.path.join("profiles", "r06", "mesher_traffic.json"))
+    per_launch = measured_traffic(kernel)
     return {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
-            "traffic": per_launch, "traffic_source": "profiles/r06/mesher_traffic.json (per 2^20-query launch)",
+            "traffic": per_launch, "traffic_source": TRAFFIC_FILE + " (per 2^20-query launch)",
             "kernel": kernel, "kernel_ms_per_grid": kern_ms, "launches": len(spans),
             "queries_with_neighbours": n_occ, "queries_empty": n - n_occ,
             "algorithmic_bytes": {"with_neighbours": b_occ, "empty": b_empty, "per_grid": algo,
@@ -991,11 +991,13 @@ def mapper_leg(args, dev, world, rank, wf=None, shard=None):
 def mapper_iter_kernels(wf):
     """The kernels one mapper iteration launches once each (gather, tile sort of the rows, forward,
     backward, loss reduction, Adam); their PMC bytes per launch summed are the iteration's
-    traffic.  The forward / backward instances carry weighted_first as their first template
-    argument; the others are shared by both decoding modes (same sizes)."""
+    traffic.  The forward instances carry weighted_first as their first template argument, the
+    per-neighbour backward is k_train_backward_nwf_sorted; the others are shared by both decoding
+    modes (same sizes)."""
     w = str(bool(wf)).lower()
+    bwd = "k_train_backward<true," if wf else "k_train_backward_nwf_sorted"
     return ("k_train_gather_packed", "k_tile_rank<16, 16384>", "k_tile_place<2, 16384>",
-            f"k_train_forward_grid<{w},", f"k_train_backward<{w},", "k_loss_final", "k_adam_train")
+            f"k_train_forward_grid<{w},", bwd, "k_loss_final", "k_adam_train")
 
 
 def mapper_traffic(wf):
