@@ -488,17 +488,24 @@ class Mapper:
         k = keep.shape[0]
         keep = keep.contiguous()
         outs, arrays = [], []
+        # every source the launches read stays referenced until they are queued: a contiguous()
+        # copy of a non-contiguous pool held only by the loop variable would go back to the caching
+        # allocator at the next iteration, which could hand its block to the next spare before the
+        # gather has read it
+        srcs = []
         for name, cur in pools:
             out = self._pool_compact_target(name, cur, k)
             outs.append(out)
             if k > 0 and cur.numel() > 0:
                 cur = cur.contiguous()
+                srcs.append(cur)
                 arrays.append(_lib.PinRowArray(cur.data_ptr(), out.data_ptr(),
                                                cur.numel() // cur.shape[0] * cur.element_size()))
         for i in range(0, len(arrays), _lib.ROW_ARRAYS_MAX):
             chunk = arrays[i:i + _lib.ROW_ARRAYS_MAX]
             arr = (_lib.PinRowArray * len(chunk))(*chunk)
             _lib.call("pin_gather_rows", arr, len(chunk), _lib.ptr(keep), k, _lib.stream())
+        del srcs   # the launches are queued (stream order keeps a freed block from reuse before them)
         return outs
 
     def _pool_compact(self, name, cur, keep):
@@ -676,6 +683,7 @@ class Mapper:
 
     def mapping(self, iter_count):
         """utils/mapper.py:425-593 (iteration body :443-575)."""
+        self.check_deferred()
         if self.train_less:
             iter_count = max(1, iter_count - 5)
         self._check_supported()
@@ -769,9 +777,31 @@ class Mapper:
             sync_side_effects(cert_delta, nm.local_point_ts_update, getattr(self, "group", None))
             cert.copy_(cert_before + cert_delta)
         nm.assign_local_to_global()
-        if fused and iter_count > 0 and int(self._buf.gather_error.item()):
-            self._buf.gather_error.zero_()
-            raise IndexError("mapping(): a batch index fell outside the sample pool")
+        if fused and iter_count > 0:
+            if getattr(self, "defer_checks", False):
+                # the flag leaves with an asynchronous copy; the next call reads it (its event has
+                # completed by then), so the host does not wait here for the whole call's kernels
+                flag = self.__dict__.get("_gather_flag_host")
+                if flag is None:
+                    flag = self._gather_flag_host = torch.zeros((1,), dtype=self._buf.gather_error.dtype,
+                                                                pin_memory=True)
+                flag.copy_(self._buf.gather_error.view(-1)[:1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._pending_gather_check = ev
+            elif int(self._buf.gather_error.item()):
+                self._buf.gather_error.zero_()
+                raise IndexError("mapping(): a batch index fell outside the sample pool")
+
+    def check_deferred(self):
+        """The device-side batch check of the last mapping() call made with defer_checks (raises
+        what that call would have raised)."""
+        ev = self.__dict__.pop("_pending_gather_check", None)
+        if ev is not None:
+            ev.synchronize()
+            if int(self._gather_flag_host[0]):
+                self._buf.gather_error.zero_()
+                raise IndexError("mapping(): a batch index fell outside the sample pool")
 
     def _dense_loop(self, iter_count, world, fdata, f_grad, f_m, f_v, mlp_params, m_grad, m_m, m_v, packed,
                     owner=None, grads=None):

@@ -70,10 +70,11 @@ _MAP_WS = {}
 
 
 def map_workspace(n: int, device) -> torch.Tensor:
-    """Device workspace of the map-maintenance kernels for n elements (grown, reused per device;
-    the calls are stream-ordered, so reuse across calls on one stream is safe)."""
+    """Device workspace of the map-maintenance kernels for n elements (grown, reused per device
+    and stream: the calls are stream-ordered, so reuse across calls on one stream is safe, and a
+    call on another stream -- FrameLoop's next-scan preprocessing -- has a buffer of its own)."""
     need = _lib.map_workspace_bytes(max(int(n), 1))
-    key = str(device)
+    key = (str(device), _lib.stream(device).value)
     buf = _MAP_WS.get(key)
     if buf is None or buf.numel() < need:
         buf = torch.empty((need,), dtype=torch.uint8, device=device)
@@ -656,6 +657,32 @@ class NeuralPoints(nn.Module):
         self.local_orientation = sensor_orientation
         self._local_rows = (self.local_mask, rows[:L])
         self._local_snapshot = self._snapshot()
+
+    # derived state rebuilt on demand: weak references, capacity buffers and views keyed on tensor
+    # identity, none of which pickles (weakref) or means anything in another process
+    _TRANSIENT = ("_cache", "_nbhd_cache", "_grid_box", "_table_trust", "_grid_view_cache", "_row_bufs",
+                  "_local_snapshot", "_local_rows", "_view_cache")
+
+    def __getstate__(self):
+        """Pickling (the reference's save_implicit_map, utils/tools.py:224-238, torch.saves the
+        NeuralPoints object itself): the map without its transient caches, and every array that is
+        a prefix view of a capacity buffer (_append_rows) saved as its own rows only."""
+        state = dict(self.__dict__)
+        for k in self._TRANSIENT:
+            state.pop(k, None)
+        state["_cache"] = {}
+
+        def own(t):
+            if isinstance(t, torch.Tensor) and t.untyped_storage().nbytes() != t.numel() * t.element_size():
+                c = t.detach().clone()
+                return nn.Parameter(c, requires_grad=t.requires_grad) if isinstance(t, nn.Parameter) else c
+            return t
+        for k, v in list(state.items()):
+            state[k] = own(v)
+        for group in ("_parameters", "_buffers"):
+            if group in state:
+                state[group] = {k: own(v) for k, v in state[group].items()}
+        return state
 
     def _snapshot(self):
         """Identity + version of the position / orientation tensors right after reset_local_map:

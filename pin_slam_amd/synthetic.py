@@ -268,15 +268,53 @@ class FrameLoop:
         self.gt_pose_provided = False
         mapper.dataset = self
 
-    def read_and_preprocess(self, pts):
+    def _clouds(self, pts, want_source):
+        """The scan's own preprocessing (slam_dataset.py:260-345): voxel down-sample, crop and --
+        after frame 0 -- the registration's source down-sample.  A function of the scan alone."""
         from .neural_points import voxel_down_sample
         c = self.config
-        self.cur_pose_ref = np.eye(4)
-        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
         cloud = pts[voxel_down_sample(pts, c.vox_down_m)]                 # slam_dataset.py:286
         dist = torch.norm(cloud, dim=1)                                    # crop_frame, :827-834
         keep = (dist > c.min_range) & (dist < c.max_range) & (cloud[:, 2] > c.min_z) & (cloud[:, 2] < c.max_z)
-        self.cur_point_cloud_torch = cloud[keep]
+        cloud = cloud[keep]
+        src = cloud[voxel_down_sample(cloud, c.source_vox_down_m)] if want_source else None
+        return cloud, src
+
+    def prefetch(self, pts, ready=None):
+        """Preprocess the NEXT scan on a side stream while the device works through this frame's
+        mapping (its host syncs then wait for the side stream only): the scan's preprocessing does
+        not depend on the map, so read_and_preprocess of that scan only picks the result up.  The
+        outputs are the same tensors, bitwise, as preprocessing it in turn."""
+        if self.__dict__.get("_side") is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        main = torch.cuda.current_stream(self.dev)
+        # the scan was produced before ``ready`` (an event of the main stream recorded when the
+        # scan was handed over): waiting for it, and not for everything queued since (this
+        # frame's mapping), keeps the side stream beside the mapping kernels
+        if ready is not None:
+            self._side.wait_event(ready)
+        else:
+            self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            cloud, src = self._clouds(pts, True)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        for t in (cloud, src):          # allocated on the side stream, read on the main one
+            if t is not None:
+                t.record_stream(main)
+        self._prefetched = (pts, cloud, src, done)
+
+    def read_and_preprocess(self, pts):
+        c = self.config
+        self.cur_pose_ref = np.eye(4)
+        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
+        pre = self.__dict__.pop("_prefetched", None)
+        if pre is not None and pre[0] is pts:
+            torch.cuda.current_stream(self.dev).wait_event(pre[3])
+            cloud, src = pre[1], pre[2]
+        else:
+            cloud, src = self._clouds(pts, self.processed_frame > 0)
+        self.cur_point_cloud_torch = cloud
         self.cur_source_points = None
         if self.processed_frame == 0:
             self.odom_poses.append(self.cur_pose_ref)
@@ -286,8 +324,7 @@ class FrameLoop:
             guess = self.last_pose_ref @ self.last_odom_tran if (c.uniform_motion_on and not self.lose_track) \
                 else self.last_pose_ref
             self.cur_pose_guess_torch = torch.tensor(guess, dtype=torch.float64, device=self.dev)
-            src = self.cur_point_cloud_torch
-            self.cur_source_points = src[voxel_down_sample(src, c.source_vox_down_m)]
+            self.cur_source_points = src
 
     def update_odom_pose(self, cur_pose_torch):
         """dataset/slam_dataset.py:376-430."""
@@ -306,11 +343,18 @@ class FrameLoop:
         self.travel_dist.append(self.travel_dist[-1] + step)
         self.last_pose_ref = self.cur_pose_ref
 
-    def frame(self, pts, draws=None, timer=None):
-        """One frame of the loop; timer(name) (optional) is called at each part's end."""
+    def frame(self, pts, draws=None, timer=None, next_pts=None):
+        """One frame of the loop; timer(name) (optional) is called at each part's end.  next_pts
+        (optional): the next scan, preprocessed on a side stream while this frame's mapping runs
+        (prefetch); its mapping() leaves the device-side batch check to the next call
+        (Mapper.defer_checks), so the host is free for that while the device maps."""
         c, nm, mapper = self.config, self.nm, self.mapper
         mark = timer or (lambda name: None)
         used = self.processed_frame
+        handed = None
+        if next_pts is not None:   # everything that produced next_pts is queued before this point
+            handed = torch.cuda.Event()
+            handed.record()
         self.read_and_preprocess(pts)
         mark("preprocess")
         if self.build_index and used > 0 and nm.backend() == "grid":
@@ -335,7 +379,10 @@ class FrameLoop:
             for p in self.dec.parameters():
                 p.requires_grad_(False)
         if used % c.mapping_freq_frame == 0:
+            mapper.defer_checks = next_pts is not None
             mapper.mapping(iters)
+        if next_pts is not None:
+            self.prefetch(next_pts, handed)
         mark("mapping")
         self.processed_frame += 1
         return valid

@@ -16,6 +16,7 @@ Runs ONLY in the build container (imports /root/reference through gen_golden).
 Usage:
   PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_slam_envelope.py run slam_seq 4 [rep]
   PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_slam_envelope.py combine slam_seq
+  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_slam_envelope.py forced slam_seq 1
 """
 import glob
 import os
@@ -25,6 +26,7 @@ import time
 import numpy as np
 
 RUN_DIR = os.environ.get("PIN_ENV_DIR", "/tmp/slam_env")
+DUMP = {int(v) for v in os.environ.get("DUMP", "").split(",") if v}   # run_forced: frames whose state is saved
 CASES = {"slam_seq": dict(frames=30, scene="street"), "slam_seq100": dict(frames=100, scene="long")}
 # per-run arrays kept in the envelope (everything else of a run must equal the stored run's)
 PER_RUN = ("hist_pose", "hist_map_count", "hist_local_count", "hist_pool", "hist_new", "f0_surface_sdf",
@@ -49,6 +51,93 @@ def run(name, threads, rep=0):
     keep["torch_version"] = np.asarray(torch.__version__)
     np.savez_compressed(os.path.join(RUN_DIR, f"{name}_t{threads}_r{rep}.npz"), **keep)
     print(name, threads, "threads done in", round(time.time() - t0, 1), "s", flush=True)
+
+
+def run_forced(name, threads):
+    """The reference's frame loop at `threads` torch threads with the tracking RESULT replaced by
+    the stored run's pose of each frame (pose forcing; tools/slam_forced.py is the same on the
+    drop-in classes): the map is then built from the stored trajectory, and the reference's own
+    tracker, still run every frame from the stored run's guess, shows how far a second reference
+    run lands from the stored pose on a map that differs only by its reduction order.  Writes
+    RUN_DIR/<name>_forced_t<threads>.npz with the per-frame tracked poses."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import types
+    import torch
+    import gen_golden as G
+    import dataset.slam_dataset as rds_mod
+    import utils.data_sampler as rds
+    z = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{name}.npz"), allow_pickle=False))
+    c = CASES[name]
+    frames = c["frames"]
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(21)
+    scene, poses = G.sequence_scene(c["scene"], rng, frames)
+    scans = [G.lidar_scan(T, scene, rng) for T in poses]
+    cfg = G.slam_config()
+    replay = G.ReplayDraws(2024)
+    rt = G._ReplayTorch(replay)
+    saved = (rds.torch, G.rmapper.torch)
+    rds.torch = rt
+    G.rmapper.torch = rt
+    rds_mod.get_time = time.time
+    tracked = []
+    try:
+        torch.manual_seed(42)
+        geo_mlp = G.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1)
+        npm = G.NeuralPoints(cfg)
+        ds = types.SimpleNamespace(config=cfg, silence=True, dtype=cfg.dtype, device="cpu", gt_pose_provided=False,
+                                   odom_poses=[], pgo_poses=None, gt_poses=None, travel_dist=[], processed_frame=0,
+                                   lose_track=False, consecutive_lose_track_frame=0, last_pose_ref=np.eye(4),
+                                   last_odom_tran=np.eye(4), cur_pose_ref=np.eye(4), stop_count=0, stop_status=False,
+                                   cur_point_cloud_torch=None, cur_point_ts_torch=None, cur_sem_labels_torch=None,
+                                   cur_source_points=None, cur_source_normals=None, cur_source_colors=None)
+        preprocess = types.MethodType(rds_mod.SLAMDataset.preprocess_frame, ds)
+        update_odom = types.MethodType(rds_mod.SLAMDataset.update_odom_pose, ds)
+        tracker = G.rtracker.Tracker(cfg, npm, geo_mlp, None, None)
+        mapper = G.rmapper.Mapper(cfg, ds, npm, geo_mlp, None, None)
+        for frame_id in range(frames):
+            used = ds.processed_frame
+            ds.cur_pose_ref = np.eye(4)
+            ds.cur_pose_torch = torch.tensor(ds.cur_pose_ref, dtype=cfg.dtype)
+            ds.cur_point_cloud_torch = torch.from_numpy(scans[frame_id].astype(np.float32) / np.float32(G.Q_SCALE))
+            ds.cur_point_ts_torch = None
+            preprocess(frame_id)
+            if used > 0:
+                if frame_id in DUMP:   # the state this tracking call sees (tools/ref_track_dump.py --compare)
+                    torch.save({"npm": npm, "dec": geo_mlp.state_dict(), "source": ds.cur_source_points,
+                                "guess": ds.cur_pose_guess_torch},
+                               os.path.join(RUN_DIR, f"refdump_{name}_f{frame_id}_t{threads}.pt"))
+                T, _, _, valid = tracker.tracking(ds.cur_source_points, ds.cur_pose_guess_torch, None, None,
+                                                  vis_result=False)
+                tracked.append(np.asarray(T, dtype=np.float64))
+                ds.lose_track = False
+                mapper.lose_track = False
+                update_odom(torch.tensor(z["hist_pose"][frame_id], dtype=torch.float64))
+            else:
+                tracked.append(np.eye(4))
+            npm.travel_dist = torch.tensor(np.array(ds.travel_dist), dtype=cfg.dtype)
+            if not mapper.lose_track and not ds.stop_status:
+                mapper.process_frame(ds.cur_point_cloud_torch, ds.cur_sem_labels_torch, ds.cur_pose_torch, used, False)
+            else:
+                npm.reset_local_map(ds.cur_pose_torch[:3, 3], None, used)
+            iters = cfg.iters * cfg.init_iter_ratio if used == 0 else cfg.iters
+            if used == cfg.freeze_after_frame:
+                G.rtools.freeze_decoders(geo_mlp, None, None, cfg)
+            if used % cfg.mapping_freq_frame == 0:
+                mapper.mapping(iters)
+            ds.processed_frame += 1
+            ref = z["hist_pose"][frame_id]
+            d = ref[:3, :3].T @ (tracked[-1][:3, 3] - ref[:3, 3])
+            print(f"{name} forced [{threads} threads] frame {frame_id}: tracked - stored (body frame) "
+                  f"{np.round(d, 4)}", flush=True)
+    finally:
+        rds.torch, G.rmapper.torch = saved
+    os.makedirs(RUN_DIR, exist_ok=True)
+    np.savez_compressed(os.path.join(RUN_DIR, f"{name}_forced_t{threads}.npz"), tracked=np.stack(tracked),
+                        stored=z["hist_pose"][:frames], torch_threads=np.int64(threads))
+    D = np.stack([p[:3, :3].T @ (t[:3, 3] - p[:3, 3]) for t, p in zip(tracked[1:], z["hist_pose"][1:frames])])
+    print(name, "forced", threads, "threads: body-frame tracked - stored mean", np.round(D.mean(0), 4), "std",
+          np.round(D.std(0), 4), "t", np.round(D.mean(0) / (D.std(0) / np.sqrt(len(D)) + 1e-12), 2))
 
 
 def combine(name):
@@ -83,5 +172,7 @@ def combine(name):
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 0)
+    elif sys.argv[1] == "forced":
+        run_forced(sys.argv[2], int(sys.argv[3]))
     else:
         combine(sys.argv[2])

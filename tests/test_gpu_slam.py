@@ -151,8 +151,8 @@ def test_slam_sequence_bitwise_reproducible(golden, dev):
     for _ in range(2):
         nm, dec, mapper, loop, replay, draws, scans = _sequence(z, dev, 12)
         poses = []
-        for pts in scans:
-            loop.frame(pts, draws=draws)
+        for k, pts in enumerate(scans):
+            loop.frame(pts, draws=draws, next_pts=scans[k + 1] if k + 1 < len(scans) else None)
             poses.append(np.array(loop.cur_pose_ref))
         runs.append((np.stack(poses), [nm.neural_points.clone(), nm.geo_features.clone(),
                                        nm.point_certainties.clone(), nm.point_ts_update.clone()]
@@ -203,7 +203,7 @@ def test_slam_sequence_matches_reference(golden, dev, fixture):
             if part == "process_frame":
                 seen["counts"] = (nm.count(), nm.local_count(), int(mapper.pool_sample_count),
                                   int(mapper.new_idx.shape[0]))
-        valid = loop.frame(pts, draws=draws, timer=check)
+        valid = loop.frame(pts, draws=draws, timer=check, next_pts=scans[k + 1] if k + 1 < frames else None)
         assert bool(valid) == bool(z["hist_valid"][k]), f"frame {k}: tracking validity"
         assert replay.calls == int(z["hist_draws_after"][k]), f"frame {k}: draw stream out of step"
         counts = seen["counts"]

@@ -142,3 +142,41 @@ def test_loaded_map_queries_match_reference(golden):
         np.testing.assert_array_equal(_np(nn), z[f"q{ql}_nn_counts"])
         np.testing.assert_allclose(_np(sdf), z[f"q{ql}_sdf"], rtol=0, atol=1e-5)
         assert_grad_close(_np(grad), z[f"q{ql}_grad"])
+
+
+@pytest.mark.gpu
+def test_reference_save_path_pickles_the_live_object(tmp_path):
+    """After install() the reference's own save_implicit_map (utils/tools.py:224-238) torch.saves
+    the NeuralPoints object itself.  After map updates (capacity-buffer arrays, weak-reference
+    caches) and a mapping() call, that pickle must work (NeuralPoints.__getstate__ drops the
+    transient caches), store only each array's own rows, and load back to a map whose arrays and
+    SDF queries equal the live map's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import pin_slam_amd as P
+    from pin_slam_amd.synthetic import surface_map, surface_pool, surface_scan
+    nm, dec, pts = surface_map(200, device="cuda", buffer_size=1 << 22, query_backend="grid")
+    nm.travel_dist = torch.arange(4, dtype=torch.float32, device="cuda")
+    for k in range(3):
+        nm.update(surface_scan(20.0 + k, 30.0, 8.0, 4096, seed=k, device="cuda"),
+                  torch.tensor([20.0 + k, 30.0, 1.7], device="cuda"), None, k)
+    coord, label, ts = surface_pool(pts, 20000, device="cuda")
+    mapper = P.Mapper(nm.config, None, nm, dec)
+    mapper.set_pool(coord, label, ts)
+    mapper.mapping(2)
+    assert nm.__dict__.get("_row_bufs"), "the map arrays should live in capacity buffers here"
+    q = pts[::7].contiguous()
+    want = P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False)
+    os.makedirs(tmp_path / "model")
+    path = str(tmp_path / "model" / "pin_map.pth")
+    torch.save({"neural_points": nm, "geo_decoder": dec.state_dict()}, path)   # the reference's call
+    assert os.path.getsize(path) < 2 * (nm.buffer_pt_index.numel() * 4 + 64 * nm.count() * 4 + (1 << 20))
+    m = torch.load(path, weights_only=False)    # a file this test wrote
+    back = m["neural_points"]
+    for k in ("neural_points", "geo_features", "point_certainties", "point_ts_update", "local_neural_points",
+              "local_geo_features", "global2local", "buffer_pt_index"):
+        assert torch.equal(getattr(back, k), getattr(nm, k)), k
+        t = getattr(back, k)
+        assert t.untyped_storage().nbytes() == t.numel() * t.element_size(), k
+    got = P.query_sdf(back, dec, q, query_locally=False, want_grad=True, want_certainty=False)
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]) and torch.equal(got[2], want[2])

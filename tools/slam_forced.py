@@ -22,6 +22,9 @@ from tests.test_gpu_slam import _pose_err, _sequence  # noqa: E402
 import pin_slam_amd as P  # noqa: E402
 
 
+DUMP = {int(v) for v in __import__("os").environ.get("DUMP", "").split(",") if v}
+
+
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "slam_seq"
     det = (sys.argv[2] if len(sys.argv) > 2 else "1") == "1"
@@ -37,8 +40,25 @@ def main():
         used = loop.processed_frame
         loop.read_and_preprocess(scans[k])
         if used > 0:
+            hist = []
+            tracker._iteration_done = lambda i, dT, st: hist.append(np.asarray(dT.cpu() if torch.is_tensor(dT) else dT))
+            if k in DUMP:   # the state this tracking call sees, for tools/ref_track_dump.py
+                import os
+                from pin_slam_amd.mapio import save_implicit_map
+                d = f"gpurun_out/dump/{name}_f{k}"
+                os.makedirs(d, exist_ok=True)
+                path = save_implicit_map(d, nm, dec, tensor_device="cpu")
+                import gzip
+                import shutil
+                with open(path, "rb") as fi, gzip.open(path + ".gz", "wb", compresslevel=1) as fo:
+                    shutil.copyfileobj(fi, fo)   # the 5e7-slot table is mostly -1: a few MB compressed
+                os.remove(path)
             T, _, _, valid = tracker.tracking(loop.cur_source_points, loop.cur_pose_guess_torch, None, None)
             ours = T.detach().cpu().numpy()
+            if k in DUMP:
+                np.savez(f"{d}/track.npz", source=loop.cur_source_points.cpu().numpy(),
+                         guess=loop.cur_pose_guess_torch.cpu().numpy(), ours=ours, ref=ref[k],
+                         iterations=int(tracker.last_iterations), deltas=np.stack(hist), valid=bool(valid))
             dt, dr = _pose_err(ours, ref[k])
             g_dt, g_dr = _pose_err(loop.cur_pose_guess_torch.cpu().numpy(), ref[k])
             # the difference in the reference pose's body frame (x: along the street)
