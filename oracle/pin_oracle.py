@@ -185,6 +185,123 @@ class Query:
     nbr_feat: np.ndarray      # [N,k,F]
 
 
+def ref_sort_row(vals) -> list:
+    """The column order torch's CPU sort(stable=False) leaves one row in: libstdc++ std::sort
+    (introsort -- median-of-three quicksort down to runs of 16, heapsort past 2 floor(log2 n)
+    levels, then an insertion sort) with a plain less-than on the values (aten SortingKernel), as
+    the reference's k-NN sort runs it (model/neural_points.py:562).  Equal values end up in an
+    order that depends on the whole row, which is what this restatement reproduces."""
+    k = [float(v) for v in vals]
+    g = list(range(len(k)))
+    n = len(k)
+
+    def swap(a, b):
+        k[a], k[b] = k[b], k[a]
+        g[a], g[b] = g[b], g[a]
+
+    def adjust_heap(f, h, ln, vk, vg):          # __adjust_heap + __push_heap
+        top, c = h, h
+        while c < (ln - 1) // 2:
+            c = 2 * (c + 1)
+            if k[f + c] < k[f + c - 1]:
+                c -= 1
+            k[f + h], g[f + h] = k[f + c], g[f + c]
+            h = c
+        if ln % 2 == 0 and c == (ln - 2) // 2:
+            c = 2 * (c + 1)
+            k[f + h], g[f + h] = k[f + c - 1], g[f + c - 1]
+            h = c - 1
+        parent = (h - 1) // 2
+        while h > top and k[f + parent] < vk:
+            k[f + h], g[f + h] = k[f + parent], g[f + parent]
+            h = parent
+            parent = (h - 1) // 2
+        k[f + h], g[f + h] = vk, vg
+
+    def heap_sort(f, l):                         # __partial_sort(first, last, last)
+        ln = l - f
+        if ln >= 2:
+            parent = (ln - 2) // 2
+            while True:
+                adjust_heap(f, parent, ln, k[f + parent], g[f + parent])
+                if parent == 0:
+                    break
+                parent -= 1
+        while l - f > 1:
+            l -= 1
+            vk, vg = k[l], g[l]
+            k[l], g[l] = k[f], g[f]
+            adjust_heap(f, 0, l - f, vk, vg)
+
+    def linear_insert(i):                        # __unguarded_linear_insert
+        vk, vg = k[i], g[i]
+        j = i - 1
+        while vk < k[j]:
+            k[i], g[i] = k[j], g[j]
+            i, j = j, j - 1
+        k[i], g[i] = vk, vg
+
+    def insertion_sort(f, l):
+        for i in range(f + 1, l):
+            if k[i] < k[f]:
+                vk, vg = k[i], g[i]
+                k[f + 1:i + 1], g[f + 1:i + 1] = k[f:i], g[f:i]
+                k[f], g[f] = vk, vg
+            else:
+                linear_insert(i)
+
+    def introsort_loop(f, l, depth):
+        while l - f > 16:
+            if depth == 0:
+                heap_sort(f, l)
+                return
+            depth -= 1
+            a, b, c = f + 1, f + (l - f) // 2, l - 1      # __move_median_to_first
+            if k[a] < k[b]:
+                swap(f, b) if k[b] < k[c] else (swap(f, c) if k[a] < k[c] else swap(f, a))
+            elif k[a] < k[c]:
+                swap(f, a)
+            elif k[b] < k[c]:
+                swap(f, c)
+            else:
+                swap(f, b)
+            lo, hi = f + 1, l                              # __unguarded_partition
+            while True:
+                while k[lo] < k[f]:
+                    lo += 1
+                hi -= 1
+                while k[f] < k[hi]:
+                    hi -= 1
+                if not lo < hi:
+                    break
+                swap(lo, hi)
+                lo += 1
+            introsort_loop(lo, l, depth)
+            l = lo
+
+    if n > 1:
+        introsort_loop(0, n, 2 * (n.bit_length() - 1))
+        if n > 16:
+            insertion_sort(0, 16)
+            for i in range(16, n):
+                linear_insert(i)
+        else:
+            insertion_sort(0, n)
+    return g
+
+
+def ref_sort_order(d2: np.ndarray) -> np.ndarray:
+    """np.argsort(d2, axis=1) in the reference's order (ref_sort_row): rows whose valid
+    distances are all distinct take a stable argsort (any sort agrees there up to the order of
+    the 9e3 entries, which hold no neighbour); rows with equal valid distances are redone."""
+    order = np.argsort(d2, axis=1, kind="stable")
+    s = np.take_along_axis(d2, order, 1)
+    tied = ((s[:, 1:] == s[:, :-1]) & (s[:, 1:] < INVALID_DIST2)).any(1)
+    for r in np.nonzero(tied)[0]:
+        order[r] = ref_sort_row(d2[r])
+    return order
+
+
 def query_feature(st: MapState, q: np.ndarray, nn_k: int, neighbor_dx: np.ndarray, maxd2: float,
                   weighted_first: bool = True, training_mode: bool = False, query_locally: bool = True,
                   query_ts: Optional[np.ndarray] = None, time_filtering: bool = True) -> Query:
@@ -201,7 +318,7 @@ def query_feature(st: MapState, q: np.ndarray, nn_k: int, neighbor_dx: np.ndarra
     nn_counts = (idx >= 0).sum(-1).astype(np.int64)
     d2 = d2.copy()
     d2[idx == -1] = np.float32(INVALID_DIST2)
-    order = np.argsort(d2, axis=1, kind="stable")
+    order = ref_sort_order(d2)   # torch.sort(dists2, dim=1): the reference's order of equal distances
     d2 = np.take_along_axis(d2, order, 1)[:, :nn_k]
     idx = np.take_along_axis(idx, order, 1)[:, :nn_k]
     gidx = np.take_along_axis(gidx, order, 1)[:, :nn_k]

@@ -10,7 +10,7 @@ ops is what that path costs on a CPU.  Written from the algorithm (SURVEY.md sec
 the reference's numerics where they decide results:
   model/neural_points.py:459-509  voxel floor (f32 division), int64 cell products, fmod hash with
                                   the negative-index wrap, candidate gather, distance gate
-  model/neural_points.py:528-674  nn_count before truncation, stable sort, k nearest, IDW weights
+  model/neural_points.py:528-674  nn_count before truncation, torch's (unstable) sort, k nearest, IDW weights
                                   1/(d2 + 1e-15) row-normalised, training-mode certainty / ts
                                   side effects, weighted_first feature sum
   model/decoder.py:66-88          Linear(11, 64) + ReLU + Linear(64, 1), times sdf_scale
@@ -78,7 +78,7 @@ def knn(m: TorchMap, q: torch.Tensor):
         bad = idx < 0
     nn_count = (~bad).sum(-1)
     key = torch.where(bad, torch.full_like(d2.detach(), 9e3), d2.detach())
-    _, order = torch.sort(key, dim=1, stable=True)
+    _, order = torch.sort(key, dim=1)   # the reference's unstable sort: its order of equal distances
     order = order[:, :m.nn_k]
     return torch.gather(idx, 1, order), torch.gather(d2, 1, order), nn_count
 

@@ -68,13 +68,15 @@ __device__ __forceinline__ float dist2(float px, float py, float pz, float qx, f
 #endif
 
 // Sorted (ascending) register list of the k nearest candidates.  Ties keep candidate
-// order (cell order), matching the stable sort of the CPU reference (:561-565).
+// order (cell order); a list with a tie is redone in the reference's order (resolve_ties).
 struct TopK {
     float d[kK];
     int g[kK];
+    float rej;   // the smallest distance that did not stay in the list (tie check, resolve_ties)
     __device__ __forceinline__ void init() {
 #pragma unroll
         for (int j = 0; j < kK; ++j) { d[j] = kInvalidDist2; g[j] = -1; }
+        rej = INFINITY;
     }
     // Branch-free insertion (pure selects).  x = +inf is a no-op, so callers insert every
     // candidate unconditionally with rejected ones mapped to +inf.
@@ -82,6 +84,7 @@ struct TopK {
     // c[j] ? d[j] : (c[j-1] ? x : d[j-1]) is the median of (d[j-1], x, d[j]) (equal values are
     // interchangeable, so ties change nothing); the payloads keep the two selects.
     __device__ __forceinline__ void insert(float x, int gi) {
+        rej = fminf(rej, fmaxf(x, d[kK - 1]));   // x itself, or the entry it pushes out
         bool c[kK];
 #pragma unroll
         for (int j = 0; j < kK; ++j) c[j] = d[j] <= x;
@@ -121,9 +124,197 @@ __device__ __forceinline__ void topk_pair_merge(TopK& tk, int ph) {
         ad[j] = ph ? tk.d[j] : od[j];
         ag[j] = ph ? tk.g[j] : og[j];
     }
+    base.rej = fminf(tk.rej, __shfl_xor(tk.rej, 1));
 #pragma unroll
     for (int j = 0; j < kK; ++j) base.insert(ad[j], ag[j]);
     tk = base;
+}
+
+// ---------------------------------------------------------------------------------------
+// Equal distances.  The reference orders a query's Kc candidate distances with torch's CPU
+// sort(stable=False) (model/neural_points.py:561-565), which is libstdc++'s std::sort over the
+// row (aten SortingKernel), and keeps the first k.  Where two VALID candidates have exactly the
+// same distance the order std::sort leaves them in is not cell order: it depends on the whole
+// row (median-of-three pivots, partitions, the final insertion sort).  Lattice-quantised scans
+// make exact ties common enough to matter: taking them in cell order (a stable sort) prefers the
+// cells of lower offsets and biased the trained map measurably.  The
+// streaming top-k above keeps cell order; a query whose kept list has a tie -- between two kept
+// entries, or between the k-th kept and the best one left out -- is redone: its whole row of Kc
+// (distance, payload) pairs in cell order, 9e3 for the invalid ones as in the reference, sorted
+// by a restatement of std::sort, and the first entries taken.
+constexpr int kRefSortMax = 128;   // rows up to this many cells (every reference config: Kc <= 93)
+
+__device__ __forceinline__ bool topk_tied(const TopK& tk, int nn_k, int nn) {
+    bool t = false;
+#pragma unroll
+    for (int j = 0; j + 1 < kK; ++j)
+        t = t || (j + 1 <= nn_k && j + 1 < nn && tk.d[j] == tk.d[j + 1]);
+    if (nn_k >= kK) t = t || (nn > kK && tk.rej == tk.d[kK - 1]);
+    return t;
+}
+
+// One row of the reference's k-NN sort, in private memory: keys (distance or 9e3) and payloads
+struct RefRow {
+    float k[kRefSortMax];
+    int g[kRefSortMax];
+    __device__ __forceinline__ bool less(int a, int b) const { return k[a] < k[b]; }
+    __device__ __forceinline__ void swap(int a, int b) {
+        const float tk = k[a];
+        k[a] = k[b];
+        k[b] = tk;
+        const int tg = g[a];
+        g[a] = g[b];
+        g[b] = tg;
+    }
+    // libstdc++ __adjust_heap + __push_heap on [f, f + len), hole at h, value (vk, vg)
+    __device__ void adjust_heap(int f, int h, int len, float vk, int vg) {
+        const int top = h;
+        int c = h;
+        while (c < (len - 1) / 2) {
+            c = 2 * (c + 1);
+            if (k[f + c] < k[f + c - 1]) --c;
+            k[f + h] = k[f + c];
+            g[f + h] = g[f + c];
+            h = c;
+        }
+        if ((len & 1) == 0 && c == (len - 2) / 2) {
+            c = 2 * (c + 1);
+            k[f + h] = k[f + c - 1];
+            g[f + h] = g[f + c - 1];
+            h = c - 1;
+        }
+        int parent = (h - 1) / 2;
+        while (h > top && k[f + parent] < vk) {
+            k[f + h] = k[f + parent];
+            g[f + h] = g[f + parent];
+            h = parent;
+            parent = (h - 1) / 2;
+        }
+        k[f + h] = vk;
+        g[f + h] = vg;
+    }
+    // __partial_sort(first, last, last): __make_heap, then __sort_heap
+    __device__ void heap_sort(int f, int l) {
+        const int len = l - f;
+        if (len >= 2) {
+            for (int parent = (len - 2) / 2;; --parent) {
+                adjust_heap(f, parent, len, k[f + parent], g[f + parent]);
+                if (parent == 0) break;
+            }
+        }
+        while (l - f > 1) {
+            --l;
+            const float vk = k[l];
+            const int vg = g[l];
+            k[l] = k[f];
+            g[l] = g[f];
+            adjust_heap(f, 0, l - f, vk, vg);
+        }
+    }
+    __device__ void unguarded_linear_insert(int i) {
+        const float vk = k[i];
+        const int vg = g[i];
+        int j = i - 1;
+        while (vk < k[j]) {
+            k[i] = k[j];
+            g[i] = g[j];
+            i = j;
+            --j;
+        }
+        k[i] = vk;
+        g[i] = vg;
+    }
+    __device__ void insertion_sort(int f, int l) {
+        if (f == l) return;
+        for (int i = f + 1; i < l; ++i) {
+            if (k[i] < k[f]) {
+                const float vk = k[i];
+                const int vg = g[i];
+                for (int j = i; j > f; --j) {
+                    k[j] = k[j - 1];
+                    g[j] = g[j - 1];
+                }
+                k[f] = vk;
+                g[f] = vg;
+            } else {
+                unguarded_linear_insert(i);
+            }
+        }
+    }
+    // std::sort(first, first + n, less): __introsort_loop with depth 2 floor(log2 n) and runs of
+    // 16, then __final_insertion_sort.  The recursion of __introsort_loop on the right part is a
+    // stack of disjoint segments (the order they are finished in does not change the result).
+    __device__ void sort(int n) {
+        if (n < 2) return;
+        int sf[16], sl[16], sd[16];
+        int top = 0;
+        sf[0] = 0;
+        sl[0] = n;
+        sd[0] = 2 * (31 - __clz(n));
+        top = 1;
+        while (top > 0) {
+            --top;
+            int f = sf[top], l = sl[top], depth = sd[top];
+            while (l - f > 16) {
+                if (depth == 0) {
+                    heap_sort(f, l);
+                    break;
+                }
+                --depth;
+                // __move_median_to_first(f, f + 1, mid, l - 1)
+                const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+                if (less(a, b)) {
+                    if (less(b, c)) swap(f, b);
+                    else if (less(a, c)) swap(f, c);
+                    else swap(f, a);
+                } else if (less(a, c)) swap(f, a);
+                else if (less(b, c)) swap(f, c);
+                else swap(f, b);
+                // __unguarded_partition(f + 1, l, f)
+                int lo = f + 1, hi = l;
+                for (;;) {
+                    while (less(lo, f)) ++lo;
+                    --hi;
+                    while (less(f, hi)) --hi;
+                    if (!(lo < hi)) break;
+                    swap(lo, hi);
+                    ++lo;
+                }
+                if (top < 16) {   // __introsort_loop(cut, last, depth); at most ~2 log2 n pending
+                    sf[top] = lo;
+                    sl[top] = l;
+                    sd[top] = depth;
+                    ++top;
+                } else {
+                    heap_sort(lo, l);   // unreachable for n <= kRefSortMax
+                }
+                l = lo;
+            }
+        }
+        if (n > 16) {
+            insertion_sort(0, 16);
+            for (int i = 16; i < n; ++i) unguarded_linear_insert(i);
+        } else {
+            insertion_sort(0, n);
+        }
+    }
+};
+
+// The reference's k first entries of a tied query (see above); src.ref_row fills the row.
+template <class Src>
+__device__ __forceinline__ void resolve_ties(const Src& src, float qx, float qy, float qz, int nn_k, int nn,
+                                             TopK& tk) {
+    if (!topk_tied(tk, nn_k, nn)) return;
+    RefRow r;
+    const int n = src.ref_row(qx, qy, qz, r);
+    if (n > kRefSortMax) return;   // larger neighbourhoods keep cell order (no reference config)
+    r.sort(n);
+#pragma unroll
+    for (int j = 0; j < kK; ++j) {
+        const bool in = j < n && r.k[j] < kInvalidDist2;
+        tk.d[j] = in ? r.k[j] : kInvalidDist2;
+        tk.g[j] = in ? r.g[j] : -1;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -178,6 +369,25 @@ struct HashSource {
             }
         }
         return nn;
+    }
+    // the whole row of the reference's sort (resolve_ties): per neighbour cell in order, the
+    // candidate's distance and payload, 9e3 / -1 where the reference has idx -1; returns Kc
+    __device__ int ref_row(float qx, float qy, float qz, RefRow& r) const {
+        const float4* __restrict__ rec = (const float4*)p.records;
+        const uint32_t B = (uint32_t)h.buffer_size;
+        const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
+        const int Kc = h.num_cells;
+        for (int c = 0; c < Kc && c < kRefSortMax; ++c) {
+            uint32_t s = base + (uint32_t)h.cells[c];
+            s = s >= B ? s - B : s;
+            const int gi = h.table[s];
+            const float4 v = rec[gi > 0 ? gi : 0];
+            const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
+            const bool ok = gi >= 0 && __float_as_int(v.w) != -1 && d2 <= h.max_valid_dist2;
+            r.k[c] = ok ? d2 : kInvalidDist2;
+            r.g[c] = ok ? gi : -1;
+        }
+        return Kc;
     }
     __device__ __forceinline__ float4 record(int pay) const { return ((const float4*)p.records)[pay > 0 ? pay : 0]; }
     __device__ __forceinline__ void features(int pay, int64_t id, float4& f0, float4& f1) const {
@@ -525,6 +735,38 @@ struct GridSource {
                 tk.insert(ok ? d2 : INFINITY, IDP ? (id & kIdMask) : ci[u]);
             }
         }
+    }
+
+    // the whole row of the reference's sort (resolve_ties): per neighbour cell in order, the
+    // candidate's distance and payload, 9e3 / -1 where the reference has idx -1; returns Kc
+    __device__ int ref_row(float qx, float qy, float qz, RefRow& r) const {
+        const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
+        const float4* __restrict__ crec = (const float4*)gr.crec;
+        const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
+        const int ex = 4 * gr.dims.nbx, ey = 4 * gr.dims.nby, ez = 4 * gr.dims.nbz;
+        const int lx = rel(qx, res, gr.dims.ox, ex);
+        const int ly = rel(qy, res, gr.dims.oy, ey);
+        const int lz = rel(qz, res, gr.dims.oz, ez);
+        const int Kc = gr.num_cells;
+        for (int c = 0; c < Kc && c < kRefSortMax; ++c) {
+            const int of = gr.offsets[c];
+            const int cx = lx + ((of & 255) - 128);
+            const int cy = ly + (((of >> 8) & 255) - 128);
+            const int cz = lz + (((of >> 16) & 255) - 128);
+            const bool in = (unsigned)cx < (unsigned)ex && (unsigned)cy < (unsigned)ey && (unsigned)cz < (unsigned)ez;
+            const uint4 w = bricks[in ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * gr.dims.nbx + (cx >> 2) : 0];
+            const int bit = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
+            const uint64_t bits = ((uint64_t)w.y << 32) | w.x;
+            const bool set = in && ((bits >> bit) & 1ull);
+            const int ci = set ? (int)(w.z + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull))) : -1;
+            const float4 v = crec[ci > 0 ? ci : 0];
+            const int id = __float_as_int(v.w);
+            const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
+            const bool ok = ci >= 0 && id != -1 && d2 <= maxd2;
+            r.k[c] = ok ? d2 : kInvalidDist2;
+            r.g[c] = ok ? (IDP ? (id & kIdMask) : ci) : -1;
+        }
+        return Kc;
     }
 
     // Per-cell scan (any window): CH cell lookups back to back, then CH record gathers.

@@ -366,6 +366,7 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
 #if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 1
     // profiling variant: candidate scan only (the top-k kept live through one output)
     if (i >= 0) {
@@ -747,6 +748,7 @@ __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoin
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
     Neighbours nb;
     load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
     const float cert = (cert_out && p.certainties) ? gather_certainty(src, nb) : 0.f;

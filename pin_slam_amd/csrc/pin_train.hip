@@ -119,6 +119,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     // pair mode: both lanes of the pair hold the row's neighbours; the even lane writes its outputs
     const bool writer = live && (!PAIR || !(threadIdx.x & 1));
     const int nn_k = c.nn_k;
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
     float u[kK];
     float S = 0.f;
 #pragma unroll
@@ -607,6 +608,7 @@ __device__ __forceinline__ void train_forward_eik_body(const Src& src, const Pin
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
     const int nn_k = c.nn_k;
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
     float u[kK];
     float S = 0.f;
 #pragma unroll

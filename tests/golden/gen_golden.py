@@ -97,17 +97,22 @@ def make_config(voxel=0.3, cells=2, alpha=0.2, nn_k=8, weighted_first=True, buff
     return c
 
 
-def build_map(cfg, n_side, seed):
-    """Surface map through the reference's own insert path (NeuralPoints.update)."""
+def build_map(cfg, n_side, seed, lattice=False):
+    """Surface map through the reference's own insert path (NeuralPoints.update).  lattice: the
+    points sit on cell centres (a power-of-two voxel keeps every coordinate exact), so queries on
+    the half-cell lattice see many exactly equal neighbour distances."""
     rng = np.random.default_rng(seed)
     res = cfg.voxel_size_m
     ii, jj = np.meshgrid(np.arange(n_side), np.arange(n_side), indexing="ij")
     x = (ii.ravel() + 0.5) * res - n_side * res / 2
     y = (jj.ravel() + 0.5) * res - n_side * res / 2
     z = surface_z(x, y)
+    if lattice:
+        z = (np.floor(z / res) + 0.5) * res
     pts = np.stack([x, y, z], 1).astype(np.float32)
     # jitter a little so the down-sample keeps interesting positions
-    pts += rng.normal(0, res * 0.05, pts.shape).astype(np.float32)
+    if not lattice:
+        pts += rng.normal(0, res * 0.05, pts.shape).astype(np.float32)
     npm = NeuralPoints(cfg)
     T = 10
     npm.travel_dist = torch.arange(T, dtype=torch.float32) * 10.0
@@ -250,13 +255,16 @@ def run_query(npm, dec, cfg, q, query_locally, training_mode=False, query_ts=Non
     return out
 
 
-def gen_query_case(name, cfg_kwargs, n_side, n_surface, seed):
+def gen_query_case(name, cfg_kwargs, n_side, n_surface, seed, lattice=False):
     cfg = make_config(**cfg_kwargs)
-    npm, _ = build_map(cfg, n_side, seed)
+    npm, _ = build_map(cfg, n_side, seed, lattice)
     # sensor at origin, current frame 9
     npm.reset_local_map(torch.zeros(3), torch.eye(3), 9)
     dec = decoder(cfg)
     q = make_queries(npm, cfg, n_surface, seed)
+    if lattice:   # queries on the half-cell lattice: equal distances to mirror-image neighbours
+        h = cfg.voxel_size_m / 2
+        q = (np.round(q / h) * h).astype(np.float32)
     rec = dict(queries=q, nn_k=np.int64(cfg.query_nn_k), weighted_first=np.bool_(cfg.weighted_first),
                num_nei_cells=np.int64(cfg.num_nei_cells), search_alpha=np.float64(cfg.search_alpha))
     rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
@@ -1126,6 +1134,8 @@ def main(only=None):
                                                       free_front_n=3, free_behind_n=2, free_sample_end_dist_m=1.5,
                                                       dist_weight_on=False, surface_sample_range_m=0.3)),
                  "process_frame": lambda: gen_process_frame_case(),
+                 "query_ties": lambda: gen_query_case("query_ties", dict(voxel=0.25, alpha=0.5, weighted_first=True),
+                                                      100, 1600, seed=16, lattice=True),
                  "slam_seq": lambda: gen_slam_sequence(),
                  "slam_seq100": lambda: gen_slam_sequence("slam_seq100", frames=100, scene="long"),
                  "mapping_calls": lambda: gen_mapping_calls()}
@@ -1149,6 +1159,7 @@ def main(only=None):
     gen_sampler_case("sampler_dropoff", 14, behind_dropoff_on=True, surface_sample_n=4, free_front_n=3,
                      free_behind_n=2, free_sample_end_dist_m=1.5, dist_weight_on=False, surface_sample_range_m=0.3)
     gen_process_frame_case()
+    gen_query_case("query_ties", dict(voxel=0.25, alpha=0.5, weighted_first=True), 100, 1600, seed=16, lattice=True)
     with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
         for k, v in meta.items():
             f.write(f"{k}: {v}\n")

@@ -140,6 +140,132 @@ def run_forced(name, threads):
           np.round(D.std(0), 4), "t", np.round(D.mean(0) / (D.std(0) / np.sqrt(len(D)) + 1e-12), 2))
 
 
+TRACE_STEPS = (1, 2, 3, 5, 10, 20, 50, 100, 200, 400, 600)
+
+
+def run_f0_trace(name, threads):
+    """Frame 0 of the fixture's loop (update, process_frame, the 15 x 40-iteration mapping() call)
+    at `threads` torch threads, recording the decoder and the feature statistics after the Adam
+    steps in TRACE_STEPS: where the reference's own runs part ways, and where ours (the same
+    record from tools/slam_forced.py) parts from them."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import types
+    import torch
+    import gen_golden as G
+    import dataset.slam_dataset as rds_mod
+    import utils.data_sampler as rds
+    c = CASES[name]
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(21)
+    scene, poses = G.sequence_scene(c["scene"], rng, c["frames"])
+    scan0 = G.lidar_scan(poses[0], scene, rng)
+    cfg = G.slam_config()
+    replay = G.ReplayDraws(2024)
+    rt = G._ReplayTorch(replay)
+    saved = (rds.torch, G.rmapper.torch, G.rmapper.setup_optimizer)
+    rds.torch = rt
+    G.rmapper.torch = rt
+    rds_mod.get_time = time.time
+    rec = {}
+    saved_np_torch = G.rnp.torch
+    if os.environ.get("TIE_PROBE"):   # experiment: rows whose top-k set depends on the sort's tie order
+        class _Probe:
+            count = [0, 0]
+
+            def __getattr__(self, k):
+                return getattr(torch, k)
+
+            def sort(self, x, dim=-1, descending=False):
+                out = torch.sort(x, dim=dim, descending=descending)
+                st = torch.sort(x, dim=dim, descending=descending, stable=True)
+                k = cfg.query_nn_k
+                big = torch.tensor(1 << 40)
+                gidx = self.last_idx                 # the radius search's candidates, local ids
+                lidx = npm.global2local[gidx] if gidx is not None else None
+                # the valid candidates' local ids among the k first, compared as sets
+                va = torch.where(out[0][:, :k] < 9e3, lidx.gather(1, out[1][:, :k]), big)
+                vb = torch.where(st[0][:, :k] < 9e3, lidx.gather(1, st[1][:, :k]), big)
+                a = torch.sort(va, 1)[0]
+                b = torch.sort(vb, 1)[0]
+                bad = (a != b).any(1)
+                first = self.count[0] == 0
+                self.count[0] += int(bad.sum())
+                self.count[1] += x.shape[0]
+                if bad.any() and first:
+                    r = int(torch.nonzero(bad)[0])
+                    print("tie row:", np.round(x[r].numpy(), 7).tolist(), "unstable", out[1][r, :k].tolist(),
+                          "stable", st[1][r, :k].tolist(), "global ids", gidx[r].tolist(), "local ids",
+                          lidx[r].tolist(), flush=True)
+                return out
+        probe = _Probe()
+        probe.last_idx = None
+        G.rnp.torch = probe
+        orig_rns = G.NeuralPoints.radius_neighborhood_search
+
+        def rns(self_, points, time_filtering=False):
+            d2, idx = orig_rns(self_, points, time_filtering)
+            probe.last_idx = idx.clone()
+            return d2, idx
+        G.NeuralPoints.radius_neighborhood_search = rns
+    if os.environ.get("STABLE_SORT"):   # experiment: the reference with a stable k-NN sort
+        class _StableSort:
+            def __getattr__(self, k):
+                return getattr(torch, k)
+
+            @staticmethod
+            def sort(x, dim=-1, descending=False):
+                return torch.sort(x, dim=dim, descending=descending, stable=True)
+        G.rnp.torch = _StableSort()
+    try:
+        torch.manual_seed(42)
+        geo_mlp = G.Decoder(cfg, cfg.geo_mlp_hidden_dim, cfg.geo_mlp_level, 1)
+        npm = G.NeuralPoints(cfg)
+        ds = types.SimpleNamespace(config=cfg, silence=True, dtype=cfg.dtype, device="cpu", gt_pose_provided=False,
+                                   odom_poses=[], pgo_poses=None, gt_poses=None, travel_dist=[], processed_frame=0,
+                                   lose_track=False, consecutive_lose_track_frame=0, last_pose_ref=np.eye(4),
+                                   last_odom_tran=np.eye(4), cur_pose_ref=np.eye(4), stop_count=0, stop_status=False,
+                                   cur_point_cloud_torch=None, cur_point_ts_torch=None, cur_sem_labels_torch=None,
+                                   cur_source_points=None, cur_source_normals=None, cur_source_colors=None)
+        preprocess = types.MethodType(rds_mod.SLAMDataset.preprocess_frame, ds)
+        mapper = G.rmapper.Mapper(cfg, ds, npm, geo_mlp, None, None)
+
+        def setup(*a, **kw):
+            opt = saved[2](*a, **kw)
+            step = opt.step
+            count = [0]
+
+            def rec_step(*sa, **skw):
+                out = step(*sa, **skw)
+                count[0] += 1
+                if count[0] in TRACE_STEPS:
+                    for k, p in zip(("W1", "b1", "W2", "b2"), geo_mlp.parameters()):
+                        rec[f"s{count[0]}_{k}"] = p.detach().numpy().copy()
+                    rec[f"s{count[0]}_feat"] = npm.local_geo_features.detach().numpy().copy()
+                return out
+            opt.step = rec_step
+            return opt
+        G.rmapper.setup_optimizer = setup
+        ds.cur_pose_ref = np.eye(4)
+        ds.cur_pose_torch = torch.tensor(ds.cur_pose_ref, dtype=cfg.dtype)
+        ds.cur_point_cloud_torch = torch.from_numpy(scan0.astype(np.float32) / np.float32(G.Q_SCALE))
+        ds.cur_point_ts_torch = None
+        preprocess(0)
+        npm.travel_dist = torch.tensor(np.array(ds.travel_dist), dtype=cfg.dtype)
+        mapper.process_frame(ds.cur_point_cloud_torch, ds.cur_sem_labels_torch, ds.cur_pose_torch, 0, False)
+        mapper.mapping(cfg.iters * cfg.init_iter_ratio)
+    finally:
+        rds.torch, G.rmapper.torch, G.rmapper.setup_optimizer = saved
+        G.rnp.torch = saved_np_torch
+    os.makedirs(RUN_DIR, exist_ok=True)
+    tag = "_stable" if os.environ.get("STABLE_SORT") else ""
+    if os.environ.get("TIE_PROBE"):
+        print("rows whose top-k set depends on the tie order:", probe.count[0], "of", probe.count[1], flush=True)
+        return
+    np.savez_compressed(os.path.join(RUN_DIR, f"{name}_f0trace{tag}_t{threads}.npz"), **rec)
+    print(name, "frame-0 trace", threads, "threads:",
+          [(s, round(float(rec[f"s{s}_b2"][0]), 5)) for s in TRACE_STEPS if f"s{s}_b2" in rec])
+
+
 def combine(name):
     """Fold the stored run and every RUN_DIR run of `name` into tests/golden/<name>.npz."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"{name}.npz")
@@ -174,5 +300,7 @@ if __name__ == "__main__":
         run(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 0)
     elif sys.argv[1] == "forced":
         run_forced(sys.argv[2], int(sys.argv[3]))
+    elif sys.argv[1] == "f0trace":
+        run_f0_trace(sys.argv[2], int(sys.argv[3]))
     else:
         combine(sys.argv[2])

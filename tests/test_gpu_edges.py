@@ -152,8 +152,9 @@ def _lattice_map(dev, nn_k, seed):
 @pytest.mark.parametrize("nn_k", [8, 6])
 def test_equal_and_near_equal_distances_match_oracle(dev, nn_k):
     """Candidates at exactly equal distances (a query on a lattice node is equidistant from 8
-    cell centres) and at distances a few ulps apart.  The reference keeps the k nearest with a
-    stable sort, ties in cell order (model/neural_points.py:561-565); the grid kernel's packed-key
+    cell centres) and at distances a few ulps apart.  The reference keeps the k nearest after
+    torch's unstable sort (model/neural_points.py:561-565; ties in the order std::sort leaves them,
+    restated by the oracle and by the kernels' resolve_ties); the grid kernel's packed-key
     selection truncates d2 to 18 mantissa bits and must fall back to the exact order where that
     matters.  Two layers (<= 32 occupied cells per query: packed keys) and six (33 > 32:
     the segmented scan).  A different neighbour set would move the SDF by ~1e-2."""

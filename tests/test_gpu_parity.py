@@ -14,7 +14,7 @@ from tests import helpers as H
 
 pytestmark = pytest.mark.gpu
 
-QUERY_CASES = ["query_wf", "query_nwf", "query_kitti"]
+QUERY_CASES = ["query_wf", "query_nwf", "query_kitti", "query_ties"]
 BACKENDS = ["hash", "grid"]
 SDF_ATOL = 1e-5
 

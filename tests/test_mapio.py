@@ -165,7 +165,7 @@ def test_reference_save_path_pickles_the_live_object(tmp_path):
     mapper.set_pool(coord, label, ts)
     mapper.mapping(2)
     assert nm.__dict__.get("_row_bufs"), "the map arrays should live in capacity buffers here"
-    q = pts[::7].contiguous()
+    q = pts[::7].to("cuda").contiguous()
     want = P.query_sdf(nm, dec, q, query_locally=False, want_grad=True, want_certainty=False)
     os.makedirs(tmp_path / "model")
     path = str(tmp_path / "model" / "pin_map.pth")

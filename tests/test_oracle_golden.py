@@ -5,7 +5,7 @@ import pytest
 
 from oracle import pin_oracle as O
 
-QUERY_CASES = ["query_wf", "query_nwf", "query_kitti"]
+QUERY_CASES = ["query_wf", "query_nwf", "query_kitti", "query_ties"]
 
 
 def _cfg(z):
@@ -281,3 +281,37 @@ def test_torch_cpu_mesher_batch(golden):
     sdf, mask = T.sdf_only(m, mlp, torch.from_numpy(z["coord"]), int(z["mesh_min_nn"]))
     np.testing.assert_array_equal(mask.numpy(), z["mc_mask"])
     np.testing.assert_allclose(sdf.numpy(), z["sdf"], atol=1e-6)
+
+
+def test_tie_fixture_needs_the_reference_sort(golden, monkeypatch):
+    """query_ties (neural points on cell centres, queries on the half-cell lattice) holds equal
+    neighbour distances in almost every row; the reference's features come out in the order its
+    unstable sort leaves them, which a stable sort does not reproduce."""
+    z = golden("query_ties")
+    d2 = np.where(z["rns1_idx"] < 0, 9e3, z["rns1_dist2"])
+    s = np.sort(d2, 1)
+    assert ((s[:, 1:] == s[:, :-1]) & (s[:, 1:] < 9e3)).any(1).mean() > 0.9
+    st = O.map_from_fixture(z)
+    mlp = O.mlp_from_fixture(z)
+    dx, maxd2, k, wf = _cfg(z)
+    monkeypatch.setattr(O, "ref_sort_order", lambda d: np.argsort(d, axis=1, kind="stable"))
+    _, _, _, qry = O.sdf_and_grad(st, mlp, z["queries"], k, dx, maxd2, wf, True)
+    assert not np.allclose(qry.feat, z["q1_feat"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("n", [2, 16, 17, 27, 33, 57, 81, 93, 125, 343])
+def test_ref_sort_row_is_torch_cpu_sort(n):
+    """ref_sort_row restates the sort the reference calls (torch.sort(dists2, dim=1) on the CPU):
+    the permutation it leaves rows with many equal keys in, 9e3 entries included."""
+    import torch
+    rng = np.random.default_rng(n)
+    for t in range(60):
+        v = rng.integers(0, max(2, n // 3), n).astype(np.float32)
+        if t % 3 == 0:
+            v[rng.random(n) < 0.3] = 9e3
+        if t % 5 == 0:
+            v = np.sort(v)
+        if t % 7 == 0:
+            v = np.sort(v)[::-1].copy()
+        _, o = torch.sort(torch.from_numpy(v)[None], dim=1)
+        assert O.ref_sort_row(v) == o[0].tolist()

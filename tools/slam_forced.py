@@ -81,6 +81,11 @@ def main():
             mapper.mapping(iters)
         loop.processed_frame += 1
         counts = (nm.count(), nm.local_count(), int(mapper.pool_sample_count), int(mapper.new_idx.shape[0]))
+        if k in (0, 3) and __import__("os").environ.get("DECSTATS"):
+            W1, b1, W2, b2 = (p.detach().double() for p in dec.parameters())
+            print(f"decoder after frame {k}: b2 {float(b2):.5f} mean b1 {float(b1.mean()):.4f} mean W2 "
+                  f"{float(W2.mean()):.4f} mean |W1| {float(W1.abs().mean()):.4f} feature mean "
+                  f"{float(nm.local_geo_features.detach().double().mean()):.5f}", flush=True)
         want = tuple(int(z[f"hist_{n}"][k]) for n in ("map_count", "local_count", "pool", "new"))
         print(f"frame {k}: counts {counts} ref {want}" + (
             f"  tracking from the reference's guess: {rows[-1][1]:.4f} m / {rows[-1][2]:.4f} deg off the reference "
