@@ -9,33 +9,39 @@ reference's Tracker / Mapper / NeuralPoints / DataSampler and its dataset bookke
 
 Both runs take every random draw of the sampler and of get_batch from the same ReplayDraws
 stream (tests/replay.py), in the reference's call order, so they differ only by floating-point
-summation order.  The loop is chaotic in that difference: the reference run twice, with 1 and with
-8 torch threads (only its reduction order changes), ends frame 0's 15 x 40-iteration mapping()
-with different decoders (|dW1| up to 1.7) and features, yet poses within ~2 cm / 0.03 deg and
-the same surface.  That spread is stored in the fixture (spread_*) and the tolerances below are
-stated against it -- element-wise feature parity after hundreds of iterations is not a property
-the reference has.  (A single 15-iteration mapping() call is pinned element-wise in
-tests/test_gpu_mapper.py::test_whole_mapping_call_fixture.)
+summation order.  The loop is chaotic in that difference: the reference itself, run again at other
+torch thread counts (or even at the same one), ends centimetres apart.  tests/golden/
+gen_slam_envelope.py ran the reference's loop 7 times on slam_seq (1, 2, 3, 4, 6, 8, 16 threads) and
+8 times on slam_seq100 (the same plus a second 8-thread run) and stored every run's poses, counts
+and surface SDFs in the fixture (env_*): that envelope is what a legitimate run looks like, and the
+bounds below place our run in it, widened by stated factors (W_POSE, W_COUNT, W_SURFACE: the
+smallest at which every reference run passes against the others), with small floors where the
+envelope is a single value.  They were fixed and committed
+before the run they judge; a run outside them is a defect to find (first failing frame and part)
+and fix, not a bound to widen.  Element-wise feature parity after hundreds of iterations is not a
+property the reference has (a single 15-iteration mapping() call is pinned element-wise in
+tests/test_gpu_mapper.py::test_whole_mapping_call_fixture).
 
-Our side runs the deterministic training mode (Mapper(deterministic=True): fixed-point gradient
-and certainty sums, stable tile order), so this test judges ONE reproducible trajectory -- two
-runs are bitwise equal -- against bounds fixed before it was run:
+Both training modes run: deterministic=True (fixed-point gradient and certainty sums,
+stable tile order -- two runs are bitwise equal, test_slam_sequence_bitwise_reproducible) and
+deterministic=False (float atomics: a run is one draw of our own run-to-run spread).  Checks:
   * preprocessed cloud / source point counts, tracking validity, draw-stream position: exact;
-  * pose within max(5 cm, 3 x spread) and max(0.1 deg, 3 x spread) of the reference's estimate
-    (spread: the largest 1- vs 8-thread difference of the reference up to that frame); the
-    distance to the ground truth is reported (bounded by the reference's own error + that
-    tolerance, which the pose bound implies);
-  * neural-point / local-map counts within max(1 %, 3 x spread), pool size within
-    max(0.1 %, 3 x spread), new samples within max(15 %, 3 x spread), the spread being the
-    largest relative 1- vs 8-thread count difference up to that frame (they follow the certainty
-    threshold); at the window-filter frames the pool count may differ by the difference carried in
-    plus the samples whose side of the filter sphere the pose differences can change (counted on
-    our pre-filter pool: displacement |dt_j| + theta_j * range per sample, |dt_k| for the centre);
+  * pose: |t - c_k| <= max(1 cm, W_POSE x e_k), c_k the mean of the reference runs' positions at
+    frame k, e_k the largest distance of any reference run from its frame's mean up to frame k;
+    the same for the rotation (chordal mean, angle floor 0.05 deg);
+  * counts (neural points, local map, pool, new samples): |n - mean_k| / mean_k within
+    max(floor, W_COUNT x the largest relative deviation of a run from its frame's mean up to frame
+    k), floors 0.2 %, 0.2 %, 0.01 %, 2 %; at the window-filter frames the pool may instead differ
+    from the stored run by the difference carried in plus the samples whose side of the filter
+    sphere our pose differences can change (counted on our pre-filter pool: displacement
+    |dt_j| + theta_j * range per sample, |dt_k| for the centre);
   * the map's SDF on the surface (scan points placed by the TRUE poses) after frame 0 and at the
-    end: mean |SDF| at most 1.25 x the reference's + 1 mm, and median |ours - reference| at most
-    3 x the median 1- vs 8-thread spread + 1 mm;
+    end: mean |SDF| at most the runs' largest + (W_SURFACE - 1) x their range + 1 mm, and the
+    median over probes of |ours - the runs' mean| at most W_SURFACE x the largest such median of
+    a run + 1 mm;
   * the end-of-run merge (recreate_hash(kept_points=False), pin_slam.py:366) raises where the
-    reference's does, and otherwise leaves a map of the same size within 1 %.
+    reference's runs do, and otherwise leaves a map whose size passes the count bound against
+    the runs' merged sizes.
 Every check is made on every frame; the failures are listed together at the end.
 """
 import json
@@ -65,24 +71,82 @@ def _pose_err(a, b):
     return dt, math.degrees(math.acos(min(1.0, max(-1.0, c))))
 
 
-def _within(got, want, rel):
-    return abs(int(got) - int(want)) <= max(1, rel * abs(int(want)))
+# Widening factors of the envelope (module docstring).  Calibrated on the reference alone, before
+# any run of ours: the smallest factor, rounded up to 0.5, at which EVERY reference run passes when
+# judged against the other runs of its fixture (tests/test_slam_envelope.py recomputes this
+# leave-one-out check): poses need 1.93, counts 4.05 (the reference's own outliers: slam_seq100's
+# stored run ends 1.5-1.9 % above the seven others), surface SDF 1.59.
+W_POSE = 2.0
+W_COUNT = 4.5
+W_SURFACE = 2.0
+COUNT_FLOORS = {"map_count": 0.002, "local_count": 0.002, "pool": 0.0001, "new": 0.02}
 
 
-def _surface_check(nm, dec, z, dev, probes_key, sdf_key, ratio=1.25):
-    """The map's SDF at surface points against the reference's (see the module docstring);
-    returns whether both bounds hold."""
+def count_check(got, runs, floor):
+    """got against the runs' counts up to its frame (runs [R, k+1]): |got - mean| / mean within
+    max(floor, W_COUNT x the largest relative deviation of a run from its frame's mean so far)."""
+    runs = np.asarray(runs, np.float64)
+    m = np.maximum(runs.mean(0), 1.0)
+    e = float((np.abs(runs - m[None]) / m[None]).max())
+    lim = max(floor, W_COUNT * e)
+    return abs(float(got) - m[-1]) / m[-1] <= lim, (m[-1] * (1 - lim), m[-1] * (1 + lim))
+
+
+def surface_bounds(got, env):
+    """The map's SDF at the probes (got [P]) against the runs' (env [R, P]): (ok, message)."""
+    got, env = np.asarray(got, np.float64), np.asarray(env, np.float64)
+    means = np.abs(env).mean(1)
+    mine = float(np.abs(got).mean())
+    centre = env.mean(0)
+    diff = float(np.median(np.abs(got - centre)))
+    run_diff = float(np.median(np.abs(env - centre[None]), axis=1).max())
+    mean_lim = float(means.max()) + (W_SURFACE - 1.0) * float(means.max() - means.min()) + 1e-3
+    diff_lim = W_SURFACE * run_diff + 1e-3
+    msg = (f"mean |SDF| ours {mine:.4f} m, reference runs {np.round(means, 4)} (limit {mean_lim:.4f}); "
+           f"median |ours - runs' mean| {diff:.4f} m, runs' largest {run_diff:.4f} m (limit {diff_lim:.4f})")
+    return mine <= mean_lim and diff <= diff_lim, msg
+
+
+def pose_check(T, k, env):
+    """Pose T of frame k against pose_envelope(z) = env: (ok, distance, limit, angle, limit)."""
+    centre, Rmean, e_t, e_r = env
+    d_c = float(np.linalg.norm(T[:3, 3] - centre[k]))
+    a_c = _angle(T[:3, :3], Rmean[k])
+    tol_t, tol_r = max(0.01, W_POSE * float(e_t[k])), max(0.05, W_POSE * float(e_r[k]))
+    return d_c <= tol_t and a_c <= tol_r, d_c, tol_t, a_c, tol_r
+
+
+def _rot_mean(Rs):
+    """Chordal mean of rotation matrices [n, 3, 3]: the arithmetic mean projected onto SO(3)."""
+    U, _, Vt = np.linalg.svd(Rs.mean(0))
+    D = np.diag([1.0, 1.0, np.sign(np.linalg.det(U @ Vt))])
+    return U @ D @ Vt
+
+
+def _angle(A, B):
+    c = (np.trace(A.T @ B) - 1.0) / 2.0
+    return math.degrees(math.acos(min(1.0, max(-1.0, c))))
+
+
+def pose_envelope(z):
+    """Per frame: the runs' mean position c_k and mean rotation, and the running maxima e_t(k),
+    e_r(k) of any run's distance / angle from its frame's mean (module docstring)."""
+    P = np.asarray(z["env_hist_pose"], np.float64)             # [runs, frames, 4, 4]
+    c = P[:, :, :3, 3].mean(0)
+    Rm = np.stack([_rot_mean(P[:, k, :3, :3]) for k in range(P.shape[1])])
+    et = np.maximum.accumulate(np.linalg.norm(P[:, :, :3, 3] - c[None], axis=-1).max(0))
+    er = np.maximum.accumulate(np.array([max(_angle(P[r, k, :3, :3], Rm[k]) for r in range(P.shape[0]))
+                                         for k in range(P.shape[1])]))
+    return c, Rm, et, er
+
+
+def _surface_check(nm, dec, z, dev, probes_key, sdf_key):
+    """The map's SDF at surface points against the reference runs' (surface_bounds)."""
     probes = torch.from_numpy(z[probes_key]).to(dev)
     sdf, _, _, _, _ = P.query_sdf(nm, dec, probes, query_locally=False, want_grad=False, want_certainty=False)
-    got = sdf.cpu().numpy()
-    want = z[sdf_key]
-    mine, ref = float(np.abs(got).mean()), float(np.abs(want).mean())
-    diff = float(np.median(np.abs(got - want)))
-    spread = float(np.median(z["spread_abs_" + sdf_key]))
-    print(f"{sdf_key}: mean |SDF| ours {mine:.4f} m, reference {ref:.4f} m (1 thread "
-          f"{float(z['t1_mean_abs_' + sdf_key]):.4f}); median |ours - reference| {diff:.4f} m, reference spread "
-          f"{spread:.4f} m")
-    return mine <= ratio * ref + 1e-3 and diff <= 3 * spread + 1e-3
+    ok, msg = surface_bounds(sdf.cpu().numpy(), z["env_" + sdf_key])
+    print(f"{sdf_key}: {msg}")
+    return ok
 
 
 def _shell_count(pre, ours, ref, k, radius):
@@ -162,15 +226,18 @@ def test_slam_sequence_bitwise_reproducible(golden, dev):
         assert torch.equal(a, b), f"state {k} differs between two runs"
 
 
+@pytest.mark.parametrize("deterministic", [True, False], ids=["det", "atomic"])
 @pytest.mark.parametrize("fixture", ["slam_seq", "slam_seq100"])
-def test_slam_sequence_matches_reference(golden, dev, fixture):
+def test_slam_sequence_matches_reference(golden, dev, fixture, deterministic):
     """slam_seq: 30 frames of the accelerating street; slam_seq100: BASELINE configs[0]'s 100
     frames on the long street (synthetic.sequence_scene("long"); window filters at frames 9..99,
-    the pool's capacity discards at frame 99)."""
+    the pool's capacity discards at frame 99).  Bounds: the module docstring."""
     z = golden(fixture)
     frames = int(z["frames"])
     nm, dec, mapper, loop, replay, draws, scans = _sequence(z, dev, frames)
+    mapper.deterministic = deterministic
     cfg = nm.config
+    penv = pose_envelope(z)
     report, failures, our_poses = [], [], []
     # the whole pool as each window filter sees it (Mapper._pool_compact_many is called by the
     # filter with the pre-filter pools): the filter frames' pool counts are checked against the
@@ -208,48 +275,43 @@ def test_slam_sequence_matches_reference(golden, dev, fixture):
         assert replay.calls == int(z["hist_draws_after"][k]), f"frame {k}: draw stream out of step"
         counts = seen["counts"]
         want = tuple(int(z[f"hist_{n_}"][k]) for n_ in ("map_count", "local_count", "pool", "new"))
-        dt, dr = _pose_err(loop.cur_pose_ref, z["hist_pose"][k])
-        dt_true, _ = _pose_err(loop.cur_pose_ref, z["truth_poses"][k])
-        ref_true, _ = _pose_err(z["hist_pose"][k], z["truth_poses"][k])
-        our_poses.append(np.array(loop.cur_pose_ref, dtype=np.float64))
-        report.append((k, round(dt, 4), round(dr, 4), round(dt_true, 4), round(ref_true, 4), counts, want))
+        T = np.asarray(loop.cur_pose_ref, dtype=np.float64)
+        pose_ok, d_c, tol_t, a_c, tol_r = pose_check(T, k, penv)
+        dt_true, _ = _pose_err(T, z["truth_poses"][k])
+        ref_true = max(_pose_err(Pr, z["truth_poses"][k])[0] for Pr in z["env_hist_pose"][:, k])
+        our_poses.append(T)
+        report.append((k, round(d_c, 4), round(tol_t, 4), round(a_c, 4), round(tol_r, 4), round(dt_true, 4),
+                       round(ref_true, 4), counts, want))
         print("frame", *report[-1], flush=True)
-        # the reference's own 1- vs 8-thread runs differ by up to 3.3 cm by frame 13 and re-converge
-        # and diverge again afterwards: the spread up to frame k bounds how far two legitimate runs
-        # may be apart at frame k
-        tol_t = max(0.05, 3 * float(np.max(z["spread_pose_dt"][:k + 1])))
-        tol_r = max(0.1, 3 * float(np.max(z["spread_pose_dr"][:k + 1])))
-        expect(dt <= tol_t and dr <= tol_r, f"frame {k}: pose differs from the reference by {dt:.4f} m / {dr:.4f} deg")
-        # the reference itself drifts from the truth over the 30 frames (6-7 cm by frame 29); with
-        # the pose bound above this is implied (triangle inequality), checked for the report
-        expect(dt_true <= max(0.05, ref_true + tol_t), f"frame {k}: pose {dt_true:.4f} m from the ground truth")
+        expect(pose_ok,
+               f"frame {k}: pose {d_c:.4f} m / {a_c:.4f} deg from the runs' mean (limits {tol_t:.4f} m / {tol_r:.4f} deg)")
+        # implied by the pose bound (triangle inequality); checked for the report
+        expect(dt_true <= ref_true + 2 * tol_t, f"frame {k}: pose {dt_true:.4f} m from the ground truth")
         filt = k % int(cfg.pool_filter_freq) == int(cfg.pool_filter_freq) - 1   # the pool's window filter ran
-        for name, g, w, rel in zip(("map_count", "local_count", "pool", "new"), counts, want, (0.01, 0.01, 0.001, 0.15)):
-            # the spread up to frame k, as for the pose (a count difference persists: points
-            # inserted differently stay in the map)
-            rel = max(rel, 3 * float(np.max(z[f"spread_rel_{name}"][:k + 1])))
-            if name == "pool" and filt:
+        for name, g, w in zip(("map_count", "local_count", "pool", "new"), counts, want):
+            ok, (lo, hi) = count_check(g, z[f"env_hist_{name}"][:, :k + 1], COUNT_FLOORS[name])
+            if name == "pool" and filt and not ok:
                 # the filter keeps the samples within window_radius of the CURRENT position: beyond
-                # the difference carried in from the previous frame, the count can differ only by
-                # samples that lie, in our pool, within their displacement bound of the sphere
-                prev = report[-2][5][2] - report[-2][6][2] if k > 0 else 0
+                # the difference carried in from the previous frame, the count can differ from the
+                # stored run's only by samples that lie, in our pool, within their displacement
+                # bound of the sphere
+                prev = report[-2][7][2] - report[-2][8][2] if k > 0 else 0
                 lim = abs(prev) + _shell_count(pre, our_poses, z["hist_pose"], k, float(cfg.window_radius))
                 print(f"frame {k}: pool {g} vs {w}: |diff| {abs(g - w)}, geometric bound {lim}", flush=True)
-                expect(abs(g - w) <= max(lim, rel * w), f"frame {k}: pool {g} vs reference {w} (bound {lim})")
-                continue
-            expect(_within(g, w, rel), f"frame {k}: {name} {g} vs reference {w} (rel {rel:.4f})")
+                ok = abs(g - w) <= lim
+            expect(ok, f"frame {k}: {name} {g} outside the reference runs' envelope [{lo:.0f}, {hi:.0f}]")
         if k == 0:
             expect(_surface_check(nm, dec, z, dev, "f0_surface_probes", "f0_surface_sdf"), "frame 0: surface")
-    print("frame, |dt| m, |dR| deg vs reference, |dt| m vs truth (ours, reference), (map, local, pool, new) ours / "
-          "reference")
+    print("frame, |t - runs' mean| m, limit, angle deg, limit, |dt| m vs truth (ours, runs' worst), "
+          "(map, local, pool, new) ours / stored run")
     for r in report:
         print(*r)
-    # the map at the end of the loop: mean |SDF| at the probes (placed by the TRUE poses) at most
-    # 1.25 x the reference's + 1 mm
     expect(_surface_check(nm, dec, z, dev, "surface_probes", "end_surface_sdf"), "end of run: surface")
     assert not failures, failures
     # pin_slam.py:366-367: merge + prune
-    if bool(z["merged_raises"]):
+    raises = np.asarray(z["env_merged_raises"], bool)
+    assert raises.all() or not raises.any(), "the reference runs disagree on the merge"
+    if raises.all():
         with pytest.raises(IndexError):
             nm.recreate_hash(None, None, False, False)
     else:
@@ -258,11 +320,13 @@ def test_slam_sequence_matches_reference(golden, dev, fixture):
         nm.prune_map(cfg.max_prune_certainty)
         pruned = merged - nm.count()
         assert pruned == 0 or pruned > 100           # prune_map removes points only above 100 candidates
-        # the map-count bound of the last frame (max(1 %, 3 x the running count spread))
-        rel = max(0.01, 3 * float(np.max(z["spread_rel_map_count"])))
-        if int(z["merged_map_count"]) == int(z["end_map_count"]) and pruned > 0:
-            # the reference pruned nothing (<= 100 candidates: its own cut-off), this run > 100: the
-            # counts before the prune are the comparable ones
-            assert _within(merged, int(z["merged_map_count"]), rel)
+        env_merged, env_end = np.asarray(z["env_merged_map_count"]), np.asarray(z["env_end_map_count"])
+        # the end-of-run map count bound, one frame further (the runs' merged sizes as a last frame)
+        runs = np.concatenate([np.asarray(z["env_hist_map_count"]), env_merged[:, None]], 1)
+        if (env_merged == env_end).all() and pruned > 0:
+            # the reference runs pruned nothing (<= 100 candidates: its own cut-off), this run > 100:
+            # the counts before the prune are the comparable ones
+            ok, lim = count_check(merged, runs, COUNT_FLOORS["map_count"])
         else:
-            assert _within(nm.count(), int(z["merged_map_count"]), rel)
+            ok, lim = count_check(nm.count(), runs, COUNT_FLOORS["map_count"])
+        assert ok, f"merged map {merged} / {nm.count()} outside the reference runs' envelope {lim}"
