@@ -136,184 +136,282 @@ __device__ __forceinline__ void topk_pair_merge(TopK& tk, int ph) {
 // row (aten SortingKernel), and keeps the first k.  Where two VALID candidates have exactly the
 // same distance the order std::sort leaves them in is not cell order: it depends on the whole
 // row (median-of-three pivots, partitions, the final insertion sort).  Lattice-quantised scans
-// make exact ties common enough to matter: taking them in cell order (a stable sort) prefers the
-// cells of lower offsets and biased the trained map measurably.  The
-// streaming top-k above keeps cell order; a query whose kept list has a tie -- between two kept
-// entries, or between the k-th kept and the best one left out -- is redone: its whole row of Kc
-// (distance, payload) pairs in cell order, 9e3 for the invalid ones as in the reference, sorted
-// by a restatement of std::sort, and the first entries taken.
-constexpr int kRefSortMax = 128;   // rows up to this many cells (every reference config: Kc <= 93)
+// make exact ties frequent enough to matter: taking them in cell order (a stable sort) prefers
+// the cells of lower offsets.  The streaming top-k above keeps cell order;
+// a query whose kept list has a tie is redone in the reference's order by its WAVE
+// (resolve_ties): the row of Kc (distance, payload) pairs, 9e3 for the invalid ones as in the
+// reference, held two entries per lane in registers (no private memory, no LDS), sorted by a
+// wave-parallel restatement of std::sort, and its first entries handed to the query's lane.
+//
+// Which ties: a tie at the k-th place (between the k-th kept candidate and the first one left
+// out) changes the neighbour SET -- the hot kernels resolve those (kTieBoundary); ties inside the
+// kept list only change the order of the neighbours, i.e. the summation order of the IDW sums,
+// which matters where the order is an output (query_feature's per-neighbour layout, kTieAll).
+constexpr int kRefSortMax = 128;   // rows up to this many cells (Kc <= 125 with num_nei_cells 2)
+enum TieScope { kTieBoundary = 0, kTieAll = 1 };
 
-__device__ __forceinline__ bool topk_tied(const TopK& tk, int nn_k, int nn) {
+#ifndef PIN_REF_TIES
+#define PIN_REF_TIES 1   // 0: keep cell order for equal distances (experiment switch)
+#endif
+
+__device__ __forceinline__ bool topk_tied(const TopK& tk, int nn_k, int nn, TieScope scope) {
     bool t = false;
+    if (scope == kTieAll) {
 #pragma unroll
-    for (int j = 0; j + 1 < kK; ++j)
-        t = t || (j + 1 <= nn_k && j + 1 < nn && tk.d[j] == tk.d[j + 1]);
-    if (nn_k >= kK) t = t || (nn > kK && tk.rej == tk.d[kK - 1]);
+        for (int j = 0; j + 1 < kK; ++j)
+            t = t || (j + 1 < nn_k && j + 1 < nn && tk.d[j] == tk.d[j + 1]);
+    }
+    // the k-th place: against the (k+1)-th candidate, kept in the list or (k == kK) the best
+    // one pushed out of it
+    if (nn_k < kK) {
+#pragma unroll
+        for (int j = 1; j < kK; ++j)
+            t = t || (j == nn_k && nn > nn_k && tk.d[j - 1] == tk.d[j]);
+    } else {
+        t = t || (nn > kK && tk.rej == tk.d[kK - 1]);
+    }
     return t;
 }
 
-// One row of the reference's k-NN sort, in private memory: keys (distance or 9e3) and payloads
-struct RefRow {
-    float k[kRefSortMax];
-    int g[kRefSortMax];
-    __device__ __forceinline__ bool less(int a, int b) const { return k[a] < k[b]; }
-    __device__ __forceinline__ void swap(int a, int b) {
-        const float tk = k[a];
-        k[a] = k[b];
-        k[b] = tk;
-        const int tg = g[a];
-        g[a] = g[b];
-        g[b] = tg;
-    }
-    // libstdc++ __adjust_heap + __push_heap on [f, f + len), hole at h, value (vk, vg)
-    __device__ void adjust_heap(int f, int h, int len, float vk, int vg) {
-        const int top = h;
-        int c = h;
-        while (c < (len - 1) / 2) {
-            c = 2 * (c + 1);
-            if (k[f + c] < k[f + c - 1]) --c;
-            k[f + h] = k[f + c];
-            g[f + h] = g[f + c];
-            h = c;
-        }
-        if ((len & 1) == 0 && c == (len - 2) / 2) {
-            c = 2 * (c + 1);
-            k[f + h] = k[f + c - 1];
-            g[f + h] = g[f + c - 1];
-            h = c - 1;
-        }
-        int parent = (h - 1) / 2;
-        while (h > top && k[f + parent] < vk) {
-            k[f + h] = k[f + parent];
-            g[f + h] = g[f + parent];
-            h = parent;
-            parent = (h - 1) / 2;
-        }
-        k[f + h] = vk;
-        g[f + h] = vg;
-    }
-    // __partial_sort(first, last, last): __make_heap, then __sort_heap
-    __device__ void heap_sort(int f, int l) {
-        const int len = l - f;
-        if (len >= 2) {
-            for (int parent = (len - 2) / 2;; --parent) {
-                adjust_heap(f, parent, len, k[f + parent], g[f + parent]);
-                if (parent == 0) break;
-            }
-        }
-        while (l - f > 1) {
-            --l;
-            const float vk = k[l];
-            const int vg = g[l];
-            k[l] = k[f];
-            g[l] = g[f];
-            adjust_heap(f, 0, l - f, vk, vg);
-        }
-    }
-    __device__ void unguarded_linear_insert(int i) {
-        const float vk = k[i];
-        const int vg = g[i];
-        int j = i - 1;
-        while (vk < k[j]) {
-            k[i] = k[j];
-            g[i] = g[j];
-            i = j;
-            --j;
-        }
-        k[i] = vk;
-        g[i] = vg;
-    }
-    __device__ void insertion_sort(int f, int l) {
-        if (f == l) return;
-        for (int i = f + 1; i < l; ++i) {
-            if (k[i] < k[f]) {
-                const float vk = k[i];
-                const int vg = g[i];
-                for (int j = i; j > f; --j) {
-                    k[j] = k[j - 1];
-                    g[j] = g[j - 1];
-                }
-                k[f] = vk;
-                g[f] = vg;
-            } else {
-                unguarded_linear_insert(i);
-            }
-        }
-    }
-    // std::sort(first, first + n, less): __introsort_loop with depth 2 floor(log2 n) and runs of
-    // 16, then __final_insertion_sort.  The recursion of __introsort_loop on the right part is a
-    // stack of disjoint segments (the order they are finished in does not change the result).
-    __device__ void sort(int n) {
-        if (n < 2) return;
-        int sf[16], sl[16], sd[16];
-        int top = 0;
-        sf[0] = 0;
-        sl[0] = n;
-        sd[0] = 2 * (31 - __clz(n));
-        top = 1;
-        while (top > 0) {
-            --top;
-            int f = sf[top], l = sl[top], depth = sd[top];
-            while (l - f > 16) {
-                if (depth == 0) {
-                    heap_sort(f, l);
-                    break;
-                }
-                --depth;
-                // __move_median_to_first(f, f + 1, mid, l - 1)
-                const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
-                if (less(a, b)) {
-                    if (less(b, c)) swap(f, b);
-                    else if (less(a, c)) swap(f, c);
-                    else swap(f, a);
-                } else if (less(a, c)) swap(f, a);
-                else if (less(b, c)) swap(f, c);
-                else swap(f, b);
-                // __unguarded_partition(f + 1, l, f)
-                int lo = f + 1, hi = l;
-                for (;;) {
-                    while (less(lo, f)) ++lo;
-                    --hi;
-                    while (less(f, hi)) --hi;
-                    if (!(lo < hi)) break;
-                    swap(lo, hi);
-                    ++lo;
-                }
-                if (top < 16) {   // __introsort_loop(cut, last, depth); at most ~2 log2 n pending
-                    sf[top] = lo;
-                    sl[top] = l;
-                    sd[top] = depth;
-                    ++top;
-                } else {
-                    heap_sort(lo, l);   // unreachable for n <= kRefSortMax
-                }
-                l = lo;
-            }
-        }
-        if (n > 16) {
-            insertion_sort(0, 16);
-            for (int i = 16; i < n; ++i) unguarded_linear_insert(i);
-        } else {
-            insertion_sort(0, n);
-        }
-    }
+// A row of up to 128 (key, payload) entries held by the wave: lane l has entry l in (ka, ga) and
+// entry l + 64 in (kb, gb).  Entry reads and writes at a wave-uniform position use readlane /
+// a lane select; permutations use ds_bpermute.  All 64 lanes must be active.
+struct WaveRow {
+    float ka, kb;
+    int ga, gb;
 };
 
-// The reference's k first entries of a tied query (see above); src.ref_row fills the row.
-template <class Src>
-__device__ __forceinline__ void resolve_ties(const Src& src, float qx, float qy, float qz, int nn_k, int nn,
-                                             TopK& tk) {
-    if (!topk_tied(tk, nn_k, nn)) return;
-    RefRow r;
-    const int n = src.ref_row(qx, qy, qz, r);
-    if (n > kRefSortMax) return;   // larger neighbourhoods keep cell order (no reference config)
-    r.sort(n);
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ float rdl_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float row_key(const WaveRow& r, int p) { return p < 64 ? rdl_f(r.ka, p) : rdl_f(r.kb, p - 64); }
+__device__ __forceinline__ int row_pay(const WaveRow& r, int p) {
+    return p < 64 ? __builtin_amdgcn_readlane(r.ga, p) : __builtin_amdgcn_readlane(r.gb, p - 64);
+}
+__device__ __forceinline__ void row_set(WaveRow& r, int p, float k, int g) {
+    const int lane = wave_lane();
+    const bool a = p < 64 && lane == p, b = p >= 64 && lane == p - 64;
+    r.ka = a ? k : r.ka;
+    r.ga = a ? g : r.ga;
+    r.kb = b ? k : r.kb;
+    r.gb = b ? g : r.gb;
+}
+__device__ __forceinline__ void row_swap(WaveRow& r, int p, int q) {
+    const float kp = row_key(r, p), kq = row_key(r, q);
+    const int gp = row_pay(r, p), gq = row_pay(r, q);
+    row_set(r, p, kq, gq);
+    row_set(r, q, kp, gp);
+}
+// new entry p = old entry src(p): sa for the lane's entry in .a, sb for its entry in .b
+__device__ __forceinline__ void row_gather(WaveRow& r, int sa, int sb) {
+    const float ka_a = __shfl(r.ka, sa & 63), kb_a = __shfl(r.kb, sa & 63);
+    const int ga_a = __shfl(r.ga, sa & 63), gb_a = __shfl(r.gb, sa & 63);
+    const float ka_b = __shfl(r.ka, sb & 63), kb_b = __shfl(r.kb, sb & 63);
+    const int ga_b = __shfl(r.ga, sb & 63), gb_b = __shfl(r.gb, sb & 63);
+    r.ka = sa < 64 ? ka_a : kb_a;
+    r.ga = sa < 64 ? ga_a : gb_a;
+    r.kb = sb < 64 ? ka_b : kb_b;
+    r.gb = sb < 64 ? ga_b : gb_b;
+}
+
+// 128-bit position masks (lo: entries 0..63, hi: 64..127)
+__device__ __forceinline__ uint64_t mask_upto(int b) {   // bits 0..b (b in [-1, 63])
+    return b < 0 ? 0ull : (b >= 63 ? ~0ull : ((2ull << b) - 1ull));
+}
+__device__ __forceinline__ int count_upto(uint64_t lo, uint64_t hi, int p) {   // set bits at positions <= p
+    return p < 64 ? __popcll(lo & mask_upto(p)) : __popcll(lo) + __popcll(hi & mask_upto(p - 64));
+}
+// position of the t-th set bit from the low end (t >= 1), 128 if there is none
+__device__ __forceinline__ int select_low(uint64_t lo, uint64_t hi, int t) {
+    uint64_t m = lo;
+    int base = 0;
+    const int cl = __popcll(lo);
+    if (t > cl) {
+        t -= cl;
+        m = hi;
+        base = 64;
+        if (t > __popcll(hi)) return 128;
+    }
+    int pos = 0;   // invariant: fewer than t set bits below pos
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1)
+        if (__popcll(m & mask_upto(pos + s - 1)) < t) pos += s;
+    return base + pos;
+}
+// position of the u-th set bit from the high end (u >= 1), -1 if there is none
+__device__ __forceinline__ int select_high(uint64_t lo, uint64_t hi, int u) {
+    const int tot = __popcll(lo) + __popcll(hi);
+    return u > tot ? -1 : select_low(lo, hi, tot - u + 1);
+}
+
+// libstdc++ __unguarded_partition(first + 1, last, first) on entries [f, l) with the pivot at f,
+// all swaps at once: with L_t the t-th entry from the left that is not below the pivot and R_t
+// the t-th from the right that is not above it (both in the row as it was), the sequential scans
+// swap L_t with R_t for every t with L_t < R_t (s pairs: their positions never overlap, and each
+// scan only crosses entries the earlier swaps left untouched) and return min(L_{s+1}, R_s)
+// (L_1 when s = 0).  Returns the cut.
+__device__ __forceinline__ int wave_partition(WaveRow& r, int f, int l) {
+    const int pa = wave_lane(), pb = pa + 64;
+    const float pv = row_key(r, f);
+    const bool ina = pa > f && pa < l, inb = pb > f && pb < l;
+    const bool gea = ina && !(r.ka < pv), geb = inb && !(r.kb < pv);
+    const bool lea = (ina || pa == f) && !(pv < r.ka), leb = (inb || pb == f) && !(pv < r.kb);
+    const uint64_t geLo = __ballot(gea), geHi = __ballot(geb);
+    const uint64_t leLo = __ballot(lea), leHi = __ballot(leb);
+    const int leTot = __popcll(leLo) + __popcll(leHi);
+    // left rank of a left stop, its partner R_t; swaps happen for L_t < R_t
+    const int ta = count_upto(geLo, geHi, pa), tb = count_upto(geLo, geHi, pb);
+    const int rta = gea ? select_high(leLo, leHi, ta) : -1, rtb = geb ? select_high(leLo, leHi, tb) : -1;
+    const bool swa = gea && pa < rta, swb = geb && pb < rtb;
+    const int s = __popcll(__ballot(swa)) + __popcll(__ballot(swb));
+    // right rank of a right stop (entries at or above it), its partner L_u
+    const int ua = leTot - count_upto(leLo, leHi, pa - 1), ub = leTot - count_upto(leLo, leHi, pb - 1);
+    const bool rsa = !swa && lea && ua <= s, rsb = !swb && leb && ub <= s;
+    const int sa = swa ? rta : (rsa ? select_low(geLo, geHi, ua) : pa);
+    const int sb = swb ? rtb : (rsb ? select_low(geLo, geHi, ub) : pb);
+    row_gather(r, sa, sb);
+    int cut = select_low(geLo, geHi, s + 1);
+    if (s > 0) {
+        const int rs = select_high(leLo, leHi, s);
+        cut = cut < rs ? cut : rs;
+    }
+    if (cut > l) cut = l;   // unreachable: the median of three guarantees a left stop
+    return __builtin_amdgcn_readfirstlane(cut);
+}
+
+// libstdc++ __adjust_heap + __push_heap / __make_heap + __sort_heap on [f, l): the depth-limit
+// fallback, run entry by entry at wave-uniform positions (rare: needs a badly split row)
+__device__ void wave_adjust_heap(WaveRow& r, int f, int h, int len, float vk, int vg) {
+    const int top = h;
+    int c = h;
+    while (c < (len - 1) / 2) {
+        c = 2 * (c + 1);
+        if (row_key(r, f + c) < row_key(r, f + c - 1)) --c;
+        row_set(r, f + h, row_key(r, f + c), row_pay(r, f + c));
+        h = c;
+    }
+    if ((len & 1) == 0 && c == (len - 2) / 2) {
+        c = 2 * (c + 1);
+        row_set(r, f + h, row_key(r, f + c - 1), row_pay(r, f + c - 1));
+        h = c - 1;
+    }
+    int parent = (h - 1) / 2;
+    while (h > top && row_key(r, f + parent) < vk) {
+        row_set(r, f + h, row_key(r, f + parent), row_pay(r, f + parent));
+        h = parent;
+        parent = (h - 1) / 2;
+    }
+    row_set(r, f + h, vk, vg);
+}
+__device__ void wave_heap_sort(WaveRow& r, int f, int l) {
+    const int len = l - f;
+    if (len >= 2) {
+        for (int parent = (len - 2) / 2;; --parent) {
+            wave_adjust_heap(r, f, parent, len, row_key(r, f + parent), row_pay(r, f + parent));
+            if (parent == 0) break;
+        }
+    }
+    while (l - f > 1) {
+        --l;
+        const float vk = row_key(r, l);
+        const int vg = row_pay(r, l);
+        row_set(r, l, row_key(r, f), row_pay(r, f));
+        wave_adjust_heap(r, f, 0, l - f, vk, vg);
+    }
+}
+
+// std::sort(row, row + n) (libstdc++: __introsort_loop with depth 2 floor(log2 n) and runs of 16,
+// then __final_insertion_sort), then the first kK entries.  The loop's recursion on the right
+// part is a stack of disjoint segments held one per lane (the order segments are finished in does
+// not change the result).  The final insertion sort moves an entry left past strictly greater
+// keys only, so it is the stable sort of the row the loop leaves: entry p lands at
+// #(keys < k_p) + #(equal keys before p).  out_d / out_g: the k first keys / payloads, uniform.
+__device__ void wave_ref_sort(WaveRow& r, int n, float (&out_d)[kK], int (&out_g)[kK]) {
+    const int lane = wave_lane();
+    int sF = 0, sL = 0, sD = 0;   // segment stack, entry e in lane e
+    int top = 0;
+    if (n > 16) {
+        sF = lane == 0 ? 0 : sF;
+        sL = lane == 0 ? n : sL;
+        sD = lane == 0 ? 2 * (31 - __clz(n)) : sD;
+        top = 1;
+    }
+    while (top > 0) {
+        --top;
+        int f = __builtin_amdgcn_readlane(sF, top), l = __builtin_amdgcn_readlane(sL, top);
+        int depth = __builtin_amdgcn_readlane(sD, top);
+        while (l - f > 16) {
+            if (depth == 0) {
+                wave_heap_sort(r, f, l);
+                break;
+            }
+            --depth;
+            // __move_median_to_first(f, f + 1, mid, l - 1)
+            const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+            const float ka = row_key(r, a), kb = row_key(r, b), kc = row_key(r, c);
+            const int m = ka < kb ? (kb < kc ? b : (ka < kc ? c : a)) : (ka < kc ? a : (kb < kc ? c : b));
+            row_swap(r, f, m);
+            const int cut = wave_partition(r, f, l);
+            sF = lane == top ? cut : sF;   // __introsort_loop(cut, last, depth)
+            sL = lane == top ? l : sL;
+            sD = lane == top ? depth : sD;
+            ++top;
+            l = cut;
+        }
+    }
+    const int pa = lane, pb = lane + 64;
+    int ra = 0, rb = 0;
+    for (int q = 0; q < n; ++q) {
+        const float kq = row_key(r, q);
+        ra += (kq < r.ka || (kq == r.ka && q < pa)) ? 1 : 0;
+        rb += (kq < r.kb || (kq == r.kb && q < pb)) ? 1 : 0;
+    }
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
-        const bool in = j < n && r.k[j] < kInvalidDist2;
-        tk.d[j] = in ? r.k[j] : kInvalidDist2;
-        tk.g[j] = in ? r.g[j] : -1;
+        const uint64_t ma = __ballot(pa < n && ra == j), mb = __ballot(pb < n && rb == j);
+        const bool hasA = ma != 0ull, hasB = mb != 0ull;
+        const int src = hasA ? (int)__builtin_ctzll(ma) : (hasB ? (int)__builtin_ctzll(mb) + 64 : -1);
+        const float d = src >= 0 ? row_key(r, src) : kInvalidDist2;
+        const int g = src >= 0 ? row_pay(r, src) : -1;
+        const bool in = d < kInvalidDist2;
+        out_d[j] = in ? d : kInvalidDist2;
+        out_g[j] = in ? g : -1;
+    }
+}
+
+// The reference's k first entries for every lane of the wave whose list has a tie in `scope`;
+// src.ref_cell(q, c, key, payload) gives cell c's candidate (9e3 / -1 where the reference has
+// idx -1).  Called by ALL lanes of the wave at the same point (the kernels run whole waves;
+// a wave with inactive lanes keeps cell order, which only the last partial wave of a launch can
+// be, and only when a rank's batch is not a multiple of 64).
+template <class Src>
+__device__ __forceinline__ void resolve_ties(const Src& src, float qx, float qy, float qz, int nn_k, int nn,
+                                             TopK& tk, TieScope scope = kTieBoundary) {
+    if (!PIN_REF_TIES) return;
+    uint64_t m = __ballot(topk_tied(tk, nn_k, nn, scope));
+    if (m == 0ull) return;
+    if (__ballot(true) != ~0ull) return;
+    const int n = src.num_cells();
+    if (n > kRefSortMax) return;   // larger neighbourhoods keep cell order
+    const int lane = wave_lane();
+    while (m) {
+        const int L = (int)__builtin_ctzll(m);
+        m &= m - 1ull;
+        const float x = rdl_f(qx, L), y = rdl_f(qy, L), z = rdl_f(qz, L);
+        WaveRow r;
+        src.ref_cell(x, y, z, lane, n, r.ka, r.ga);
+        src.ref_cell(x, y, z, lane + 64, n, r.kb, r.gb);
+        float d[kK];
+        int g[kK];
+        wave_ref_sort(r, n, d, g);
+        if (lane == L) {
+#pragma unroll
+            for (int j = 0; j < kK; ++j) {
+                tk.d[j] = d[j];
+                tk.g[j] = g[j];
+            }
+        }
     }
 }
 
@@ -370,24 +468,21 @@ struct HashSource {
         }
         return nn;
     }
-    // the whole row of the reference's sort (resolve_ties): per neighbour cell in order, the
-    // candidate's distance and payload, 9e3 / -1 where the reference has idx -1; returns Kc
-    __device__ int ref_row(float qx, float qy, float qz, RefRow& r) const {
+    // one cell of the reference's sort row (resolve_ties): cell c's candidate distance and
+    // payload, 9e3 / -1 where the reference has idx -1 (c >= n: an unused entry)
+    __device__ __forceinline__ int num_cells() const { return h.num_cells; }
+    __device__ __forceinline__ void ref_cell(float qx, float qy, float qz, int c, int n, float& k, int& g) const {
         const float4* __restrict__ rec = (const float4*)p.records;
         const uint32_t B = (uint32_t)h.buffer_size;
         const uint32_t base = base_slot(qx, qy, qz, h.resolution, h.buffer_size);
-        const int Kc = h.num_cells;
-        for (int c = 0; c < Kc && c < kRefSortMax; ++c) {
-            uint32_t s = base + (uint32_t)h.cells[c];
-            s = s >= B ? s - B : s;
-            const int gi = h.table[s];
-            const float4 v = rec[gi > 0 ? gi : 0];
-            const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
-            const bool ok = gi >= 0 && __float_as_int(v.w) != -1 && d2 <= h.max_valid_dist2;
-            r.k[c] = ok ? d2 : kInvalidDist2;
-            r.g[c] = ok ? gi : -1;
-        }
-        return Kc;
+        uint32_t s = base + (uint32_t)h.cells[c < n ? c : 0];
+        s = s >= B ? s - B : s;
+        const int gi = c < n ? h.table[s] : -1;
+        const float4 v = rec[gi > 0 ? gi : 0];
+        const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
+        const bool ok = gi >= 0 && __float_as_int(v.w) != -1 && d2 <= h.max_valid_dist2;
+        k = ok ? d2 : kInvalidDist2;
+        g = ok ? gi : -1;
     }
     __device__ __forceinline__ float4 record(int pay) const { return ((const float4*)p.records)[pay > 0 ? pay : 0]; }
     __device__ __forceinline__ void features(int pay, int64_t id, float4& f0, float4& f1) const {
@@ -737,9 +832,10 @@ struct GridSource {
         }
     }
 
-    // the whole row of the reference's sort (resolve_ties): per neighbour cell in order, the
-    // candidate's distance and payload, 9e3 / -1 where the reference has idx -1; returns Kc
-    __device__ int ref_row(float qx, float qy, float qz, RefRow& r) const {
+    // one cell of the reference's sort row (resolve_ties): cell c's candidate distance and
+    // payload, 9e3 / -1 where the reference has idx -1 (c >= n: an unused entry)
+    __device__ __forceinline__ int num_cells() const { return gr.num_cells; }
+    __device__ __forceinline__ void ref_cell(float qx, float qy, float qz, int c, int n, float& k, int& g) const {
         const uint4* __restrict__ bricks = (const uint4*)gr.bricks;
         const float4* __restrict__ crec = (const float4*)gr.crec;
         const float res = gr.resolution, maxd2 = gr.max_valid_dist2;
@@ -747,26 +843,22 @@ struct GridSource {
         const int lx = rel(qx, res, gr.dims.ox, ex);
         const int ly = rel(qy, res, gr.dims.oy, ey);
         const int lz = rel(qz, res, gr.dims.oz, ez);
-        const int Kc = gr.num_cells;
-        for (int c = 0; c < Kc && c < kRefSortMax; ++c) {
-            const int of = gr.offsets[c];
-            const int cx = lx + ((of & 255) - 128);
-            const int cy = ly + (((of >> 8) & 255) - 128);
-            const int cz = lz + (((of >> 16) & 255) - 128);
-            const bool in = (unsigned)cx < (unsigned)ex && (unsigned)cy < (unsigned)ey && (unsigned)cz < (unsigned)ez;
-            const uint4 w = bricks[in ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * gr.dims.nbx + (cx >> 2) : 0];
-            const int bit = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
-            const uint64_t bits = ((uint64_t)w.y << 32) | w.x;
-            const bool set = in && ((bits >> bit) & 1ull);
-            const int ci = set ? (int)(w.z + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull))) : -1;
-            const float4 v = crec[ci > 0 ? ci : 0];
-            const int id = __float_as_int(v.w);
-            const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
-            const bool ok = ci >= 0 && id != -1 && d2 <= maxd2;
-            r.k[c] = ok ? d2 : kInvalidDist2;
-            r.g[c] = ok ? (IDP ? (id & kIdMask) : ci) : -1;
-        }
-        return Kc;
+        const int of = gr.offsets[c < n ? c : 0];
+        const int cx = lx + ((of & 255) - 128);
+        const int cy = ly + (((of >> 8) & 255) - 128);
+        const int cz = lz + (((of >> 16) & 255) - 128);
+        const bool in = c < n && (unsigned)cx < (unsigned)ex && (unsigned)cy < (unsigned)ey && (unsigned)cz < (unsigned)ez;
+        const uint4 w = bricks[in ? ((cz >> 2) * gr.dims.nby + (cy >> 2)) * gr.dims.nbx + (cx >> 2) : 0];
+        const int bit = ((cx & 3) << 4) | ((cy & 3) << 2) | (cz & 3);
+        const uint64_t bits = ((uint64_t)w.y << 32) | w.x;
+        const bool set = in && ((bits >> bit) & 1ull);
+        const int ci = set ? (int)(w.z + (uint32_t)__popcll(bits & ((1ull << bit) - 1ull))) : -1;
+        const float4 v = crec[ci > 0 ? ci : 0];
+        const int id = __float_as_int(v.w);
+        const float d2 = dist2(v.x, v.y, v.z, qx, qy, qz);
+        const bool ok = ci >= 0 && id != -1 && d2 <= maxd2;
+        k = ok ? d2 : kInvalidDist2;
+        g = ok ? (IDP ? (id & kIdMask) : ci) : -1;
     }
 
     // Per-cell scan (any window): CH cell lookups back to back, then CH record gathers.

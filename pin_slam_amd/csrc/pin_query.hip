@@ -366,7 +366,7 @@ __device__ __forceinline__ void query_sdf_body(const Src& src, const PinPoints& 
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
-    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's neighbour set at equal distances
 #if defined(PIN_PROF_STAGE) && PIN_PROF_STAGE == 1
     // profiling variant: candidate scan only (the top-k kept live through one output)
     if (i >= 0) {
@@ -392,7 +392,7 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
     __shared__ uint4 s_pk[MF ? kPkBytes / 16 : 1];
     const MlpW mw = stage_decoder<MF>(m, s_mlp, s_pk);
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (MF ? (t & ~(int64_t)63) >= n : t >= n) return;
+    if ((t & ~(int64_t)63) >= n) return;   // whole waves (the MFMA decoder, resolve_ties): lanes past n run query 0
     const int64_t i = t < n ? t : -1, iq = t < n ? t : 0;
     const HashSource src(h, p);
     query_sdf_body<WF, PGO, GRAD, HashSource, MF>(src, p, mw, q[3 * iq], q[3 * iq + 1], q[3 * iq + 2], i, nn_k,
@@ -427,14 +427,9 @@ k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float
 #if PIN_MLP_MFMA
     __shared__ float s_xs[kBlock / 64][64 * kWRow];
     if (!WF && !MF) mw.xs = s_xs[threadIdx.x >> 6];
-    if (MF || !WF) {   // the MFMA decoders need whole waves: lanes past n run query 0 and write nothing
-#else
-    if (MF) {
 #endif
-        if ((t & ~(int64_t)63) >= n) return;
-    } else if (t >= n) {
-        return;
-    }
+    // whole waves (the MFMA decoders, resolve_ties): lanes past n run query 0 and write nothing
+    if ((t & ~(int64_t)63) >= n) return;
     const int64_t tt = t < n ? t : 0;
     float qx, qy, qz;
     int64_t i;
@@ -748,7 +743,7 @@ __device__ __forceinline__ void query_feature_body(const Src& src, const PinPoin
     TopK tk;
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
-    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk, kTieAll);   // the reference's neighbour order (layout)
     Neighbours nb;
     load_topk(src, p, tk, nn, nn_k, qx, qy, qz, nb);
     const float cert = (cert_out && p.certainties) ? gather_certainty(src, nb) : 0.f;
@@ -795,8 +790,9 @@ __global__ void __launch_bounds__(kBlock)
 k_query_feature_fwd(const PinHash h, const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k,
                     float* __restrict__ feat, float* __restrict__ weights, int64_t* __restrict__ nn_counts,
                     float* __restrict__ cert_out, int* __restrict__ ids, int* __restrict__ gids) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~(int64_t)63) >= n) return;   // whole waves (resolve_ties): lanes past n redo query n-1
+    const int64_t i = i0 < n ? i0 : n - 1;   // (identical values to the same addresses)
     const HashSource src(h, p);
     query_feature_body<WF, PGO>(src, p, q, i, nn_k, feat, weights, nn_counts, cert_out, ids, gids);
 }
@@ -806,8 +802,9 @@ __global__ void __launch_bounds__(kBlock)
 k_query_feature_fwd_grid(const PinGrid g, const PinPoints p, const float* __restrict__ q, int64_t n, int nn_k,
                          float* __restrict__ feat, float* __restrict__ weights, int64_t* __restrict__ nn_counts,
                          float* __restrict__ cert_out, int* __restrict__ ids, int* __restrict__ gids) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~(int64_t)63) >= n) return;   // whole waves (resolve_ties): lanes past n redo query n-1
+    const int64_t i = i0 < n ? i0 : n - 1;   // (identical values to the same addresses)
     const GridSource<false> src(g, p);
     query_feature_body<WF, PGO>(src, p, q, i, nn_k, feat, weights, nn_counts, cert_out, ids, gids);
 }

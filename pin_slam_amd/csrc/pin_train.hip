@@ -119,7 +119,7 @@ __device__ __forceinline__ void train_forward_body(const Src& src, const PinPoin
     // pair mode: both lanes of the pair hold the row's neighbours; the even lane writes its outputs
     const bool writer = live && (!PAIR || !(threadIdx.x & 1));
     const int nn_k = c.nn_k;
-    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's neighbour set at equal distances
     float u[kK];
     float S = 0.f;
 #pragma unroll
@@ -360,7 +360,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     float cw[kK];
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if (MF ? (t & ~(int64_t)63) < rows : t < rows) {
+    if ((t & ~(int64_t)63) < rows) {   // whole waves (the MFMA decoder, resolve_ties); live: t < rows
         const HashSource src(h, p);
         train_forward_body<WF, HashSource, MF, DX>(src, p, mw, coord, ts, c, t, st, cid, cw, t < rows);
     }
@@ -377,7 +377,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
 // the scan chain each.
 template <bool WF, bool MF, bool DX = MF, bool PAIR = false>
 __global__ void __launch_bounds__(kTBlock) PIN_FWD_WAVES_ATTR
-__attribute__((amdgpu_waves_per_eu((!WF && MF) ? PIN_TRAIN_NWF_WAVES : 1)))
+__attribute__((amdgpu_waves_per_eu((!WF && MF) ? PIN_TRAIN_NWF_WAVES : (MF ? 3 : 1))))
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
@@ -390,7 +390,7 @@ k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const f
     float cw[kK];
 #pragma unroll
     for (int j = 0; j < kK; ++j) { cid[j] = -1; cw[j] = 0.f; }
-    if ((MF || PAIR) ? (tl & ~(int64_t)63) < (PAIR ? 2 * rows : rows) : t < rows) {
+    if ((tl & ~(int64_t)63) < (PAIR ? 2 * rows : rows)) {   // whole waves (MFMA, resolve_ties); live: t < rows
         const GridSource<false, PIN_TRAIN_IDP> src(g, p);
         train_forward_body<WF, GridSource<false, PIN_TRAIN_IDP>, MF, DX, PAIR>(src, p, mw, coord, ts, c, t, st, cid,
                                                                            cw, t < rows);
@@ -608,7 +608,7 @@ __device__ __forceinline__ void train_forward_eik_body(const Src& src, const Pin
     tk.init();
     const int nn = src.template scan<Src::kChunk>(qx, qy, qz, tk);
     const int nn_k = c.nn_k;
-    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's order of equal distances
+    resolve_ties(src, qx, qy, qz, nn_k, nn, tk);   // the reference's neighbour set at equal distances
     float u[kK];
     float S = 0.f;
 #pragma unroll
@@ -761,7 +761,10 @@ __device__ __forceinline__ void train_forward_eik_kernel_body(const Src& src, co
                                                               const float* coord, const int64_t* ts, PinTrainCfg c,
                                                               PinTrainState st, bool mlp_trains) {
     const int64_t t = xcd_block() * kTBlock + threadIdx.x;
-    if (t < c.n_main) train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t, st, mlp_trains);
+    // whole waves (resolve_ties): lanes past the rows redo the last row (identical values to the
+    // same addresses; this forward has no atomics)
+    if ((t & ~(int64_t)63) < c.n_main)
+        train_forward_eik_body<WF>(src, p, mw, coord, ts, c, t < c.n_main ? t : c.n_main - 1, st, mlp_trains);
 }
 
 template <bool WF>
