@@ -539,11 +539,14 @@ typedef struct PinTrainState {
                                     1: it leaves them, and the caller's pin_adam_step_train takes the
                                     gradient as grad_features + the replicas' sum (one launch less) */
     /* Deterministic accumulation: with grad_fixed non-NULL the feature
-     * terms are added as 64-bit fixed-point integers, round(term * 2^fixed_shift), into
-     * grad_fixed [max(replicas, 1), L+1, 8] (zero on the first call) instead of float atomics into
-     * grad_features / grad_replicas.  Integer addition is associative, so the sum does not depend on
+     * terms are added as 64-bit fixed-point integers into grad_fixed [2, max(replicas, 1), L+1, 8]
+     * (zero on the first call) instead of float atomics into grad_features / grad_replicas: a term
+     * with |term| 2^fixed_shift >= 4096 as round(term 2^fixed_shift) into the first (coarse) part, a
+     * smaller one as round(term 2^(fixed_shift + 40)) into the second (fine) part, so gradients down
+     * to ~1e-27 keep their value (the reference's Adam, eps 1e-15, steps on gradients of 1e-18).  Integer addition is associative, so the sum does not depend on
      * the order the atomics arrive in: the gradient is a function of the batch alone, bitwise.  It
-     * reaches grad_features as float(sum * 2^-fixed_shift) through pin_train_backward (replica_mode
+     * reaches grad_features as float(coarse 2^-fixed_shift + fine 2^-(fixed_shift + 40)) through
+     * pin_train_backward (replica_mode
      * 0) or pin_adam_step_train (replica_mode 1), which zero the integers again.  With cert_fixed
      * non-NULL the certainty side effect goes the same way into cert_fixed [L] (shift cert_shift),
      * and the caller folds it into the certainties with pin_fixed_accumulate (certainties is then
@@ -699,8 +702,9 @@ int pin_adam_step_segments(float* param, float* grad, float* exp_avg, float* exp
  * mlp / packed (non-NULL, nseg > 0): the same block then writes the stepped decoder's
  * pin_mlp_pack image (no pin_mlp_pack call before the next forward).  grad_stride must be 8.
  * grad_fixed (non-NULL; grad_replicas must then be NULL): the deterministic mode's fixed-point
- * replicas of PinTrainState.grad_fixed, [max(replicas, 1), n] int64 at shift fixed_shift: the
- * gradient is grad + float(their integer sum * 2^-fixed_shift), and they are zeroed again.
+ * replicas of PinTrainState.grad_fixed, [2, max(replicas, 1), n] int64 (coarse part at shift
+ * fixed_shift, fine part at fixed_shift + 40): the gradient is grad + float(their integer sums
+ * scaled back), and they are zeroed again.
  */
 int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                         float* grad_replicas, int32_t replicas, int64_t* grad_fixed, int32_t fixed_shift,
@@ -709,8 +713,11 @@ int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_av
 
 /* pin_fixed_accumulate -- out[i] += float((sum_k acc[k n + i]) * 2^-shift) for k < max(nrep, 1),
  * then acc := 0: folds the deterministic mode's fixed-point accumulators (PinTrainState.grad_fixed
- * / cert_fixed) into a float array.  The integer sum is exact; the result is rounded once. */
-int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, float* out, void* stream);
+ * / cert_fixed) into a float array.  parts 2 (grad_fixed): acc holds a second, fine part of nrep n
+ * entries at shift + 40 after the first, added as f64(coarse) 2^-shift + f64(fine) 2^-(shift + 40).
+ * The integer sums are exact; the result is rounded once. */
+int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, int32_t parts, float* out,
+                         void* stream);
 /* pin_adam_segments -- the same Adam update over nseg (<= 8) separate parameter tensors params[k]
  * of sizes[k] floats whose gradients and moments lie end to end in contiguous grad / exp_avg /
  * exp_avg_sq (the decoder's W1, b1, W2, b2 against pin_train_backward's mlp_grad): one launch

@@ -45,6 +45,29 @@ __device__ __forceinline__ unsigned long long to_fixed(float v, double scale) {
 __device__ __forceinline__ float from_fixed(long long v, double inv_scale) { return (float)((double)v * inv_scale); }
 __device__ __forceinline__ double fixed_scale(int shift) { return (double)(1ull << (shift & 63)); }
 
+// The feature gradients take TWO fixed-point parts (PinTrainState.grad_fixed [2, replicas, L+1, 8]):
+// a term t = g 2^shift with |t| >= 4096 goes to the coarse part as round(t); a smaller one to the
+// fine part as round(t 2^40) (< 2^52: 2,048 such terms per element before any overflow).  One part
+// at 2^-50 would round every term below ~4e-16 to zero and terms of ~1e-13 to a few per cent --
+// and the reference's Adam (eps 1e-15) turns a gradient of 1e-18 into a step of 1e-3 lr: the
+// dominated neighbours of a query that sits on a neural point (u_j / S ~ 1e-15) train on exactly
+// such gradients.  Each term goes to one part, chosen by its own value, so
+// the sums stay exact integers and order-free; the fold adds coarse 2^-shift + fine 2^-(shift + 40).
+constexpr double kFixedFineMul = 1099511627776.0;   // 2^40
+__device__ __forceinline__ void fixed_add(unsigned long long* __restrict__ dst, int64_t e, float g, double scale,
+                                          int64_t fine_off) {
+    const double t = (double)g * scale;
+    if (fabs(t) >= 4096.0) atomicAdd(dst + e, to_fixed(g, scale));
+    else if (t != 0.0) atomicAdd(dst + fine_off + e, (unsigned long long)__double2ll_rn(t * kFixedFineMul));
+}
+__device__ __forceinline__ float from_fixed2(long long coarse, long long fine, double inv_scale) {
+    return (float)((double)coarse * inv_scale + (double)fine * (inv_scale / kFixedFineMul));
+}
+// offset of the fine part: the coarse part's replicas x rows x 8
+__device__ __forceinline__ int64_t fixed_fine_off(const PinTrainState& st, int64_t rows) {
+    return (int64_t)(st.replicas > 1 ? st.replicas : 1) * rows * kF;
+}
+
 // row r of the iteration: a main query or a stencil query (x+,x-,y+,y-,z+,z- blocks)
 __device__ __forceinline__ void row_coord(const float* __restrict__ coord, const PinTrainCfg& c, int64_t r, float& qx,
                                           float& qy, float& qz) {
@@ -1053,6 +1076,7 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
                                                 int nrow_blk, const float* gst, const float* s_dsdf,
                                                 float* __restrict__ grad_features, unsigned long long* __restrict__ fdst,
                                                 double fscale, int* buf, int64_t frows = 1) {
+    const int64_t ffine = fixed_fine_off(st, frows);
     int* const s_ids = buf;
     float* const s_wt = (float*)(buf + kTBlock * kK);
     float* const s_al = (float*)(buf + 2 * kTBlock * kK);
@@ -1081,7 +1105,7 @@ __device__ __forceinline__ void feature_scatter(const PinTrainCfg& c, const PinT
         float g;
         if (EIK) g = fmaf(s_wt[rj], s_dsdf[lr], s_al[rj]) * gst[lr * kF + d];
         else g = s_wt[rj] * gst[lr * kF + d];
-        if (fdst) atomicAdd(fdst + (int64_t)id * kF + d, to_fixed(g, fscale));   // deterministic mode
+        if (fdst) fixed_add(fdst, (int64_t)id * kF + d, g, fscale, ffine);   // deterministic mode
         else atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
 }
@@ -1188,7 +1212,7 @@ __device__ __forceinline__ void feature_scatter_sorted(const PinTrainCfg& c, con
             else g = fmaf(s_wt[pidx], gst[lr * kF + d], g);
         }
         const int id = s_run_id[run];
-        if (fdst) atomicAdd(fdst + (int64_t)id * kF + d, to_fixed(g, fscale));
+        if (fdst) fixed_add(fdst, (int64_t)id * kF + d, g, fscale, fixed_fine_off(st, frows));
         else atomicAdd(grad_features + (int64_t)id * kF + d, g);
     }
     if (!side) return;
@@ -1430,7 +1454,7 @@ k_train_backward(const PinPoints p, const PinMlp m, const float* __restrict__ la
                     const int e = u * 64 + lane;
                     const int rid = wid[e >> 3];
                     if (rid < 0) continue;
-                    if (fdst) atomicAdd(fdst + (int64_t)rid * kF + (e & (kF - 1)), to_fixed(wg[e], fscale));
+                    if (fdst) fixed_add(fdst, (int64_t)rid * kF + (e & (kF - 1)), wg[e], fscale, fixed_fine_off(st, p.rows));
                     else atomicAdd(gdst + (int64_t)rid * kF + (e & (kF - 1)), wg[e]);
                 }
             }
@@ -1635,7 +1659,7 @@ k_train_backward_nwf_sorted(const PinPoints p, const PinMlp m, const float* __re
                 wave_lds_sync();
                 for (int e = lane; e < nt * kF; e += 64) {
                     const int rid = wid[e >> 3];
-                    if (fdst) atomicAdd(fdst + (int64_t)rid * kF + (e & (kF - 1)), to_fixed(ws[e], fscale));
+                    if (fdst) fixed_add(fdst, (int64_t)rid * kF + (e & (kF - 1)), ws[e], fscale, fixed_fine_off(st, p.rows));
                     else atomicAdd(grad_features + (int64_t)rid * kF + (e & (kF - 1)), ws[e]);
                 }
                 wave_lds_sync();   // the next round's decode reuses the scratch
@@ -1670,16 +1694,22 @@ static_assert(kXsWave >= 64 * (kF + 1), "a wave's run totals (8 floats + id per 
 
 // out[i] += float(sum of the nrep fixed-point accumulators at i * 2^-shift); the accumulators are
 // zeroed (pin_fixed_accumulate, and the deterministic pin_train_backward with replica_mode 0)
+// parts 2: the feature gradients' coarse and fine parts (fixed_add), the fine part at acc + nrep n
 __global__ void __launch_bounds__(kTBlock)
-k_fixed_reduce(long long* __restrict__ acc, int nrep, int64_t n, int shift, float* __restrict__ out) {
+k_fixed_reduce(long long* __restrict__ acc, int nrep, int64_t n, int shift, int parts, float* __restrict__ out) {
     const double inv = 1.0 / fixed_scale(shift);
+    long long* const fine = acc + (int64_t)nrep * n;
     for (int64_t e = (int64_t)blockIdx.x * kTBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kTBlock) {
-        long long s = 0;
+        long long s = 0, f = 0;
         for (int k = 0; k < nrep; ++k) {
             s += acc[k * n + e];
             acc[k * n + e] = 0;
+            if (parts > 1) {
+                f += fine[k * n + e];
+                fine[k * n + e] = 0;
+            }
         }
-        out[e] += from_fixed(s, inv);
+        out[e] += parts > 1 ? from_fixed2(s, f, inv) : from_fixed(s, inv);
     }
 }
 
@@ -2014,18 +2044,21 @@ k_adam_train(float* __restrict__ prm, float* __restrict__ grad, float* __restric
     const int64_t bid = (int64_t)blockIdx.x - (sg.n > 0 ? 1 : 0);
     if (bid >= 0) {
         const int64_t i0 = 4 * (bid * kTBlock + threadIdx.x);
-        if (fix && i0 < n) {   // deterministic mode: grad + float(integer sum of the fixed-point replicas)
-            long long s[4] = {0, 0, 0, 0};
+        if (fix && i0 < n) {   // deterministic mode: grad + float(integer sums of the fixed-point replicas)
+            long long s[4] = {0, 0, 0, 0}, f[4] = {0, 0, 0, 0};
             for (int k = 0; k < nfix; ++k) {
                 longlong2* r = (longlong2*)(fix + k * n + i0);
-                const longlong2 v0 = r[0], v1 = r[1];
+                longlong2* q = (longlong2*)(fix + (nfix + k) * n + i0);   // the fine part (fixed_add)
+                const longlong2 v0 = r[0], v1 = r[1], w0 = q[0], w1 = q[1];
                 r[0] = r[1] = make_longlong2(0, 0);
+                q[0] = q[1] = make_longlong2(0, 0);
                 s[0] += v0.x; s[1] += v0.y; s[2] += v1.x; s[3] += v1.y;
+                f[0] += w0.x; f[1] += w0.y; f[2] += w1.x; f[3] += w1.y;
             }
             const double inv = 1.0 / fixed_scale(fshift);
             float4 g = *(float4*)(grad + i0);
-            g.x += from_fixed(s[0], inv); g.y += from_fixed(s[1], inv);
-            g.z += from_fixed(s[2], inv); g.w += from_fixed(s[3], inv);
+            g.x += from_fixed2(s[0], f[0], inv); g.y += from_fixed2(s[1], f[1], inv);
+            g.z += from_fixed2(s[2], f[2], inv); g.w += from_fixed2(s[3], f[3], inv);
             *(float4*)(grad + i0) = g;
         } else if (nrep > 1 && i0 < n) {   // n % 4 == 0 (checked by the host)
             float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2212,12 +2245,13 @@ int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_av
     return launch_status();
 }
 
-int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, float* out, void* stream) {
-    if (n < 0 || (n > 0 && (!acc || !out)) || shift < 0 || shift > 62) return PIN_ERR_ARG;
+int pin_fixed_accumulate(int64_t* acc, int32_t nrep, int64_t n, int32_t shift, int32_t parts, float* out,
+                         void* stream) {
+    if (n < 0 || (n > 0 && (!acc || !out)) || shift < 0 || shift > 62 || parts < 1 || parts > 2) return PIN_ERR_ARG;
     if (n == 0) return PIN_OK;
     const int64_t nb = (n + kTBlock - 1) / kTBlock;
     hipLaunchKernelGGL(k_fixed_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, as_stream(stream),
-                       (long long*)acc, nrep > 1 ? (int)nrep : 1, n, (int)shift, out);
+                       (long long*)acc, nrep > 1 ? (int)nrep : 1, n, (int)shift, (int)parts, out);
     return launch_status();
 }
 
@@ -2488,7 +2522,7 @@ int pin_train_backward(const PinPoints* pts, const PinMlp* mlp, const float* lab
         const int64_t n = pts->rows * kF;
         const int64_t nb = (n + kTBlock - 1) / kTBlock;
         hipLaunchKernelGGL(k_fixed_reduce, dim3((unsigned)(nb < 2048 ? nb : 2048)), dim3(kTBlock), 0, s,
-                           (long long*)st->grad_fixed, st->replicas > 1 ? st->replicas : 1, n, st->fixed_shift,
+                           (long long*)st->grad_fixed, st->replicas > 1 ? st->replicas : 1, n, st->fixed_shift, 2,
                            grad_features);
     } else if (grad_features && st->grad_replicas && st->replicas > 1 && st->replica_mode == 0) {
         const int64_t n4 = pts->rows * kF / 4;

@@ -113,7 +113,7 @@ class _TrainBuffers:
 
     def fixed(self, n, device):
         """Zeroed int64 scratch for PinTrainState.grad_fixed (the deterministic mode's fixed-point
-        replicas; the consumer re-zeroes it)."""
+        replicas, coarse and fine parts; the consumer re-zeroes it)."""
         return self._zeroed("grad_fixed", n, torch.int64, device)
 
     def cert_fixed(self, n, device):
@@ -210,7 +210,7 @@ class _StepPlan:
         nm = self.mapper.neural_points
         if self.cert_fix is not None:   # the deterministic mode's certainty sums, folded in once
             cert = nm.local_point_certainties
-            _lib.call("pin_fixed_accumulate", _lib.ptr(self.cert_fix), 1, cert.numel(), CERT_SHIFT, _lib.ptr(cert),
+            _lib.call("pin_fixed_accumulate", _lib.ptr(self.cert_fix), 1, cert.numel(), CERT_SHIFT, 1, _lib.ptr(cert),
                       self.s)
         nm.mark_modified(nm.local_point_certainties, nm.local_point_ts_update if self.ts64 is not None else None)
         self.mapper.last_loss = self.b.loss
@@ -1041,7 +1041,7 @@ class Mapper:
             if grad_features.shape[0] != pv.features.shape[0]:
                 raise ValueError("deterministic mapping needs grad_features of the local map's [L+1, 8] shape")
             nrep = _REPLICAS if use_rep else 1
-            fix = b.fixed(nrep * grad_features.numel(), q.device)
+            fix = b.fixed(2 * nrep * grad_features.numel(), q.device)   # coarse and fine parts
             st.grad_fixed, st.fixed_shift = fix.data_ptr(), FIXED_SHIFT
             st.replicas, st.replica_mode = nrep, int(defer)
             P.fix, P.nfix = (fix if defer else None), nrep

@@ -101,6 +101,36 @@ def test_deterministic_tiled_training_call_bitwise(dev):
         assert _norm(_np(a) - _np(b)) <= 1e-4 * _norm(_np(b))
 
 
+def test_deterministic_mode_keeps_tiny_gradients(dev):
+    """A query that sits ON a neural point gives that point u = 1 / (0 + 1e-15) and its other
+    neighbours IDW weights of ~1e-15, so they train on gradients of ~1e-18 -- and Adam with eps
+    1e-15 (utils/tools.py:89-116) turns those into steps of ~1e-3 lr.  The reference's float sums
+    keep them (its frame-0 mapping of the configs[0] replay moves such elements by ~1e-5 on the
+    first step); the deterministic mode's fixed point must too (its fine part, fixed_add): one
+    mapping step from the same state in both modes, every element's step equal to float noise."""
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+    steps = []
+    for det in (False, True):
+        nm, dec, pts = surface_map(200, device=dev, buffer_size=1 << 22, query_backend="grid", bs=20000)
+        for p in dec.parameters():
+            p.requires_grad_(False)
+        coord, label, ts = surface_pool(pts, 60000, seed=5, sigma=0.0, device=dev)   # rows ON neural points
+        label = torch.randn(label.shape, generator=torch.Generator().manual_seed(3)).to(dev) * 0.1
+        mapper = P.Mapper(nm.config, None, nm, dec, deterministic=det)
+        mapper.set_pool(coord, label, ts)
+        before = nm.geo_features.detach().clone()
+        torch.manual_seed(77)
+        mapper.mapping(1)
+        steps.append((nm.geo_features.detach() - before).double().cpu().numpy())
+    lr = float(nm.config.lr)
+    f, d = steps
+    frac = (np.abs(f) > 0) & (np.abs(f) < 0.5 * lr)   # steps of a gradient within ~eps: the tiny ones
+    assert int(frac.sum()) > 100, "the batch should train elements on eps-sized gradients"
+    np.testing.assert_allclose(d[frac], f[frac], rtol=1e-4, atol=1e-3 * lr * 1e-3)
+    off = np.abs(d - f) > 1e-4 * lr
+    assert off.mean() <= 1e-3, f"{off.sum()} of {off.size} steps differ"
+
+
 def test_fixed_accumulate_exact(dev):
     """pin_fixed_accumulate: out += float32(float64(integer sum of the replicas) * 2^-shift), the
     replicas zeroed -- against numpy on the same integers."""
@@ -109,11 +139,21 @@ def test_fixed_accumulate_exact(dev):
     acc = g.integers(-(1 << 55), 1 << 55, size=(R, n), dtype=np.int64)
     out = g.standard_normal(n).astype(np.float32)
     a, o = torch.from_numpy(acc.copy()).to(dev), torch.from_numpy(out.copy()).to(dev)
-    _lib.call("pin_fixed_accumulate", _lib.ptr(a), R, n, shift, _lib.ptr(o), _lib.stream())
+    _lib.call("pin_fixed_accumulate", _lib.ptr(a), R, n, shift, 1, _lib.ptr(o), _lib.stream())
     torch.cuda.synchronize()
     want = out + (acc.sum(0).astype(np.float64) * 2.0 ** -shift).astype(np.float32)
     np.testing.assert_array_equal(_np(o), want)
     assert int(a.abs().max()) == 0
+    # two parts (PinTrainState.grad_fixed): coarse at 2^-shift, fine at 2^-(shift + 40)
+    acc2 = g.integers(-(1 << 55), 1 << 55, size=(2, R, n), dtype=np.int64)
+    a2, o2 = torch.from_numpy(acc2.copy()).to(dev), torch.from_numpy(out.copy()).to(dev)
+    _lib.call("pin_fixed_accumulate", _lib.ptr(a2), R, n, shift, 2, _lib.ptr(o2), _lib.stream())
+    torch.cuda.synchronize()
+    inv = 2.0 ** -shift
+    want2 = out + (acc2[0].sum(0).astype(np.float64) * inv + acc2[1].sum(0).astype(np.float64) * (inv / 2.0 ** 40)
+                   ).astype(np.float32)
+    np.testing.assert_array_equal(_np(o2), want2)
+    assert int(a2.abs().max()) == 0
 
 
 def _host_tiles(gv, q, large):

@@ -9,8 +9,10 @@ Usage: python tools/slam_runs.py [slam_seq|slam_seq100] [det 0|1] [runs]
 import sys
 
 import numpy as np
+import torch
 
 sys.path.insert(0, ".")
+import pin_slam_amd as P  # noqa: E402
 from tests import test_gpu_slam as S  # noqa: E402
 
 
@@ -34,16 +36,27 @@ def main():
             worst_t = max(worst_t, (d / tt, k))
             worst_r = max(worst_r, (a / tr, k))
         allp.append(np.stack(poses))
+        probes = torch.from_numpy(z["surface_probes"]).cuda()
+        sdf, _, _, _, _ = P.query_sdf(nm, dec, probes, query_locally=False, want_grad=False, want_certainty=False)
+        ok, msg = S.surface_bounds(sdf.cpu().numpy(), z["env_end_surface_sdf"])
+        dtrue = np.linalg.norm(poses[-1][:3, 3] - z["truth_poses"][frames - 1][:3, 3])
         print(f"run {r}: worst position / limit {worst_t[0]:.3f} at frame {worst_t[1]}, worst angle / limit "
-              f"{worst_r[0]:.3f} at frame {worst_r[1]}", flush=True)
-    P = np.stack(allp)
-    c = P[:, :, :3, 3].mean(0)
+              f"{worst_r[0]:.3f} at frame {worst_r[1]}; last pose {dtrue:.4f} m from the truth; end surface "
+              f"{'ok' if ok else 'OUT'}: {msg}", flush=True)
+    Q = np.stack(allp)
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez(f"gpurun_out/slam_runs_{name}_det{int(det)}.npz", poses=Q)
+    c = Q[:, :, :3, 3].mean(0)
     print("our runs' largest distance from their mean per frame (m):",
-          np.round(np.linalg.norm(P[:, :, :3, 3] - c[None], axis=-1).max(0), 4).tolist())
+          np.round(np.linalg.norm(Q[:, :, :3, 3] - c[None], axis=-1).max(0), 4).tolist())
     print("our runs' largest angle from their mean per frame (deg):",
-          np.round([max(S._angle(P[r, k, :3, :3], S._rot_mean(P[:, k, :3, :3])) for r in range(R))
+          np.round([max(S._angle(Q[r, k, :3, :3], S._rot_mean(Q[:, k, :3, :3])) for r in range(R))
                     for k in range(frames)], 4).tolist())
     print("reference runs' e_r (deg):", np.round(penv[3], 4).tolist())
+    ref_true = [float(np.linalg.norm(Pr[frames - 1][:3, 3] - z["truth_poses"][frames - 1][:3, 3]))
+                for Pr in z["env_hist_pose"]]
+    print("reference runs' last pose from the truth (m):", np.round(ref_true, 4).tolist())
 
 
 if __name__ == "__main__":
