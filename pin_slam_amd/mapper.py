@@ -53,13 +53,20 @@ _PACK_POOL = os.environ.get("PIN_PACK_POOL", "1") != "0"
 # deterministic mode (Mapper(deterministic=True) / config.deterministic): the feature-gradient
 # terms and the certainty side effect are summed as 64-bit fixed-point integers
 # (PinTrainState.grad_fixed / cert_fixed), the rows tile-sorted stably -- a mapping() call is then
-# a function of its inputs and draws, bitwise.  Shifts: 2^-50 resolution (8.9e-16) with a range of
-# +-8192 per gradient element; 2^-32 (2.3e-10) and +-2^30 for a call's certainty sums
+# a function of its inputs and draws, bitwise.  Shifts: the feature gradients in two parts, 2^-50
+# (8.9e-16, range +-8192) for terms >= 2^-38 and 2^-90 for smaller ones (fixed_add, pin_train.hip);
+# 2^-32 (2.3e-10) and +-2^30 for a call's certainty sums
 FIXED_SHIFT = 50
 CERT_SHIFT = 32
 # the dense loop draws get_batch's rows on the device (pin_train_gather_packed_draw: no draw
 # launches) unless _randint is replaced on the instance (the tests' replay hook) or
-# Mapper.device_draws is False; PIN_DEVICE_DRAWS=0 turns it off everywhere
+# Mapper.device_draws is False; PIN_DEVICE_DRAWS=0 turns it off everywhere.  The draws are NOT the
+# reference's numbers: its get_batch calls torch.randint on the device (utils/mapper.py:683-711),
+# these are SplitMix64 of (seed, iteration, row) -- the same distribution (history rows uniform
+# over the pool, new rows uniform over new_idx; test_device_batch_draws), another stream.  The
+# seed comes from the device's torch generator (its seed and Philox offset, the offset then
+# advanced as the reference's two randint draws per iteration would), so torch.manual_seed still
+# fixes a run, no host sync is needed and the CPU generator is left alone (_device_seed).
 _DEVICE_DRAWS = os.environ.get("PIN_DEVICE_DRAWS", "1") != "0"
 # data-parallel dense loop: the feature gradient reduce-scattered in this many row buckets, each
 # rank's piece of a bucket stepped by Adam as soon as it lands and all-gathered (_owner_adam)
@@ -588,6 +595,23 @@ class Mapper:
         self._pool_packed, self._pool_packed_sig = pk, sig
         return pk
 
+    def _device_seed(self, iters):
+        """A 62-bit seed for one mapping() call's device draws from the device's torch generator:
+        its initial seed and Philox offset, the offset advanced by 8 per iteration (two randint
+        draws of <= 4 values per thread each, as get_batch's would consume).  Falls back to the CPU
+        generator where the device generator has no offset API."""
+        dev = torch.device(self.device)
+        try:
+            gen = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+            off = int(gen.get_offset())
+            gen.set_offset(off + 8 * max(int(iters), 1))
+            x = (int(gen.initial_seed()) * 0x9E3779B97F4A7C15 + off + 1) & ((1 << 64) - 1)
+            x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+            x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+            return (x ^ (x >> 31)) >> 2
+        except (AttributeError, RuntimeError, IndexError):
+            return int(torch.randint(0, 1 << 62, (1,)).item())
+
     def _randint(self, high, n):
         """torch.randint(0, high, (n,)) on the mapper's device: every draw of get_batch goes through
         here (tests replay the reference's recorded draws by replacing it on the instance)."""
@@ -821,7 +845,7 @@ class Mapper:
         # keeps the host draws
         dev_draw = (_DEVICE_DRAWS and packed is not None and getattr(self, "device_draws", True)
                     and "_randint" not in self.__dict__ and getattr(type(self), "_randint", None) is Mapper._randint)
-        seed = int(torch.randint(0, 1 << 62, (1,)).item()) if dev_draw else 0
+        seed = self._device_seed(iter_count) if dev_draw else 0
         for it in range(iter_count):
             draw = None
             if dev_draw:

@@ -48,6 +48,27 @@ import torch
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
+MANIFEST = os.path.join(OUT, "GENERATED_WITH.json")
+
+
+def record_fixture(name, generator, **extra):
+    """Per-fixture provenance in GENERATED_WITH.json: the generating call, the date, the torch /
+    numpy versions and thread count it ran with, and the file's SHA-256."""
+    import hashlib
+    import json
+    path = os.path.join(OUT, f"{name}.npz")
+    m = json.load(open(MANIFEST)) if os.path.exists(MANIFEST) else {}
+    m[f"{name}.npz"] = dict(generator=generator, generated=time.strftime("%Y-%m-%d"), torch=torch.__version__,
+                           numpy=np.__version__, torch_threads=torch.get_num_threads(),
+                           sha256=hashlib.sha256(open(path, "rb").read()).hexdigest(), **extra)
+    with open(MANIFEST, "w") as f:
+        json.dump(dict(sorted(m.items())), f, indent=1)
+        f.write("\n")
+
+
+def save_fixture(name, rec, generator, **extra):
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    record_fixture(name, generator, **extra)
 
 sys.dont_write_bytecode = True
 for _name in ["open3d", "roma", "wandb", "skimage", "skimage.measure", "natsort",
@@ -303,7 +324,7 @@ def gen_query_case(name, cfg_kwargs, n_side, n_surface, seed, lattice=False):
     rec["qc_neighbor_dx"] = npm.neighbor_dx.numpy().copy()
     rec["qc_certainty"] = npm.query_certainty(torch.from_numpy(q)).numpy()
     npm.set_search_neighborhood(num_nei_cells=cfg.num_nei_cells, search_alpha=cfg.search_alpha)
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "M=", npm.count(), "L=", npm.local_count(), "N=", q.shape[0],
           "Kc=", npm.neighbor_K, "valid rows", int((rec["q1_nn_counts"] > 0).sum()))
 
@@ -388,7 +409,7 @@ def gen_mapper_case(name, cfg_kwargs, n_side, n_batch, seed, iters=2):
     rec["global_features_after"] = npm.geo_features.detach().numpy().copy()
     rec["global_cert_after"] = npm.point_certainties.numpy().copy()
     rec["global_ts_update_after"] = npm.point_ts_update.numpy().copy()
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "L=", npm.local_count(), "loss", [rec[f"it{i}_loss"] for i in range(iters)])
 
 
@@ -478,7 +499,7 @@ def gen_tracker_case(name, cfg_kwargs, n_src, seed, n_train=150):
     rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
     rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
     rec["local_features"] = npm.local_geo_features.detach().numpy().copy()
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "valid", rec["valid_count"], "resid_cm", resid_cm)
     print(delta_T)
     print("tracking", valid_track, T_track)
@@ -508,7 +529,7 @@ def gen_mesher_case(name, cfg_kwargs, n_side, seed):
                mesh_min_nn=np.int64(cfg.mesh_min_nn))
     rec.update({f"map_{k}": v for k, v in map_state(npm).items()})
     rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "grid", voxel_num_xyz, "mask", int(mask.sum()))
 
 
@@ -627,7 +648,7 @@ def gen_map_case(name, seed, use_mid_ts=False, fill_all=False):
         rec[f"vds_{key}_values"] = values[key]
         rec[f"vds_{key}_idx"] = rtools.voxel_down_sample_torch(t, 0.3).numpy()
         rec[f"vds_{key}_min_idx"] = rtools.voxel_down_sample_min_value_torch(t, 0.3, torch.from_numpy(values[key])).numpy()
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     torch.set_num_threads(8)
 
 
@@ -656,7 +677,7 @@ def gen_pin_map_case(name="pin_map_ref", seed=12):
     rec["local_features"] = npm.local_geo_features.detach().numpy().copy()
     rec["local_neural_points"] = npm.local_neural_points.numpy().copy()
     rec.update({f"dec_{k}": v for k, v in dec_params(dec).items()})
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "points", npm.count(), "local", npm.local_count())
 
 
@@ -724,7 +745,7 @@ def gen_sampler_case(name, seed, **cfg_over):
     for k in ["surface_sample_range_m", "surface_sample_n", "free_front_n", "free_behind_n", "free_sample_begin_ratio",
               "free_sample_end_dist_m", "dist_weight_on", "dist_weight_scale", "max_range", "behind_dropoff_on"]:
         rec[f"cfg_{k}"] = np.asarray(getattr(cfg, k))
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "rows", coord.shape[0])
 
 
@@ -784,7 +805,7 @@ def gen_process_frame_case(name="process_frame", seed=15, frames=4):
               "surface_sample_range_m", "voxel_size_m", "bs_new_sample", "new_certainty_thre", "map_surface_ratio",
               "local_map_travel_dist_ratio", "pool_capacity"]:
         rec[f"cfg_{k}"] = np.asarray(getattr(cfg, k))
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "pool", mapper.pool_sample_count, "points", npm.count(), "new", mapper.new_idx.shape[0])
 
 
@@ -869,7 +890,7 @@ def gen_slam_sequence(name="slam_seq", frames=30, seed=21, replay_seed=2024, sce
     for key in ("map_count", "local_count", "pool", "new"):
         a, b = rec["hist_" + key].astype(np.float64), t1["hist_" + key].astype(np.float64)
         rec["spread_rel_" + key] = np.abs(a - b) / np.maximum(a, 1.0)
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     print(name, "saved; 1- vs 8-thread spread: pose", max(dts), "m", max(drs), "deg;",
           {k: float(np.max(v)) for k, v in rec.items() if k.startswith("spread_rel")},
           "surface sdf |diff| median", float(np.median(rec["spread_abs_end_surface_sdf"])),
@@ -1022,7 +1043,7 @@ def gen_mapping_call(name, cfg_kwargs, frozen, iters=15, pool_n=100000, n_side=1
             rec["spread_norm_" + k] = np.float64(np.linalg.norm(diff))
             rec["spread_max_" + k] = np.float64(np.abs(diff).max())
             rec["spread_frac1e4_" + k] = np.float64((np.abs(diff) > 1e-4).mean())
-    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    save_fixture(name, rec, "gen_golden.py " + name)
     d = np.abs(rec["global_features_after"] - t1["global_features_after"])
     print(name, "L=", rec["L"], "require_gradient", rec["require_gradient"], "1- vs 8-thread features: max",
           float(d.max()), "off > 1e-3", float((d > 1e-3).mean()))
@@ -1119,7 +1140,7 @@ def gen_neighborhoods():
         rec[f"{key}_dx"] = npm.neighbor_dx.numpy()
         rec[f"{key}_K"] = np.int64(npm.neighbor_K)
         rec[f"{key}_max_valid_dist2"] = np.float64(npm.max_valid_dist2)
-    np.savez_compressed(os.path.join(OUT, "neighborhoods.npz"), **rec)
+    save_fixture("neighborhoods", rec, "gen_golden.py gen_neighborhoods")
 
 
 def main(only=None):
@@ -1142,7 +1163,6 @@ def main(only=None):
         for name in only:
             cases[name]()
         return
-    meta = {"torch": torch.__version__, "numpy": np.__version__, "generated": time.strftime("%Y-%m-%d")}
     gen_neighborhoods()
     gen_query_case("query_wf", dict(weighted_first=True), 120, 1600, seed=1)
     gen_query_case("query_nwf", dict(weighted_first=False), 120, 1600, seed=2)
@@ -1160,9 +1180,6 @@ def main(only=None):
                      free_behind_n=2, free_sample_end_dist_m=1.5, dist_weight_on=False, surface_sample_range_m=0.3)
     gen_process_frame_case()
     gen_query_case("query_ties", dict(voxel=0.25, alpha=0.5, weighted_first=True), 100, 1600, seed=16, lattice=True)
-    with open(os.path.join(OUT, "GENERATED_WITH.txt"), "w") as f:
-        for k, v in meta.items():
-            f.write(f"{k}: {v}\n")
 
 
 if __name__ == "__main__":

@@ -287,6 +287,10 @@ def combine(name):
     z["env_torch"] = np.asarray([str(r["torch_version"]) for r in runs])
     z["env_generated"] = np.asarray(time.strftime("%Y-%m-%d"))
     np.savez_compressed(path, **z)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import build_manifest
+    build_manifest.update(name, envelope_runs=labels, envelope_generated=str(z["env_generated"]),
+                          envelope_torch=sorted(set(str(v) for v in z["env_torch"])))
     P = z["env_hist_pose"]
     dt = np.linalg.norm(P[:, :, :3, 3] - P[:1, :, :3, 3], axis=-1)
     m = np.abs(z["env_end_surface_sdf"]).mean(axis=1)

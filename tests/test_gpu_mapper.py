@@ -535,6 +535,35 @@ def test_device_batch_draws(dev):
     counts = np.bincount(idx[:n_hist] * 64 // N, minlength=64)
     chi2 = float(((counts - n_hist / 64) ** 2 / (n_hist / 64)).sum())
     assert chi2 < 120, chi2    # 63 degrees of freedom: p ~ 1e-5 at 120
+    # the new-sample rows: positions in new_idx, uniform over [0, n_sel)
+    assert idx[n_hist:].min() >= 0 and idx[n_hist:].max() < n_sel and idx[:n_hist].max() < N
+    counts = np.bincount(idx[n_hist:] * 16 // n_sel, minlength=16)
+    chi2 = float(((counts - n_new / 16) ** 2 / (n_new / 16)).sum())
+    assert chi2 < 45, chi2     # 15 degrees of freedom: p ~ 1e-4 at 45
+
+
+def test_device_draws_leave_the_cpu_generator_alone(dev):
+    """mapping()'s device draws take their seed from the device's torch generator (seed + Philox
+    offset, advanced per call) -- the CPU generator's stream is untouched, torch.manual_seed fixes
+    the run (two calls from the same seed draw the same batches) and consecutive calls differ."""
+    from pin_slam_amd.synthetic import surface_map, surface_pool
+
+    def call(reseed):
+        nm, dec, pts = surface_map(120, device=dev, buffer_size=1 << 20, query_backend="grid", bs=4096)
+        coord, label, ts = surface_pool(pts, 30000, seed=5, device=dev)
+        mapper = P.Mapper(nm.config, None, nm, dec)
+        mapper.set_pool(coord, label, ts)
+        if reseed:
+            torch.manual_seed(123)
+        cpu = torch.get_rng_state()
+        mapper.mapping(2)
+        assert torch.equal(cpu, torch.get_rng_state()), "mapping() advanced the CPU generator"
+        return nm.geo_features.detach().clone()
+    a, b = call(True), call(True)
+    c = call(False)   # the device generator moved on: another batch
+    # the same batches: equal up to float-atomic noise (Adam's sign-sized steps on noise gradients)
+    assert float((~torch.isclose(a, b, rtol=1e-4, atol=1e-6)).float().mean()) <= 2e-3
+    assert float((~torch.isclose(a, c, rtol=1e-4, atol=1e-6)).float().mean()) >= 0.05
 
 
 def test_fat_cache_sees_training_writes(dev):
