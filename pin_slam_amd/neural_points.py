@@ -237,8 +237,7 @@ class NeuralPoints(nn.Module):
         self._nbhd_key = key
         hit = self.__dict__.setdefault("_nbhd_cache", {}).get(key)
         if hit is not None:
-            for k, v in hit.items():
-                setattr(self, k, v)
+            self._set_plain(hit)
             return
         dx = neighbor_offsets(num_nei_cells, search_alpha)          # host, then one copy
         self.neighbor_dx = dx.to(self.primes.device)
@@ -252,6 +251,18 @@ class NeuralPoints(nn.Module):
         self._num_columns = 0
         self._grid_exact = grid_window_collision_free(self.buffer_size, num_nei_cells)
         self._save_neighborhood()
+
+    def _set_plain(self, fields):
+        """Attribute writes without nn.Module.__setattr__'s registry checks (~3 us each, a dozen
+        per frame) for names that are not parameters, buffers or submodules; others go through
+        setattr as usual."""
+        reg = (self._parameters, self._buffers, self._modules)
+        d = self.__dict__
+        for k, v in fields.items():
+            if isinstance(v, (nn.Parameter, nn.Module)) or any(k in r for r in reg):
+                setattr(self, k, v)
+            else:
+                d[k] = v
 
     def _save_neighborhood(self):
         key = self.__dict__.get("_nbhd_key")
@@ -570,19 +581,20 @@ class NeuralPoints(nn.Module):
         # buffers with spare capacity (_append_rows): no per-frame copy of the whole map and no
         # allocator growth as the map grows (a growing torch.cat needed a fresh, larger block from
         # time to time -- a ~10 ms frame)
-        self.neural_points = self._append_rows("neural_points", self.neural_points, pts[new_rows[:k]])
+        self._set_plain(dict(neural_points=self._append_rows("neural_points", self.neural_points, pts[new_rows[:k]])))
         if was_trusted:
             self._trust_table()
         quat = torch.zeros((k, 4), dtype=self.dtype, device=dev)
         quat[:, 0] = 1.0
-        self.point_orientations = self._append_rows("point_orientations", self.point_orientations, quat)
         ts = torch.full((k,), int(cur_ts), device=dev, dtype=torch.long)
-        self.point_ts_create = self._append_rows("point_ts_create", self.point_ts_create, ts)
-        self.point_ts_update = self._append_rows("point_ts_update", self.point_ts_update, ts)
         new_fts = self.geo_feature_std * torch.randn(k + 1, self.geo_feature_dim, device=dev, dtype=self.dtype)
-        self.geo_features = self._append_rows("geo_features", self.geo_features, new_fts, replace_last=True)
-        self.point_certainties = self._append_rows("point_certainties", self.point_certainties,
-                                                   torch.zeros(k, device=dev, dtype=self.dtype))
+        self._set_plain(dict(
+            point_orientations=self._append_rows("point_orientations", self.point_orientations, quat),
+            point_ts_create=self._append_rows("point_ts_create", self.point_ts_create, ts),
+            point_ts_update=self._append_rows("point_ts_update", self.point_ts_update, ts),
+            geo_features=self._append_rows("geo_features", self.geo_features, new_fts, replace_last=True),
+            point_certainties=self._append_rows("point_certainties", self.point_certainties,
+                                                torch.zeros(k, device=dev, dtype=self.dtype))))
         self.reset_local_map(sensor_position, sensor_orientation, cur_ts)
 
     def _append_rows(self, name, cur, new, replace_last=False):
@@ -647,15 +659,11 @@ class NeuralPoints(nn.Module):
                                 ts_update=lts.data_ptr(), certainties=lcert.data_ptr(), features=lfeat.data_ptr(),
                                 count=L, feature_dim=F, reserved=0)
         _lib.call("pin_map_gather", ctypes.byref(src), _lib.ptr(rows), L, 1, ctypes.byref(dst), _lib.stream())
-        self.local_neural_points = lpos
-        self.local_point_orientations = lquat
-        self.local_point_certainties = lcert
-        self.local_point_ts_update = lts
-        self.local_mask = mask.view(torch.bool)
-        self.global2local = g2l
+        lmask = mask.view(torch.bool)
+        self._set_plain(dict(local_neural_points=lpos, local_point_orientations=lquat, local_point_certainties=lcert,
+                             local_point_ts_update=lts, local_mask=lmask, global2local=g2l,
+                             local_orientation=sensor_orientation, _local_rows=(lmask, rows[:L])))
         self.local_geo_features = nn.Parameter(lfeat)
-        self.local_orientation = sensor_orientation
-        self._local_rows = (self.local_mask, rows[:L])
         self._local_snapshot = self._snapshot()
 
     # derived state rebuilt on demand: weak references, capacity buffers and views keyed on tensor
