@@ -84,7 +84,9 @@ struct TopK {
     // c[j] ? d[j] : (c[j-1] ? x : d[j-1]) is the median of (d[j-1], x, d[j]) (equal values are
     // interchangeable, so ties change nothing); the payloads keep the two selects.
     __device__ __forceinline__ void insert(float x, int gi) {
-        rej = fminf(rej, fmaxf(x, d[kK - 1]));   // x itself, or the entry it pushes out
+        // the smaller of rej and what leaves the list (x itself, or the entry x pushes out):
+        // rej >= d[kK-1] always, so that is the median of (d[kK-1], x, rej) -- one v_med3
+        rej = __builtin_amdgcn_fmed3f(d[kK - 1], x, rej);
         bool c[kK];
 #pragma unroll
         for (int j = 0; j < kK; ++j) c[j] = d[j] <= x;

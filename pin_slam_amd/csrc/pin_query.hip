@@ -415,7 +415,9 @@ k_query_sdf(const PinHash h, const PinPoints p, const PinMlp m, const float* __r
 // MF: decoder on the f16 matrix cores (mlp_sdf_mfma16, m.packed from pin_mlp_pack).
 template <bool WF, bool PGO, bool GRAD, bool FAT, bool MF>
 __global__ void __launch_bounds__(kBlock)
-__attribute__((amdgpu_waves_per_eu(PGO ? PIN_SDF_WAVES_PGO : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES_NWF))))
+__attribute__((amdgpu_waves_per_eu(PGO ? PIN_SDF_WAVES_PGO
+                                        : (!MF && (!GRAD || !WF)) ? 4   // the SDF-only / f32 per-neighbour forms fit 128
+                                        : (WF ? PIN_SDF_WAVES : PIN_SDF_WAVES_NWF))))
 k_query_sdf_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ q,
                  const float4* __restrict__ q4, int64_t n, int nn_k, int zero_empty, float* __restrict__ sdf_out,
                  float* __restrict__ grad_out, int* __restrict__ nn_out, float* __restrict__ cert_out,
