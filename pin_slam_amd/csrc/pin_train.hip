@@ -390,6 +390,9 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
     flush_rows(c, st, xcd_block() * kTBlock, rows, cid, cw);
 }
 
+#ifndef PIN_TRAIN_NWF_F32_WAVES
+#define PIN_TRAIN_NWF_F32_WAVES 1   // the f32 per-neighbour training forward's minimum waves/SIMD (experiment switch)
+#endif
 #ifdef PIN_TRAIN_FWD_WAVES   // experiment: the grid training forward compiled for this many waves per SIMD
 #define PIN_FWD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(PIN_TRAIN_FWD_WAVES)))
 #else
@@ -400,7 +403,7 @@ k_train_forward_hash(const PinHash h, const PinPoints p, const PinMlp m, const f
 // the scan chain each.
 template <bool WF, bool MF, bool DX = MF, bool PAIR = false>
 __global__ void __launch_bounds__(kTBlock) PIN_FWD_WAVES_ATTR
-__attribute__((amdgpu_waves_per_eu((!WF && MF) ? PIN_TRAIN_NWF_WAVES : (MF ? 3 : 1))))
+__attribute__((amdgpu_waves_per_eu((!WF && MF) ? PIN_TRAIN_NWF_WAVES : (MF ? 3 : (!WF ? PIN_TRAIN_NWF_F32_WAVES : 1)))))
 k_train_forward_grid(const PinGrid g, const PinPoints p, const PinMlp m, const float* __restrict__ coord,
                      const int64_t* __restrict__ ts, PinTrainCfg c, PinTrainState st) {
     __shared__ float s_mlp[MF ? 1 : kWSize];
