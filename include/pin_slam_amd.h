@@ -711,6 +711,12 @@ int pin_adam_step_train(float* param, float* grad, float* exp_avg, float* exp_av
                         float* const* params, const int64_t* sizes, int nseg, float* seg_grad, float* seg_exp_avg,
                         float* seg_exp_avg_sq, const PinMlp* mlp, void* packed, const PinAdamStep* a, void* stream);
 
+/* pin_ref_sort_rows -- test hook for the k-NN tie order (pin_device.h resolve_ties): order[r, :] =
+ * the permutation libstdc++'s std::sort leaves row r of keys [rows, n] in (n <= 128), i.e. what the
+ * reference's torch.sort(dists2, dim=1) returns as indices (model/neural_points.py:562), computed
+ * by the same wave-parallel restatement the query and training kernels use on tied rows. */
+int pin_ref_sort_rows(const float* keys, int32_t n, int64_t rows, int32_t* order, void* stream);
+
 /* pin_fixed_accumulate -- out[i] += float((sum_k acc[k n + i]) * 2^-shift) for k < max(nrep, 1),
  * then acc := 0: folds the deterministic mode's fixed-point accumulators (PinTrainState.grad_fixed
  * / cert_fixed) into a float array.  parts 2 (grad_fixed): acc holds a second, fine part of nrep n

@@ -185,13 +185,13 @@ class Query:
     nbr_feat: np.ndarray      # [N,k,F]
 
 
-def ref_sort_row(vals) -> list:
+def ref_sort_row(vals, stats=None, raw=False) -> list:
     """The column order torch's CPU sort(stable=False) leaves one row in: libstdc++ std::sort
     (introsort -- median-of-three quicksort down to runs of 16, heapsort past 2 floor(log2 n)
     levels, then an insertion sort) with a plain less-than on the values (aten SortingKernel), as
     the reference's k-NN sort runs it (model/neural_points.py:562).  Equal values end up in an
     order that depends on the whole row, which is what this restatement reproduces."""
-    k = [float(v) for v in vals]
+    k = list(vals) if raw else [float(v) for v in vals]   # raw: keys compared as given (adversary tests)
     g = list(range(len(k)))
     n = len(k)
 
@@ -219,6 +219,8 @@ def ref_sort_row(vals) -> list:
         k[f + h], g[f + h] = vk, vg
 
     def heap_sort(f, l):                         # __partial_sort(first, last, last)
+        if stats is not None:
+            stats["heap"] = stats.get("heap", 0) + 1
         ln = l - f
         if ln >= 2:
             parent = (ln - 2) // 2

@@ -196,6 +196,7 @@ _SIGS = {
     "pin_adam_step_train": [c_void_p, c_void_p, c_void_p, c_void_p, i64, c_void_p, i32, c_void_p, i32, _P(c_void_p),
                             _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinMlp), c_void_p, _P(PinAdamStep), c_void_p],
     "pin_fixed_accumulate": [c_void_p, i32, i64, i32, i32, c_void_p, c_void_p],
+    "pin_ref_sort_rows": [c_void_p, i32, i64, c_void_p, c_void_p],
     "pin_adam_segments": [_P(c_void_p), _P(i64), i32, c_void_p, c_void_p, c_void_p, _P(PinAdamStep), c_void_p],
     "pin_adam_step_segments": [c_void_p, c_void_p, c_void_p, c_void_p, i64, _P(c_void_p), _P(i64), i32, c_void_p,
                                c_void_p, c_void_p, _P(PinAdamStep), c_void_p],

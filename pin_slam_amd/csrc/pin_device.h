@@ -329,7 +329,7 @@ __device__ void wave_heap_sort(WaveRow& r, int f, int l) {
 // not change the result).  The final insertion sort moves an entry left past strictly greater
 // keys only, so it is the stable sort of the row the loop leaves: entry p lands at
 // #(keys < k_p) + #(equal keys before p).  out_d / out_g: the k first keys / payloads, uniform.
-__device__ void wave_ref_sort(WaveRow& r, int n, float (&out_d)[kK], int (&out_g)[kK]) {
+__device__ void wave_introsort_loop(WaveRow& r, int n) {
     const int lane = wave_lane();
     int sF = 0, sL = 0, sD = 0;   // segment stack, entry e in lane e
     int top = 0;
@@ -362,13 +362,25 @@ __device__ void wave_ref_sort(WaveRow& r, int n, float (&out_d)[kK], int (&out_g
             l = cut;
         }
     }
-    const int pa = lane, pb = lane + 64;
-    int ra = 0, rb = 0;
+}
+
+// where the final insertion sort puts the lane's two entries (ra for entry lane, rb for lane + 64)
+__device__ __forceinline__ void wave_final_rank(const WaveRow& r, int n, int& ra, int& rb) {
+    const int pa = wave_lane(), pb = pa + 64;
+    ra = 0;
+    rb = 0;
     for (int q = 0; q < n; ++q) {
         const float kq = row_key(r, q);
         ra += (kq < r.ka || (kq == r.ka && q < pa)) ? 1 : 0;
         rb += (kq < r.kb || (kq == r.kb && q < pb)) ? 1 : 0;
     }
+}
+
+__device__ void wave_ref_sort(WaveRow& r, int n, float (&out_d)[kK], int (&out_g)[kK]) {
+    wave_introsort_loop(r, n);
+    const int pa = wave_lane(), pb = pa + 64;
+    int ra, rb;
+    wave_final_rank(r, n, ra, rb);
 #pragma unroll
     for (int j = 0; j < kK; ++j) {
         const uint64_t ma = __ballot(pa < n && ra == j), mb = __ballot(pb < n && rb == j);

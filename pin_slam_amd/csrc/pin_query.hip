@@ -1343,6 +1343,36 @@ __global__ void __launch_bounds__(256) k_mlp_pack(const PinMlp m, unsigned char*
     mlp_pack_block(m, out);
 }
 
+// pin_ref_sort_rows: the tie resolution's wave-parallel std::sort (resolve_ties, pin_device.h) on
+// given rows, whole permutation out -- the test hook that pins it to torch's CPU sort on rows the
+// geometry rarely produces (the depth-limit heap sort, heavy ties).  One wave per row.
+__global__ void __launch_bounds__(kBlock)
+k_ref_sort_rows(const float* __restrict__ keys, int n, int64_t rows, int32_t* __restrict__ order) {
+    const int64_t row = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    if (row >= rows) return;   // whole waves: kBlock is a multiple of 64
+    const int lane = threadIdx.x & 63;
+    const float* kr = keys + row * n;
+    WaveRow r;
+    r.ka = lane < n ? kr[lane] : 0.f;
+    r.ga = lane;
+    r.kb = lane + 64 < n ? kr[lane + 64] : 0.f;
+    r.gb = lane + 64;
+    wave_introsort_loop(r, n);
+    int ra, rb;
+    wave_final_rank(r, n, ra, rb);
+    if (lane < n) order[row * n + ra] = r.ga;
+    if (lane + 64 < n) order[row * n + rb] = r.gb;
+}
+
+int pin_ref_sort_rows(const float* keys, int32_t n, int64_t rows, int32_t* order, void* stream) {
+    if (n < 1 || n > kRefSortMax || rows < 0 || (rows > 0 && (!keys || !order))) return PIN_ERR_ARG;
+    if (rows == 0) return PIN_OK;
+    const int64_t waves_per_block = kBlock / 64;
+    hipLaunchKernelGGL(k_ref_sort_rows, dim3((unsigned)((rows + waves_per_block - 1) / waves_per_block)), dim3(kBlock),
+                       0, as_stream(stream), keys, n, rows, order);
+    return hipGetLastError() == hipSuccess ? PIN_OK : PIN_ERR_HIP;
+}
+
 int pin_mlp_pack(const PinMlp* mlp, void* packed, void* stream) {
     if (!mlp || !mlp->W1 || !mlp->b1 || !mlp->W2 || !mlp->b2 || !packed || ((uintptr_t)packed & 15)) return PIN_ERR_ARG;
     hipLaunchKernelGGL(k_mlp_pack, dim3(1), dim3(256), 0, as_stream(stream), *mlp, (unsigned char*)packed);

@@ -215,3 +215,21 @@ def test_dynamic_filter_both_strategies_match_oracle(dev):
         assert got.dtype == np.bool_ and got.shape == (qn.shape[0],)
         np.testing.assert_array_equal(got[~near], ref[~near])
         assert 0.05 < float(ref.mean()) < 0.95
+
+
+@pytest.mark.parametrize("n", [2, 16, 17, 33, 57, 81, 93, 125, 128])
+def test_wave_ref_sort_is_torch_cpu_sort(dev, n):
+    """The kernels' tie order (resolve_ties: the row held by the wave, std::sort restated with
+    parallel partitions, the heap-sort fallback entry by entry, a stable final rank) through its
+    test hook pin_ref_sort_rows: the whole permutation equals torch's CPU sort(stable=False) --
+    the sort the reference's k-NN calls -- on tie-heavy rows, sorted / reversed rows, and
+    adversarial rows (McIlroy) that drive the introsort into its heap sort, with and without ties."""
+    from pin_slam_amd import _lib
+    from tests.test_oracle_golden import ref_sort_test_rows
+    rows = np.stack(ref_sort_test_rows(n, np.random.default_rng(100 + n)))
+    keys = torch.from_numpy(rows).to(dev)
+    order = torch.full(rows.shape, -1, dtype=torch.int32, device=dev)
+    _lib.call("pin_ref_sort_rows", _lib.ptr(keys), n, rows.shape[0], _lib.ptr(order), _lib.stream())
+    torch.cuda.synchronize()
+    _, want = torch.sort(torch.from_numpy(rows), dim=1)
+    np.testing.assert_array_equal(_np(order).astype(np.int64), want.numpy())

@@ -299,12 +299,39 @@ def test_tie_fixture_needs_the_reference_sort(golden, monkeypatch):
     assert not np.allclose(qry.feat, z["q1_feat"], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("n", [2, 16, 17, 27, 33, 57, 81, 93, 125, 343])
-def test_ref_sort_row_is_torch_cpu_sort(n):
-    """ref_sort_row restates the sort the reference calls (torch.sort(dists2, dim=1) on the CPU):
-    the permutation it leaves rows with many equal keys in, 9e3 entries included."""
-    import torch
-    rng = np.random.default_rng(n)
+def antiqsort_row(n):
+    """McIlroy's adversary ("A killer adversary for quicksort") run against ref_sort_row: keys
+    fixed lazily so that every median-of-three pivot is near the minimum, which drives libstdc++'s
+    introsort past its depth limit into the heap sort.  Returns the keys it fixed (distinct)."""
+    gas = n
+    val = [gas] * n
+    state = {"solid": 0, "cand": 0}
+
+    class Item:
+        __slots__ = ("i",)
+
+        def __init__(self, i):
+            self.i = i
+
+        def __lt__(self, other):
+            x, y = self.i, other.i
+            if val[x] == gas and val[y] == gas:
+                z = x if x == state["cand"] else y
+                val[z] = state["solid"]
+                state["solid"] += 1
+            if val[x] == gas:
+                state["cand"] = x
+            elif val[y] == gas:
+                state["cand"] = y
+            return val[x] < val[y]
+    O.ref_sort_row([Item(i) for i in range(n)], raw=True)
+    return np.asarray(val, np.float32)
+
+
+def ref_sort_test_rows(n, rng):
+    """Rows for the sort restatements: tie-heavy random rows (some with 9e3 entries), sorted and
+    reversed rows, and adversarial rows with and without ties (heap-sort fallback)."""
+    rows = []
     for t in range(60):
         v = rng.integers(0, max(2, n // 3), n).astype(np.float32)
         if t % 3 == 0:
@@ -313,5 +340,28 @@ def test_ref_sort_row_is_torch_cpu_sort(n):
             v = np.sort(v)
         if t % 7 == 0:
             v = np.sort(v)[::-1].copy()
+        rows.append(v)
+    if n >= 17:
+        a = antiqsort_row(n)
+        rows += [a, np.floor(a / 2).astype(np.float32), np.floor(a / 3).astype(np.float32)]
+    return rows
+
+
+def test_adversarial_rows_reach_the_heap_sort():
+    for n in (40, 81, 128):
+        a = antiqsort_row(n)
+        for w in (a, np.floor(a / 2).astype(np.float32)):
+            stats = {}
+            O.ref_sort_row(w, stats=stats)
+            assert stats.get("heap", 0) > 0, n
+
+
+@pytest.mark.parametrize("n", [2, 16, 17, 27, 33, 57, 81, 93, 125, 128, 343])
+def test_ref_sort_row_is_torch_cpu_sort(n):
+    """ref_sort_row restates the sort the reference calls (torch.sort(dists2, dim=1) on the CPU):
+    the permutation it leaves rows with many equal keys in, 9e3 entries included, and adversarial
+    rows that end in the heap sort."""
+    import torch
+    for v in ref_sort_test_rows(n, np.random.default_rng(n)):
         _, o = torch.sort(torch.from_numpy(v)[None], dim=1)
         assert O.ref_sort_row(v) == o[0].tolist()
