@@ -304,10 +304,15 @@ class FrameLoop:
                 t.record_stream(main)
         self._prefetched = (pts, cloud, src, done)
 
+    def _h2d(self, a, dtype):
+        """A small host array on the device without a blocking copy: staged in pinned memory (the
+        caching host allocator keeps it until the stream-ordered copy has run)."""
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dtype).pin_memory().to(self.dev, non_blocking=True)
+
     def read_and_preprocess(self, pts):
         c = self.config
         self.cur_pose_ref = np.eye(4)
-        self.cur_pose_torch = torch.tensor(self.cur_pose_ref, dtype=torch.float32, device=self.dev)
+        self.cur_pose_torch = self._h2d(self.cur_pose_ref, torch.float32)
         pre = self.__dict__.pop("_prefetched", None)
         if pre is not None and pre[0] is pts:
             torch.cuda.current_stream(self.dev).wait_event(pre[3])
@@ -323,7 +328,7 @@ class FrameLoop:
         else:                                                              # :320-339
             guess = self.last_pose_ref @ self.last_odom_tran if (c.uniform_motion_on and not self.lose_track) \
                 else self.last_pose_ref
-            self.cur_pose_guess_torch = torch.tensor(guess, dtype=torch.float64, device=self.dev)
+            self.cur_pose_guess_torch = self._h2d(guess, torch.float64)
             self.cur_source_points = src
 
     def update_odom_pose(self, cur_pose_torch):
@@ -367,7 +372,7 @@ class FrameLoop:
             mapper.lose_track = not valid
             self.update_odom_pose(T)
         mark("tracking")
-        nm.travel_dist = torch.tensor(np.array(self.travel_dist), dtype=torch.float32, device=self.dev)
+        nm.travel_dist = self._h2d(np.array(self.travel_dist), torch.float32)
         if not mapper.lose_track and not self.stop_status:
             d = draws(self.cur_point_cloud_torch.shape[0]) if draws is not None else None
             mapper.process_frame(self.cur_point_cloud_torch, None, self.cur_pose_torch, used, False, draws=d)
