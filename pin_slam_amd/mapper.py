@@ -339,6 +339,20 @@ class Mapper:
         self.cur_sample_count = sdf_label.shape[0]
         self.pool_sample_count = self.sdf_label_pool.shape[0]
         sig_before = self._pool_signature() if self.global_coord_pool is not None else None
+        # :185-188 first (the reference appends after the map update; the pools do not depend on
+        # it): the appends are device copies with no host read, so they run while the host works
+        # through the update's launches and count reads.  Appended into growable buffers (same
+        # contents as the reference's torch.cat, without reallocating and copying the whole pool
+        # every frame)
+        self.coord_pool = self._pool_append("coord", self.coord_pool, coord)
+        self.weight_pool = self._pool_append("weight", self.weight_pool, weight)
+        self.sdf_label_pool = self._pool_append("sdf_label", self.sdf_label_pool, sdf_label)
+        self.time_pool = self._pool_append("time", self.time_pool, time_repeat)
+        self.sem_label_pool = None if sem_label is None else (
+            sem_label if self.sem_label_pool is None else self._pool_append(
+                "sem", self.sem_label_pool, sem_label.to(self.sem_label_pool.dtype)))
+        self.color_pool = None if color_label is None else (
+            color_label if self.color_pool is None else self._pool_append("color", self.color_pool, color_label))
         if getattr(c, "from_sample_points", True):                                       # :163-171
             if getattr(c, "from_all_samples", False):
                 update_points = coord
@@ -351,17 +365,6 @@ class Mapper:
             if self.neural_points.prune_map(c.max_prune_certainty):
                 self.neural_points.recreate_hash(None, None, True, True, frame_id)
         self.neural_points.update(update_points, frame_origin, frame_orientation, frame_id)   # :177
-        # :185-188 -- appended into growable buffers (same contents as the reference's torch.cat,
-        # without reallocating and copying the whole pool every frame)
-        self.coord_pool = self._pool_append("coord", self.coord_pool, coord)
-        self.weight_pool = self._pool_append("weight", self.weight_pool, weight)
-        self.sdf_label_pool = self._pool_append("sdf_label", self.sdf_label_pool, sdf_label)
-        self.time_pool = self._pool_append("time", self.time_pool, time_repeat)
-        self.sem_label_pool = None if sem_label is None else (
-            sem_label if self.sem_label_pool is None else self._pool_append(
-                "sem", self.sem_label_pool, sem_label.to(self.sem_label_pool.dtype)))
-        self.color_pool = None if color_label is None else (
-            color_label if self.color_pool is None else self._pool_append("color", self.color_pool, color_label))
         self.normal_label_pool = None
         self.used_poses = self._used_poses()                                             # :205-211
         if self.ba_done_flag:                                                            # :214-217
