@@ -36,7 +36,7 @@ from .tracker import Tracker
 # pool (process_frame :110-321, dynamic_filter :79-108) and the helpers those call
 MAPPER_METHODS = ("mapping", "train_step", "_step_index", "_step_plan", "_dense_loop", "_owner_adam", "check_deferred", "_device_seed", "_adam",
                   "_adam_segments", "_check_supported", "_world", "_pools_fusable", "_slab_partition", "_batch_index",
-                  "_batch_parts", "_batch_sizes", "_randint", "_new_sample_mode", "process_frame", "dynamic_filter", "_used_poses",
+                  "_batch_parts", "_batch_sizes", "_randint", "_new_sample_mode", "process_frame", "dynamic_filter", "_used_poses", "_poses_dev",
                   "_pool_append", "_pool_compact", "_pool_compact_many", "_pool_compact_target", "_window_buffers", "_pool_rows_hint", "set_pool", "_pool_signature", "_pack",
                   "_packed_pool")
 # utils/tracker.py:Tracker -- the fused query, the registration step and the tracking loop

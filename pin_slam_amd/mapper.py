@@ -303,12 +303,20 @@ class Mapper:
         if ds is None:
             return self.used_poses
         if getattr(c, "pgo_on", False):
-            return torch.tensor(np.array(ds.pgo_poses), device=self.device, dtype=torch.float64)
+            return self._poses_dev(ds.pgo_poses)
         if getattr(c, "track_on", False):
-            return torch.tensor(np.array(ds.odom_poses), device=self.device, dtype=torch.float64)
+            return self._poses_dev(ds.odom_poses)
         if getattr(ds, "gt_pose_provided", False):
-            return torch.tensor(np.array(ds.gt_poses), device=self.device, dtype=torch.float64)
+            return self._poses_dev(ds.gt_poses)
         return self.used_poses
+
+    def _poses_dev(self, poses):
+        """torch.tensor(np.array(poses), f64) on the device, copied from pinned memory without
+        waiting (a pageable copy drains the stream: one host wait per frame for a few KB)."""
+        a = torch.from_numpy(np.array(poses, dtype=np.float64))
+        if torch.device(self.device).type != "cuda":
+            return a.to(self.device)
+        return a.pin_memory().to(self.device, non_blocking=True)
 
     def process_frame(self, point_cloud_torch, frame_label_torch, cur_pose_torch, frame_id: int,
                       filter_dynamic: bool = False, draws=None):

@@ -584,40 +584,56 @@ class NeuralPoints(nn.Module):
         self._set_plain(dict(neural_points=self._append_rows("neural_points", self.neural_points, pts[new_rows[:k]])))
         if was_trusted:
             self._trust_table()
-        quat = torch.zeros((k, 4), dtype=self.dtype, device=dev)
-        quat[:, 0] = 1.0
-        ts = torch.full((k,), int(cur_ts), device=dev, dtype=torch.long)
-        new_fts = self.geo_feature_std * torch.randn(k + 1, self.geo_feature_dim, device=dev, dtype=self.dtype)
+        # the new rows' initial values written straight into the appended rows (no temporaries and
+        # copies): identity quaternions, the frame's ts, zero certainty, and padded features drawn
+        # as the reference draws them -- randn(k + 1, F) from the same generator, times the std
+        std, ts_val = self.geo_feature_std, int(cur_ts)
+
+        def quat(v):
+            v.zero_()
+            v[:, 0] = 1.0
+
+        def feats(v):
+            torch.randn(v.shape, out=v, dtype=self.dtype, device=dev)
+            v.mul_(std)
         self._set_plain(dict(
-            point_orientations=self._append_rows("point_orientations", self.point_orientations, quat),
-            point_ts_create=self._append_rows("point_ts_create", self.point_ts_create, ts),
-            point_ts_update=self._append_rows("point_ts_update", self.point_ts_update, ts),
-            geo_features=self._append_rows("geo_features", self.geo_features, new_fts, replace_last=True),
-            point_certainties=self._append_rows("point_certainties", self.point_certainties,
-                                                torch.zeros(k, device=dev, dtype=self.dtype))))
+            point_orientations=self._append_rows("point_orientations", self.point_orientations, None, fill=(k, quat)),
+            point_ts_create=self._append_rows("point_ts_create", self.point_ts_create, None,
+                                              fill=(k, lambda v: v.fill_(ts_val))),
+            point_ts_update=self._append_rows("point_ts_update", self.point_ts_update, None,
+                                              fill=(k, lambda v: v.fill_(ts_val))),
+            geo_features=self._append_rows("geo_features", self.geo_features, None, replace_last=True,
+                                           fill=(k + 1, feats)),
+            point_certainties=self._append_rows("point_certainties", self.point_certainties, None,
+                                                fill=(k, lambda v: v.zero_()))))
         self.reset_local_map(sensor_position, sensor_orientation, cur_ts)
 
-    def _append_rows(self, name, cur, new, replace_last=False):
+    def _append_rows(self, name, cur, new, replace_last=False, fill=None):
         """torch.cat((cur, new)) -- or torch.cat((cur[:-1], new)) with replace_last (the padding
         feature row) -- as a prefix view of a buffer with spare rows, written in place when cur is
         the view this method returned last time (anything else, e.g. an array a caller assigned,
         is copied once into a new buffer with 1.25x the rows).  The rows of cur are not touched,
-        except the padding row with replace_last, whose old tensor then gets a version bump."""
+        except the padding row with replace_last, whose old tensor then gets a version bump.
+        fill=(m, fn) instead of new: m rows of cur's dtype, written by fn(view of those rows)."""
         bufs = self.__dict__.setdefault("_row_bufs", {})
         buf, last = bufs.get(name, (None, None))
         n = cur.shape[0] - (1 if replace_last else 0)
-        m = new.shape[0]
-        dt = torch.promote_types(cur.dtype, new.dtype)
+        m = new.shape[0] if fill is None else int(fill[0])
+        dt = cur.dtype if fill is not None else torch.promote_types(cur.dtype, new.dtype)
+        dev = cur.device if fill is not None else new.device
         in_place = (buf is not None and last is not None and last() is cur and buf.dtype == dt
                     and buf.shape[1:] == cur.shape[1:] and buf.shape[0] >= n + m and cur.is_contiguous()
                     and (cur.shape[0] == 0 or cur.data_ptr() == buf.data_ptr()))
         if not in_place:
             rows = max(int((n + m) * 1.25), n + m, 1024)
-            buf = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
+            buf = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=dev)
             buf[:n] = cur[:n]
         elif replace_last:
             torch.autograd.graph.increment_version(cur)
-        buf[n:n + m] = new
+        if fill is None:
+            buf[n:n + m] = new
+        elif m > 0:
+            fill[1](buf[n:n + m])
         out = buf[:n + m]
         bufs[name] = (buf, weakref.ref(out))
         return out
