@@ -343,7 +343,6 @@ class Mapper:
             frame_label_torch = frame_label_torch[self.static_mask]
         coord, sdf_label, normal_label, sem_label, color_label, weight, global_coord = self.sampler.sample(
             frame_point, None, frame_label_torch, frame_color, pose=cur_pose_torch, draws=draws)   # :149-151
-        time_repeat = torch.full((coord.shape[0],), int(frame_id), dtype=torch.long, device=self.device)
         self.cur_sample_count = sdf_label.shape[0]
         self.pool_sample_count = self.sdf_label_pool.shape[0]
         sig_before = self._pool_signature() if self.global_coord_pool is not None else None
@@ -355,7 +354,10 @@ class Mapper:
         self.coord_pool = self._pool_append("coord", self.coord_pool, coord)
         self.weight_pool = self._pool_append("weight", self.weight_pool, weight)
         self.sdf_label_pool = self._pool_append("sdf_label", self.sdf_label_pool, sdf_label)
-        self.time_pool = self._pool_append("time", self.time_pool, time_repeat)
+        m_new, fid = coord.shape[0], int(frame_id)
+        self.time_pool = self._pool_append("time", self.time_pool, None,
+                                           fill=(m_new, torch.long, lambda v: v.fill_(fid)))
+        time_repeat = self.time_pool[self.time_pool.shape[0] - m_new:]   # torch.full((m,), frame_id)
         self.sem_label_pool = None if sem_label is None else (
             sem_label if self.sem_label_pool is None else self._pool_append(
                 "sem", self.sem_label_pool, sem_label.to(self.sem_label_pool.dtype)))
@@ -385,8 +387,9 @@ class Mapper:
         track = _PACK_POOL and self.__dict__.get("_pool_packed") is not None and sig_before is not None \
             and self.__dict__.get("_pool_packed_sig") == sig_before and self._pools_fusable()
         if track:
-            self._pool_packed = self._pool_append("packed", self._pool_packed,
-                                                  self._pack(global_coord, sdf_label, time_repeat, weight))
+            self._pool_packed = self._pool_append(
+                "packed", self._pool_packed, None,
+                fill=(m_new, torch.float32, lambda v: self._pack(global_coord, sdf_label, time_repeat, weight, out=v)))
         if (frame_id + 1) % int(c.pool_filter_freq) == 0:                                # :226-262
             # the sphere test, the kept-row list and both counts in one pass (pin_pool_window),
             # one host read for the counts; the origin keeps the pose's dtype (torch promotes the
@@ -469,14 +472,17 @@ class Mapper:
             return 0
         return int(getattr(c, "pool_capacity", 0)) + int(getattr(c, "pool_filter_freq", 1)) * m * 5 // 4
 
-    def _pool_append(self, name, cur, new):
+    def _pool_append(self, name, cur, new, fill=None):
         """torch.cat((cur, new)) as a prefix view of a buffer sized once for the steady-state pool
         (grown by 1.5x if ever full); cur must be the previous return value to be appended in
-        place (anything else is copied once)."""
+        place (anything else is copied once).  fill=(m, dtype, fn) instead of new: m rows of that
+        dtype, written by fn(view of the appended rows) (no temporary and copy)."""
         bufs = self.__dict__.setdefault("_pool_bufs", {})
         buf, last = bufs.get(name, (None, -1))
-        n, m = cur.shape[0], new.shape[0]
-        dt = torch.promote_types(cur.dtype, new.dtype)    # torch.cat's type promotion
+        n = cur.shape[0]
+        m = new.shape[0] if fill is None else int(fill[0])
+        dt = torch.promote_types(cur.dtype, new.dtype if fill is None else fill[1])   # torch.cat's promotion
+        dev = new.device if fill is None else cur.device
         # in place only when cur IS the view returned last time: a shorter prefix view (a
         # truncated pool) still references the rows past it, so it gets a fresh buffer
         in_place = (buf is not None and n == last and buf.dtype == dt and buf.shape[1:] == cur.shape[1:]
@@ -484,7 +490,7 @@ class Mapper:
                     and cur.is_contiguous())
         if not in_place:
             rows = max(int((n + m) * 1.5), 1024, self._pool_rows_hint(m))
-            nb = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=new.device)
+            nb = torch.empty((rows,) + tuple(cur.shape[1:]), dtype=dt, device=dev)
             nb[:n] = cur
             buf = nb
             # the window filter's compaction target, sized alike now rather than at the first
@@ -493,9 +499,12 @@ class Mapper:
             sp = spares.get(name)
             if sp is None or sp.shape[0] < rows or sp.dtype != dt or sp.shape[1:] != nb.shape[1:]:
                 spares[name] = torch.empty_like(nb)
-            if name == "global_coord" and new.is_cuda:   # the window filter's buffers, sized alike
-                self._window_buffers(rows, new.device)
-        buf[n:n + m] = new
+            if name == "global_coord" and dev.type == "cuda":   # the window filter's buffers, sized alike
+                self._window_buffers(rows, dev)
+        if fill is None:
+            buf[n:n + m] = new
+        elif m > 0:
+            fill[2](buf[n:n + m])
         bufs[name] = (buf, n + m)
         return buf[:n + m]
 
