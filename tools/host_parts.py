@@ -18,7 +18,8 @@ from pin_slam_amd.synthetic import FrameLoop, Q_SCALE, lidar_scan, slam_poses, s
 
 PARTS = ("frame", "read_and_preprocess", "update", "tracking", "process_frame", "mapping", "_dense_loop",
          "_step_plan", "reset_local_map", "query_certainty", "sample", "_build_occupancy", "grid_view",
-         "voxel_down_sample")
+         "voxel_down_sample", "_views", "_packed_pool", "_grid_view", "mlp_view", "_build_compact", "records",
+         "_batch_sizes", "draw_shapes", "run", "assign_local_to_global")
 
 
 def main(warm=10, n=16):
