@@ -30,7 +30,7 @@ import torch.distributed as dist
 
 from . import _lib
 from .data_sampler import DataSampler
-from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, query_sdf, query_sort
+from .query import _MLP_PACK, _TILE_MIN, _TILE_QUERIES, mlp_view, mlp_view_repacked, query_sdf, query_sort
 from .sharding import OwnerAdam, all_reduce
 
 # weighted_first with a training decoder: decode each row in the backward on the matrix cores
@@ -810,6 +810,8 @@ class Mapper:
             nm.mark_modified(feats)
             for p in mlp_params:
                 torch.autograd.graph.increment_version(p)
+            if mlp_params and plan.mv.struct.packed:   # the loop's Adam launches re-packed the image
+                mlp_view_repacked(self.geo_mlp, plan.mv.struct.packed)
             self.total_iter += iter_count
         if part is not None:
             part.reconcile_side_effects(cert_before, nm.local_point_certainties, nm.local_point_ts_update)

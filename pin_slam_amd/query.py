@@ -94,13 +94,34 @@ def mlp_view(decoder, packed=False) -> _View:
         # parameters in place, so it stays consistent with the image)
         buf = decoder.__dict__.get("_pin_mlp_pack_buf") if ps is not None else None
         if buf is None or buf.device != v.keep[0].device:
-            buf = torch.empty(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=v.keep[0].device)
+            # zeroed once: the image has padding bytes the pack never writes (images compare bytewise)
+            buf = torch.zeros(_lib.MLP_PACK_BYTES, dtype=torch.uint8, device=v.keep[0].device)
             if ps is not None:
                 decoder.__dict__["_pin_mlp_pack_buf"] = buf
         _lib.call("pin_mlp_pack", v.ref(), _lib.ptr(buf), _lib.stream(buf.device))
         v.struct.packed = buf.data_ptr()
         v.keep = v.keep + (buf,)
     return v
+
+
+def mlp_view_repacked(decoder, packed_ptr) -> bool:
+    """After a launch that stepped the decoder AND rewrote its operand image (the mapping loop's
+    pin_adam_step_train re-packs it, bitwise pin_mlp_pack's image): cache the view under the
+    parameters' new versions with that image attached, so the next mlp_view(packed=True) -- the
+    tracker's -- does not pack again.  False (nothing cached) unless packed_ptr is this decoder's
+    image buffer."""
+    buf = decoder.__dict__.get("_pin_mlp_pack_buf")
+    try:
+        ps = (decoder.layers[0].weight, decoder.layers[0].bias, decoder.lout.weight, decoder.lout.bias)
+    except (AttributeError, IndexError):
+        return False
+    if not _MLP_PACK or buf is None or buf.data_ptr() != packed_ptr or len(decoder.layers) != 1:
+        return False
+    v = _mlp_view(decoder)
+    v.struct.packed = buf.data_ptr()
+    v.keep = v.keep + (buf,)
+    decoder.__dict__["_pin_mlp_view"] = ((tensor_key(ps), float(decoder.sdf_scale)), v)
+    return True
 
 
 def _mlp_view(decoder) -> _View:

@@ -12,6 +12,7 @@ import torch
 
 import pin_slam_amd as P
 from pin_slam_amd import _lib
+from pin_slam_amd.query import tensor_key
 from tests import helpers as H
 
 pytestmark = pytest.mark.gpu
@@ -605,10 +606,18 @@ def test_decoder_image_sees_training_writes(dev):
     mapper.set_pool(coord, label, ts)
     mapper.mapping(3)
     assert max((p - w).abs().max().item() for p, w in zip(dec.parameters(), w0)) > 0   # the decoder moved
+    # the loop's last Adam launch re-packed the image: mapping() caches it under the new parameter
+    # versions (mlp_view_repacked), so this query does not pack again
+    hit = dec.__dict__.get("_pin_mlp_view")
+    assert hit is not None and hit[1].struct.packed == dec.__dict__["_pin_mlp_pack_buf"].data_ptr()
+    assert hit[0] == (tensor_key((dec.layers[0].weight, dec.layers[0].bias, dec.lout.weight, dec.lout.bias)),
+                      float(dec.sdf_scale))
     after = P.query_sdf(nm, dec, q, query_locally=True, want_grad=True)
     copy = P.Decoder(nm.config, 64, 1, 1)
     copy.load_state_dict(dec.state_dict())
     fresh = P.query_sdf(nm, copy, q, query_locally=True, want_grad=True)
+    # the cached image is byte for byte the fresh decoder's pin_mlp_pack image
+    assert torch.equal(dec.__dict__["_pin_mlp_pack_buf"], copy.__dict__["_pin_mlp_pack_buf"])
     assert not torch.equal(before[0], after[0])
     torch.testing.assert_close(after[0], fresh[0], rtol=0, atol=0)
     torch.testing.assert_close(after[1], fresh[1], rtol=0, atol=0)
